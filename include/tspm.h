@@ -1,0 +1,209 @@
+/*
+ * tspm.h — C ABI of the MI355X-native AVMNIST late-fusion training path (libtspm.so, gfx950).
+ *
+ * Drop-in boundary for the reference's hot path (TArsenii/task-specific-pretraining-multimodal,
+ * MML_Suite; paths below are relative to MML_Suite/).  The reference is pure Python/PyTorch: each
+ * entry point here replaces the ATen op family that the cited reference line dispatches.  The
+ * Python host side (task-specific-pretraining-multimodal_amd/_lib.py) binds these with ctypes —
+ * the stub a maintainer adds to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer unless stated otherwise; sizes are element counts.
+ *   - Activations are "HWNC": rows ordered (h, w, n), C contiguous fp32 per row.
+ *   - Conv weights are OHWI fp32 (the channels_last view of the reference's OIHW nn.Conv2d weight;
+ *     the state_dict keeps shape [O, I, H, W]).
+ *   - No entry point allocates, synchronises the host, or keeps mutable global state; workspace is
+ *     caller-provided (size queries provided).  Every call is enqueued on `stream` (a hipStream_t),
+ *     so calls are capturable into a hipGraph.
+ *   - Return value: TSPM_OK (0) or a TSPM_ERR_* code; nothing is launched on error.
+ */
+#ifndef TSPM_H_
+#define TSPM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* tspm_stream_t; /* hipStream_t */
+
+enum {
+  TSPM_OK = 0,
+  TSPM_ERR_INVALID = 1,   /* bad shape / null pointer / unsupported configuration */
+  TSPM_ERR_LAUNCH = 2,    /* the HIP launch failed (hipGetLastError != hipSuccess) */
+  TSPM_ERR_WORKSPACE = 3, /* caller-provided workspace too small */
+};
+
+/* Version of this ABI (bumped on any signature change). */
+int tspm_abi_version(void);
+/* Static string for a status code. */
+const char* tspm_status_string(int status);
+
+/* ------------------------------------------------------------------------------------------------
+ * Convolution (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32)
+ * Replaces nn.Conv2d forward / input-grad / weight-grad at models/msa/networks/resnet.py:25,30
+ * (3x3 s1/s2 p1), :137 (7x7 s2 p3 stem, Cin=1) and :176 (1x1 s2 downsample); no bias.
+ * ----------------------------------------------------------------------------------------------*/
+typedef struct tspm_conv_shape {
+  int32_t n, h, w, c;  /* input batch, height, width, channels */
+  int32_t k, r, s;     /* output channels, kernel height, kernel width */
+  int32_t stride, pad; /* symmetric stride / zero padding */
+  int32_t p, q;        /* output height, width (= (h + 2 pad - r) / stride + 1, ...) */
+} tspm_conv_shape;
+
+/* Tile / split configuration.  tm, tn: 32x32 MFMA tiles per wave along M (rows) and N (columns);
+ * wm * wn == 4 waves per 256-thread workgroup; splits: reduction split (>1 uses workspace slabs,
+ * combined deterministically in slab order).  All-zero fields select the built-in heuristic. */
+typedef struct tspm_conv_algo {
+  int32_t tm, tn, wm, wn, splits;
+} tspm_conv_algo;
+
+/* Element strides (n, h, w, c) of a conv input tensor.  HWNC tensors: {c, w*n*c, n*c, 1}.
+ * The reference's NCHW stem input [N,1,H,W] / [N,H,W]: {h*w, w, 1, 0}. */
+typedef struct tspm_strides4 {
+  int64_t sn, sh, sw, sc;
+} tspm_strides4;
+
+/* y[P,Q,N,K] = conv(x, w).  y is HWNC. */
+int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
+                  const tspm_strides4* x_strides, const float* w, float* y, void* workspace,
+                  size_t workspace_bytes, tspm_stream_t stream);
+size_t tspm_conv_fwd_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+
+/* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}. */
+int tspm_conv_dgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy,
+                    const float* w, float* dx, int32_t beta, void* workspace, size_t workspace_bytes,
+                    tspm_stream_t stream);
+size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+
+/* dw[K,R,S,C] (OHWI) = conv_weight_grad(x, dy[P,Q,N,K]); overwritten (zero_grad semantics). */
+int tspm_conv_wgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
+                    const tspm_strides4* x_strides, const float* dy, float* dw, void* workspace,
+                    size_t workspace_bytes, tspm_stream_t stream);
+size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+
+/* ------------------------------------------------------------------------------------------------
+ * BatchNorm2d, training mode (batch statistics over N*H*W, biased variance for normalisation,
+ * unbiased for running_var, momentum 0.1, eps 1e-5) — resnet.py:26,31,138,177.
+ * ----------------------------------------------------------------------------------------------*/
+/* Batch statistics of y[M,C] (M = N*H*W rows).  If nslab > 1, y holds nslab partial slabs
+ * (slab_stride elements apart) that are summed in slab order and written to y_out (the conv output
+ * used downstream); with nslab == 1, y_out may be NULL or == y.  Writes save_mean / save_invstd [C]
+ * and updates running_mean / running_var in place (if non-NULL).  Workspace: tspm_bn_stats_workspace. */
+int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab, int64_t slab_stride,
+                  float* y_out, float* running_mean, float* running_var, float momentum, float eps,
+                  float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
+                  tspm_stream_t stream);
+size_t tspm_bn_stats_workspace(int64_t m, int32_t c);
+
+/* out = act( gamma*(y-mean)*invstd + beta  [+ residual] ), act = ReLU if relu != 0.
+ * res_mode 0: no residual; 1: residual = res (raw tensor, same [M,C]); 2: residual =
+ * BN(res; res_mean, res_invstd, res_gamma, res_beta) — the downsample branch (resnet.py:47-52). */
+int tspm_bn_apply(int64_t m, int32_t c, const float* y, const float* mean, const float* invstd,
+                  const float* gamma, const float* beta, int32_t res_mode, const float* res,
+                  const float* res_mean, const float* res_invstd, const float* res_gamma,
+                  const float* res_beta, int32_t relu, float* out, tspm_stream_t stream);
+
+/* Eval-mode BN (running statistics) with the same fusion options. */
+int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* running_mean,
+                       const float* running_var, float eps, const float* gamma, const float* beta,
+                       int32_t res_mode, const float* res, const float* res_rmean, const float* res_rvar,
+                       const float* res_gamma, const float* res_beta, int32_t relu, float* out,
+                       tspm_stream_t stream);
+
+/* BN backward through  out = relu(BN(y) [+ BN2(y2)])  (y2 / second BN optional, may be NULL):
+ *   g' = g * (out > 0)  (out may be NULL: no ReLU)
+ *   dgamma = sum(g' * xhat), dbeta = sum(g')          (written, not accumulated)
+ *   dy  = gamma*invstd*(g' - dbeta/M - xhat*dgamma/M)
+ *   dy2 likewise for the second BN; if dres != NULL it receives g' (identity residual grad).
+ * Workspace: tspm_bn_bwd_workspace. */
+int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y,
+                const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                float* dy, const float* y2, const float* mean2, const float* invstd2,
+                const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres,
+                void* workspace, size_t workspace_bytes, tspm_stream_t stream);
+size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
+
+/* ------------------------------------------------------------------------------------------------
+ * Pooling — nn.MaxPool2d(3, 2, 1) (resnet.py:140,208) and AdaptiveAvgPool2d(1)+flatten (:149,215-216)
+ * ----------------------------------------------------------------------------------------------*/
+/* y[P,Q,N,C] = maxpool(x[H,W,N,C]); argmax tap (0..k*k-1, first max in row-major window order,
+ * as ATen's CPU kernel) stored in idx (uint8, same shape as y). */
+int tspm_maxpool_fwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
+                     int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, tspm_stream_t stream);
+/* dx = scatter of dy to the argmax positions (gather form, deterministic); dx overwritten. */
+int tspm_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
+                     int32_t p, int32_t q, const float* dy, const uint8_t* idx, float* dx,
+                     tspm_stream_t stream);
+/* y[N,C] = mean over the npos positions of x[npos,N,C] (HWNC). */
+int tspm_avgpool_fwd(int32_t npos, int32_t n, int32_t c, const float* x, float* y, tspm_stream_t stream);
+/* dx[npos,N,C] = dy[N,C] / npos (dy row stride ldy). */
+int tspm_avgpool_bwd(int32_t npos, int32_t n, int32_t c, const float* dy, int32_t ldy, float* dx,
+                     tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Linear layers — encoder fc (resnet.py:150,217) and the fusion head (models/avmnist.py:219-230,267)
+ * w is [out, in] row-major (nn.Linear layout).  ld* are row strides (elements).
+ * ----------------------------------------------------------------------------------------------*/
+/* y = act(x @ w^T + b) [* keep*scale]; relu != 0 applies ReLU; keep (uint8 [n,out], may be NULL)
+ * applies the dropout mask with scale 1/(1-p) (models/avmnist.py:219-230). */
+int tspm_linear_fwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* w,
+                    const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
+                    int32_t ldy, tspm_stream_t stream);
+/* dx = dy @ w  (dx overwritten). */
+int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,
+                         float* dx, int32_t ldx, tspm_stream_t stream);
+/* dw = dy^T @ x, db = sum_n dy (both overwritten). */
+int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx,
+                           const float* dy, int32_t ldy, float* dw, float* db, tspm_stream_t stream);
+/* In-place gradient masking through a ReLU(+dropout) output y: g = (y > 0) ? g * scale : 0
+ * (scale = 1/(1-p) when y is the post-dropout output — y > 0 implies the unit was kept). */
+int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,
+                 tspm_stream_t stream);
+
+/* Dropout keep mask (uint8) from a counter-based hash RNG: keep[i] = u(seed, ctr, i) >= p, where
+ * ctr is read from device memory (*counter) so graph replays draw fresh masks. */
+int tspm_dropout_mask(int64_t count, float p, uint64_t seed, const uint64_t* counter, uint8_t* keep,
+                      tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Loss — LossFunctionGroup{cross_entropy: 1.0} (experiment_utils/loss.py:123-148,
+ * models/avmnist.py:301) + on-device accuracy counters (avmnist.py:305-309)
+ * ----------------------------------------------------------------------------------------------*/
+/* loss[0] = mean_i CE(logits_i, labels_i); dlogits = (softmax - onehot)/n * grad_scale;
+ * if stats != NULL: stats[0] += loss*n, stats[1] += #correct (argmax == label), stats[2] += n. */
+int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const int64_t* labels, float* loss,
+                       float* dlogits, float grad_scale, float* stats, tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Adam — torch.optim.Adam (L2 weight decay folded into the gradient) as instantiated by
+ * config/optimizer_config.py:199-226 with lr 5e-4, wd 1e-4 (train_avmnist_resnet.yaml)
+ * ----------------------------------------------------------------------------------------------*/
+typedef struct tspm_adam_hyper {
+  /* doubles, like torch.optim.Adam's Python-float hyper-parameters: 1-beta2 and the bias
+   * corrections are formed in double and rounded to fp32 once, as ATen does */
+  double lr, beta1, beta2, eps, weight_decay, grad_scale; /* grad_scale multiplies g (e.g. 1/world) */
+  int64_t step;                                          /* incremented on device by tspm_adam_begin */
+  int64_t pad_;
+} tspm_adam_hyper;
+/* hyper->step += 1 (device-side, so a captured graph advances the bias correction per replay). */
+int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream);
+/* One fused Adam update over `count` contiguous fp32 elements (the flat parameter buffer). */
+int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   const tspm_adam_hyper* hyper, tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Layout / data-stage helpers (collate → device, MML_Suite/data/avmnist.py:186-191,248-277)
+ * ----------------------------------------------------------------------------------------------*/
+/* image_f32[i] = lut[u8[i]] * (1/255)  (gist_earth→L colormap LUT, torchvision ToDtype(scale)). */
+int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* lut, float* out, tspm_stream_t stream);
+/* Sum `nslab` slabs of `count` floats (slab_stride apart) into out (deterministic slab order). */
+int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs, float* out,
+                      tspm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSPM_H_ */

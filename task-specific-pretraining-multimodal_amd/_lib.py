@@ -1,0 +1,149 @@
+"""ctypes binding of libtspm.so (the C ABI declared in ``include/tspm.h``).
+
+This is the "reference-side binding" of the drop-in boundary: plain device pointers, sizes and a
+hipStream_t cross the ABI; PyTorch only supplies device memory and the current stream.  The library
+is loaded lazily and every call checks its status code — there is no fallback: a missing or broken
+library raises ``TspmLibraryError`` (the product path never silently runs on ATen or the CPU).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, Structure, c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
+ABI_VERSION = 2
+
+
+class TspmLibraryError(RuntimeError):
+    pass
+
+
+class TspmError(RuntimeError):
+    pass
+
+
+class ConvShape(Structure):
+    _fields_ = [(n, c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "p", "q")]
+
+
+class ConvAlgo(Structure):
+    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wm", "wn", "splits")]
+
+
+class Strides4(Structure):
+    _fields_ = [(n, c_int64) for n in ("sn", "sh", "sw", "sc")]
+
+
+class AdamHyper(Structure):
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("grad_scale", ctypes.c_double),
+                ("step", c_int64), ("pad_", c_int64)]
+
+HYPER_STEP_OFFSET = 48  # byte offset of tspm_adam_hyper.step
+
+
+# name -> (restype, argtypes)
+_P = c_void_p
+_SIGS = {
+    "tspm_abi_version": (c_int32, []),
+    "tspm_status_string": (ctypes.c_char_p, [c_int32]),
+    "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, c_size_t, _P]),
+    "tspm_conv_fwd_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_dgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, _P, _P, c_int32, _P, c_size_t, _P]),
+    "tspm_conv_dgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_wgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, c_size_t, _P]),
+    "tspm_conv_wgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_bn_stats": (c_int32, [c_int64, c_int32, _P, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P,
+                                c_size_t, _P]),
+    "tspm_bn_stats_workspace": (c_size_t, [c_int64, c_int32]),
+    "tspm_bn_apply": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P]),
+    "tspm_bn_apply_eval": (c_int32, [c_int64, c_int32, _P, _P, _P, c_float, _P, _P, c_int32, _P, _P, _P, _P, _P,
+                                     c_int32, _P, _P]),
+    "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                              _P, c_size_t, _P]),
+    "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
+    "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
+    "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
+    "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),
+    "tspm_avgpool_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P]),
+    "tspm_linear_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, c_float, _P, c_int32, _P]),
+    "tspm_linear_bwd_data": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P]),
+    "tspm_linear_bwd_weight": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P]),
+    "tspm_act_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, c_float, _P]),
+    "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
+    "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
+    "tspm_adam_begin": (c_int32, [_P, _P]),
+    "tspm_adam_step": (c_int32, [c_int64, _P, _P, _P, _P, _P, _P]),
+    "tspm_image_lut": (c_int32, [c_int64, _P, _P, _P, _P]),
+    "tspm_reduce_slabs": (c_int32, [c_int64, c_int32, c_int64, _P, _P, _P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: Optional[str] = None):
+    """Load libtspm.so (import torch first so the process shares torch's HIP runtime)."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise TspmLibraryError(
+                f"libtspm.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or `make -C task-specific-pretraining-multimodal_amd/csrc`). There is no fallback path.")
+        try:
+            lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - environment specific
+            raise TspmLibraryError(f"failed to load {p}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)  # AttributeError -> missing export = broken build
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.tspm_abi_version()
+        if v != ABI_VERSION:
+            raise TspmLibraryError(f"libtspm ABI version {v} != expected {ABI_VERSION}")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().tspm_status_string(status).decode()
+        raise TspmError(f"{what} failed: {msg} (status {status})")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream: Optional[torch.cuda.Stream] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def require_cuda_f32(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise TspmError(f"{name} must be a ROCm device tensor (got {t.device}); the HIP path has no CPU fallback")
+    if t.dtype != torch.float32:
+        raise TspmError(f"{name} must be float32 (got {t.dtype})")
+
+
+def hwnc_strides(n: int, h: int, w: int, c: int) -> Strides4:
+    return Strides4(c, w * n * c, n * c, 1)

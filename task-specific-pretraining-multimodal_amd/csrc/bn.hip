@@ -1,0 +1,417 @@
+// BatchNorm2d (training + eval) forward/backward for HWNC activations — HBM-bound kernels.
+//
+// Replaces nn.BatchNorm2d at MML_Suite/models/msa/networks/resnet.py:26,31,138,177 together with the
+// ReLU (:27,42,52,139) and the residual add (:51) that follow it.
+//
+// Statistics: each workgroup computes its rows' mean and sum of squared deviations in two passes
+// (the second from L2), and a per-channel finalisation merges them in double in block order
+// (deterministic).  No E[y^2] - E[y]^2 cancellation — the audio stem produces |y| ~ 1e8 and border
+// positions of tiny feature maps sit many standard deviations from the channel mean.
+#include "common.h"
+
+namespace {
+
+constexpr int kElemsPerBlock = 16384;
+
+int stats_blocks(long long m, int c) {
+  long long g = cdiv64(m * c, kElemsPerBlock);
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  if (g > m) g = m;
+  return (int)g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward statistics: per-workgroup two-pass (block mean, then sum of squared deviations from it —
+// the second pass re-reads the block's rows from L2), merged across workgroups with Chan's formula
+// in double.  Numerically as good as ATen's two-pass CPU kernel even when the channel mean is many
+// standard deviations away from any single sample (border positions of 1x3 / 2x2 feature maps).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_stats_partial(long long M, int C, const float* __restrict__ y,
+                                                          int nslab, long long slab_stride, float* __restrict__ y_out,
+                                                          long long rows_per_block, float* __restrict__ part) {
+  __shared__ f32x4 sh[256];
+  __shared__ f32x4 smean[256];
+  const int L = C >> 2;            // threads per row
+  const int RP = 256 / L;          // rows per pass
+  const int t = threadIdx.x;
+  const int c4 = t % L, rg = t / L;
+  const long long r_begin = blockIdx.x * rows_per_block;
+  const long long r_end = min(M, r_begin + rows_per_block);
+  const float inv_n = 1.0f / (float)(r_end - r_begin);
+  auto load = [&](long long off) -> f32x4 {
+    f32x4 v = ld4(y + off);
+    for (int z = 1; z < nslab; ++z) v += ld4(y + z * slab_stride + off);
+    return v;
+  };
+  // pass 1: block sums shifted by the block's first row K (an exact data value), so the fp32 sum
+  // carries the spread of the data, not its offset (channels can sit at 1e7 with a spread of 1e-2)
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 K = load(r_begin * C + 4 * c4);
+  if (rg < RP) {
+    for (long long row = r_begin + rg; row < r_end; row += RP) {
+      const long long off = row * C + 4 * c4;
+      const f32x4 v = load(off);
+      if (nslab > 1) st4(y_out + off, v);
+      s1 += v - K;
+    }
+  }
+  sh[t] = s1;
+  __syncthreads();
+  if (rg == 0) {
+    for (int k = 1; k < RP; ++k) s1 += sh[k * L + c4];
+    smean[c4] = s1 * inv_n;  // block mean minus K (small)
+  }
+  __syncthreads();
+  // pass 2 (rows are L2-resident): d = (v - K) - off; mean_b = K + off + sum(d)/n and
+  // M2_b = sum(d^2) - sum(d)^2/n (corrected two-pass; the final correction in double)
+  f32x4 s2 = {0.f, 0.f, 0.f, 0.f}, sd = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 off = smean[c4];
+  if (rg < RP) {
+    for (long long row = r_begin + rg; row < r_end; row += RP) {
+      const f32x4 d = (load(row * C + 4 * c4) - K) - off;
+      sd += d;
+      s2 += d * d;
+    }
+  }
+  __shared__ f32x4 sh2[256];
+  sh[t] = sd;
+  sh2[t] = s2;
+  __syncthreads();
+  if (rg == 0) {
+    for (int k = 1; k < RP; ++k) { sd += sh[k * L + c4]; s2 += sh2[k * L + c4]; }
+    const double n = (double)(r_end - r_begin);
+    f32x4 lo, m2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo[j] = (float)((double)off[j] + (double)sd[j] / n);
+      m2[j] = (float)((double)s2[j] - (double)sd[j] * (double)sd[j] / n);
+    }
+    const long long G = gridDim.x;
+    st4(part + (long long)blockIdx.x * C + 4 * c4, K);
+    st4(part + (G + blockIdx.x) * C + 4 * c4, lo);
+    st4(part + (2 * G + blockIdx.x) * C + 4 * c4, m2);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_stats_final(long long M, int C, int G, long long rows_per_block,
+                                                        const float* __restrict__ part, float* __restrict__ rmean,
+                                                        float* __restrict__ rvar, float momentum, float eps,
+                                                        float* __restrict__ smean, float* __restrict__ sinv) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  // Chan et al. pairwise-free merge in block order: (n, mean, M2) += (n_b, mean_b, M2_b)
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int g = 0; g < G; ++g) {
+    const double nb = (double)min(rows_per_block, M - (long long)g * rows_per_block);
+    const double mb = (double)part[(long long)g * C + c] + (double)part[((long long)G + g) * C + c];
+    const double m2b = (double)part[(2LL * G + g) * C + c];
+    const double tot = n + nb;
+    const double delta = mb - mean;
+    mean += delta * (nb / tot);
+    m2 += m2b + delta * delta * (n * nb / tot);
+    n = tot;
+  }
+  double var = m2 / n;
+  if (var < 0.0) var = 0.0;
+  const float fmean = (float)mean, fvar = (float)var;
+  smean[c] = fmean;
+  sinv[c] = 1.0f / sqrtf(fvar + eps);
+  if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
+  if (rvar) {
+    const float unb = M > 1 ? (float)(m2 / (n - 1.0)) : fvar;
+    rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// apply: out = act(y*scale + shift [+ res | + res*scale2 + shift2])
+// ------------------------------------------------------------------------------------------------
+template <int RES, bool RELU, bool EVAL>
+__global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const float* __restrict__ y,
+                                                  const float* __restrict__ mean, const float* __restrict__ inv,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  const float* __restrict__ res, const float* __restrict__ mean2,
+                                                  const float* __restrict__ inv2, const float* __restrict__ gamma2,
+                                                  const float* __restrict__ beta2, float eps, float* __restrict__ out) {
+  const int L = C >> 2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    f32x4 mu = ld4(mean + 4 * c4), iv = ld4(inv + 4 * c4);
+    if (EVAL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) iv[j] = 1.0f / sqrtf(iv[j] + eps);
+    }
+    const f32x4 sc = ld4(gamma + 4 * c4) * iv;
+    const f32x4 sf = ld4(beta + 4 * c4) - mu * sc;
+    f32x4 v = ld4(y + 4 * i);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaf(v[j], sc[j], sf[j]);
+    if (RES == 1) {
+      o += ld4(res + 4 * i);
+    } else if (RES == 2) {
+      f32x4 mu2 = ld4(mean2 + 4 * c4), iv2 = ld4(inv2 + 4 * c4);
+      if (EVAL) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) iv2[j] = 1.0f / sqrtf(iv2[j] + eps);
+      }
+      const f32x4 sc2 = ld4(gamma2 + 4 * c4) * iv2;
+      const f32x4 sf2 = ld4(beta2 + 4 * c4) - mu2 * sc2;
+      const f32x4 v2 = ld4(res + 4 * i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += fmaf(v2[j], sc2[j], sf2[j]);
+    }
+    if (RELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    st4(out + 4 * i, o);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward: partial sums of g', g'*(y-mean) [, g'*(y2-mean2)]
+// ------------------------------------------------------------------------------------------------
+template <bool HAS_OUT, bool TWO>
+__global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
+                                                        const float* __restrict__ out, const float* __restrict__ y,
+                                                        const float* __restrict__ mean, const float* __restrict__ y2,
+                                                        const float* __restrict__ mean2, long long rows_per_block,
+                                                        float* __restrict__ part) {
+  __shared__ f32x4 sh[3][256];
+  const int L = C >> 2, RP = 256 / L;
+  const int t = threadIdx.x;
+  const int c4 = t % L, rg = t / L;
+  const long long r_begin = blockIdx.x * rows_per_block;
+  const long long r_end = min(M, r_begin + rows_per_block);
+  f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sx = sg, sx2 = sg;
+  if (rg < RP) {
+    const f32x4 mu = ld4(mean + 4 * c4);
+    const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (long long row = r_begin + rg; row < r_end; row += RP) {
+      const long long off = row * C + 4 * c4;
+      f32x4 gv = ld4(g + off);
+      if (HAS_OUT) {
+        const f32x4 ov = ld4(out + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gv[j] = ov[j] > 0.f ? gv[j] : 0.f;
+      }
+      sg += gv;
+      sx += gv * (ld4(y + off) - mu);
+      if (TWO) sx2 += gv * (ld4(y2 + off) - mu2);
+    }
+  }
+  sh[0][t] = sg;
+  sh[1][t] = sx;
+  if (TWO) sh[2][t] = sx2;
+  __syncthreads();
+  if (rg == 0) {
+    for (int k = 1; k < RP; ++k) {
+      sg += sh[0][k * L + c4];
+      sx += sh[1][k * L + c4];
+      if (TWO) sx2 += sh[2][k * L + c4];
+    }
+    const long long G = gridDim.x;
+    st4(part + (long long)blockIdx.x * C + 4 * c4, sg);
+    st4(part + (G + blockIdx.x) * C + 4 * c4, sx);
+    if (TWO) st4(part + (2 * G + blockIdx.x) * C + 4 * c4, sx2);
+  }
+}
+
+// coef layout [6][C]: ca, cb, cm (first BN), ca2, cb2, cm2 (second BN)
+__global__ __launch_bounds__(256) void k_bn_bwd_final(long long M, int C, int G, int two, const float* __restrict__ part,
+                                                      const float* __restrict__ inv, const float* __restrict__ gamma,
+                                                      const float* __restrict__ inv2, const float* __restrict__ gamma2,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                      float* __restrict__ dgamma2, float* __restrict__ dbeta2,
+                                                      float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sx = 0.0, sx2 = 0.0;
+  for (int g = 0; g < G; ++g) {
+    sg += (double)part[(long long)g * C + c];
+    sx += (double)part[((long long)G + g) * C + c];
+    if (two) sx2 += (double)part[(2LL * G + g) * C + c];
+  }
+  const double n = (double)M;
+  {
+    const double iv = inv[c], ga = gamma[c];
+    const double dg = sx * iv;
+    if (dgamma) dgamma[c] = (float)dg;
+    if (dbeta) dbeta[c] = (float)sg;
+    const double ca = ga * iv;
+    coef[c] = (float)ca;
+    coef[C + c] = (float)(ca * iv * dg / n);
+    coef[2 * C + c] = (float)(ca * sg / n);
+  }
+  if (two) {
+    const double iv = inv2[c], ga = gamma2[c];
+    const double dg = sx2 * iv;
+    if (dgamma2) dgamma2[c] = (float)dg;
+    if (dbeta2) dbeta2[c] = (float)sg;
+    const double ca = ga * iv;
+    coef[3 * C + c] = (float)ca;
+    coef[4 * C + c] = (float)(ca * iv * dg / n);
+    coef[5 * C + c] = (float)(ca * sg / n);
+  }
+}
+
+template <bool HAS_OUT, bool TWO, bool DRES>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(long long n4, int C, const float* __restrict__ g,
+                                                      const float* __restrict__ out, const float* __restrict__ y,
+                                                      const float* __restrict__ mean, const float* __restrict__ y2,
+                                                      const float* __restrict__ mean2, const float* __restrict__ coef,
+                                                      float* __restrict__ dy, float* __restrict__ dy2,
+                                                      float* __restrict__ dres) {
+  const int L = C >> 2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    f32x4 gv = ld4(g + 4 * i);
+    if (HAS_OUT) {
+      const f32x4 ov = ld4(out + 4 * i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[j] = ov[j] > 0.f ? gv[j] : 0.f;
+    }
+    {
+      const f32x4 ca = ld4(coef + 4 * c4), cb = ld4(coef + C + 4 * c4), cm = ld4(coef + 2 * C + 4 * c4);
+      const f32x4 d = ld4(y + 4 * i) - ld4(mean + 4 * c4);
+      st4(dy + 4 * i, ca * gv - cm - cb * d);
+    }
+    if (TWO) {
+      const f32x4 ca = ld4(coef + 3 * C + 4 * c4), cb = ld4(coef + 4 * C + 4 * c4), cm = ld4(coef + 5 * C + 4 * c4);
+      const f32x4 d = ld4(y2 + 4 * i) - ld4(mean2 + 4 * c4);
+      st4(dy2 + 4 * i, ca * gv - cm - cb * d);
+    }
+    if (DRES) st4(dres + 4 * i, gv);
+  }
+}
+
+int ew_blocks(long long n4) {
+  long long b = cdiv64(n4, 256);
+  if (b > 2048) b = 2048;
+  return (int)(b < 1 ? 1 : b);
+}
+
+bool c_ok(int C) { return C >= 4 && C % 4 == 0 && C <= 1024; }
+
+}  // namespace
+
+extern "C" size_t tspm_bn_stats_workspace(int64_t m, int32_t c) {
+  if (m <= 0 || !c_ok(c)) return 0;
+  return (size_t)3 * stats_blocks(m, c) * c * sizeof(float);
+}
+
+extern "C" int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab, int64_t slab_stride, float* y_out,
+                             float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                             float* save_invstd, void* ws, size_t ws_bytes, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || !y || nslab < 1 || !save_mean || !save_invstd) return TSPM_ERR_INVALID;
+  if (nslab > 1 && !y_out) return TSPM_ERR_INVALID;
+  if (!ws || ws_bytes < tspm_bn_stats_workspace(m, c)) return TSPM_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int G = stats_blocks(m, c);
+  const long long rpb = cdiv64(m, G);
+  const int Greal = (int)cdiv64(m, rpb);
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(k_bn_stats_partial, dim3(Greal), dim3(256), 0, st, (long long)m, c, y, nslab,
+                     (long long)slab_stride, y_out, rpb, part);
+  TSPM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bn_stats_final, dim3(cdiv(c, 256)), dim3(256), 0, st, (long long)m, c, Greal, rpb, part,
+                     running_mean, running_var, momentum, eps, save_mean, save_invstd);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+#define BN_APPLY_LAUNCH(RES, RELU, EVAL)                                                                   \
+  hipLaunchKernelGGL((k_bn_apply<RES, RELU, EVAL>), dim3(ew_blocks(n4)), dim3(256), 0, st, n4, c, y, mean, \
+                     inv, gamma, beta, res, mean2, inv2, gamma2, beta2, eps, out)
+
+static int bn_apply_common(int64_t m, int32_t c, const float* y, const float* mean, const float* inv,
+                           const float* gamma, const float* beta, int32_t res_mode, const float* res,
+                           const float* mean2, const float* inv2, const float* gamma2, const float* beta2,
+                           int32_t relu, float* out, bool eval, float eps, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || !y || !mean || !inv || !gamma || !beta || !out) return TSPM_ERR_INVALID;
+  if (res_mode < 0 || res_mode > 2) return TSPM_ERR_INVALID;
+  if (res_mode >= 1 && !res) return TSPM_ERR_INVALID;
+  if (res_mode == 2 && (!mean2 || !inv2 || !gamma2 || !beta2)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const long long n4 = (long long)m * c / 4;
+  const bool r = relu != 0;
+  if (!eval) {
+    if (res_mode == 0) { if (r) BN_APPLY_LAUNCH(0, true, false); else BN_APPLY_LAUNCH(0, false, false); }
+    else if (res_mode == 1) { if (r) BN_APPLY_LAUNCH(1, true, false); else BN_APPLY_LAUNCH(1, false, false); }
+    else { if (r) BN_APPLY_LAUNCH(2, true, false); else BN_APPLY_LAUNCH(2, false, false); }
+  } else {
+    if (res_mode == 0) { if (r) BN_APPLY_LAUNCH(0, true, true); else BN_APPLY_LAUNCH(0, false, true); }
+    else if (res_mode == 1) { if (r) BN_APPLY_LAUNCH(1, true, true); else BN_APPLY_LAUNCH(1, false, true); }
+    else { if (r) BN_APPLY_LAUNCH(2, true, true); else BN_APPLY_LAUNCH(2, false, true); }
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn_apply(int64_t m, int32_t c, const float* y, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int32_t res_mode, const float* res,
+                             const float* res_mean, const float* res_invstd, const float* res_gamma,
+                             const float* res_beta, int32_t relu, float* out, tspm_stream_t stream) {
+  return bn_apply_common(m, c, y, mean, invstd, gamma, beta, res_mode, res, res_mean, res_invstd, res_gamma,
+                         res_beta, relu, out, false, 0.f, stream);
+}
+
+extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* running_mean,
+                                  const float* running_var, float eps, const float* gamma, const float* beta,
+                                  int32_t res_mode, const float* res, const float* res_rmean, const float* res_rvar,
+                                  const float* res_gamma, const float* res_beta, int32_t relu, float* out,
+                                  tspm_stream_t stream) {
+  return bn_apply_common(m, c, y, running_mean, running_var, gamma, beta, res_mode, res, res_rmean, res_rvar,
+                         res_gamma, res_beta, relu, out, true, eps, stream);
+}
+
+extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
+  if (m <= 0 || !c_ok(c)) return 0;
+  return ((size_t)3 * stats_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
+}
+
+extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y, const float* mean,
+                           const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dy,
+                           const float* y2, const float* mean2, const float* invstd2, const float* gamma2,
+                           float* dgamma2, float* dbeta2, float* dy2, float* dres, void* ws, size_t ws_bytes,
+                           tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || !g || !y || !mean || !invstd || !gamma || !dy) return TSPM_ERR_INVALID;
+  const bool two = y2 != nullptr;
+  if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
+  if (!ws || ws_bytes < tspm_bn_bwd_workspace(m, c)) return TSPM_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int G = stats_blocks(m, c);
+  const long long rpb = cdiv64(m, G);
+  const int Greal = (int)cdiv64(m, rpb);
+  float* part = static_cast<float*>(ws);
+  float* coef = part + (size_t)3 * G * c;
+  const bool ho = out != nullptr;
+#define BNB_P(HO, TW)                                                                                           \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW>), dim3(Greal), dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
+                     y2, mean2, rpb, part)
+  if (ho) { if (two) BNB_P(true, true); else BNB_P(true, false); }
+  else { if (two) BNB_P(false, true); else BNB_P(false, false); }
+#undef BNB_P
+  TSPM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 256)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
+                     invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, coef);
+  TSPM_LAUNCH_CHECK();
+  const long long n4 = (long long)m * c / 4;
+  const int nb = ew_blocks(n4);
+  const bool dr = dres != nullptr;
+#define BNB_A(HO, TW, DR)                                                                                          \
+  hipLaunchKernelGGL((k_bn_bwd_apply<HO, TW, DR>), dim3(nb), dim3(256), 0, st, n4, c, g, out, y, mean, y2, mean2, \
+                     coef, dy, dy2, dres)
+  if (ho) {
+    if (two) { if (dr) BNB_A(true, true, true); else BNB_A(true, true, false); }
+    else { if (dr) BNB_A(true, false, true); else BNB_A(true, false, false); }
+  } else {
+    if (two) { if (dr) BNB_A(false, true, true); else BNB_A(false, true, false); }
+    else { if (dr) BNB_A(false, false, true); else BNB_A(false, false, false); }
+  }
+#undef BNB_A
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}

@@ -1,0 +1,305 @@
+// Fusion head (Linear/ReLU/Dropout, MML_Suite/models/avmnist.py:219-230,267), encoder fc
+// (resnet.py:150,217), cross-entropy (experiment_utils/loss.py:123-148), Adam (torch.optim.Adam as
+// built at config/optimizer_config.py:199-226) and the image colormap LUT (data/avmnist.py:186-191).
+#include "common.h"
+
+namespace {
+
+int grid_for(long long work) {
+  long long b = cdiv64(work, 256);
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// y[n,o] = act(x[n,:] . w[o,:] + b[o]) * keep-scale
+__global__ __launch_bounds__(256) void k_linear_fwd(int N, int IN, int OUT, const float* __restrict__ x, int ldx,
+                                                    const float* __restrict__ w, const float* __restrict__ b,
+                                                    int relu, const uint8_t* __restrict__ keep, float kscale,
+                                                    float* __restrict__ y, int ldy) {
+  const long long total = (long long)N * OUT;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int o = (int)(i % OUT), n = (int)(i / OUT);
+    const float* xr = x + (long long)n * ldx;
+    const float* wr = w + (long long)o * IN;
+    float s = 0.f;
+    if ((IN & 3) == 0 && (ldx & 3) == 0) {
+      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < IN; k += 4) s4 += ld4(xr + k) * ld4(wr + k);
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    } else {
+      for (int k = 0; k < IN; ++k) s = fmaf(xr[k], wr[k], s);
+    }
+    if (b) s += b[o];
+    if (relu) s = fmaxf(s, 0.f);
+    if (keep) s = keep[(long long)n * OUT + o] ? s * kscale : 0.f;
+    y[(long long)n * ldy + o] = s;
+  }
+}
+
+// dx[n,i] = sum_o dy[n,o] w[o,i]
+__global__ __launch_bounds__(256) void k_linear_bwd_data(int N, int IN, int OUT, const float* __restrict__ dy,
+                                                         int ldy, const float* __restrict__ w, float* __restrict__ dx,
+                                                         int ldx) {
+  const long long total = (long long)N * IN;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int i = (int)(t % IN), n = (int)(t / IN);
+    const float* g = dy + (long long)n * ldy;
+    float s = 0.f;
+    for (int o = 0; o < OUT; ++o) s = fmaf(g[o], w[(long long)o * IN + i], s);
+    dx[(long long)n * ldx + i] = s;
+  }
+}
+
+// dw[o,i] = sum_n dy[n,o] x[n,i];  db[o] = sum_n dy[n,o]
+__global__ __launch_bounds__(256) void k_linear_bwd_weight(int N, int IN, int OUT, const float* __restrict__ x, int ldx,
+                                                           const float* __restrict__ dy, int ldy,
+                                                           float* __restrict__ dw, float* __restrict__ db) {
+  const long long total = (long long)OUT * IN;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int i = (int)(t % IN), o = (int)(t / IN);
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s = fmaf(dy[(long long)n * ldy + o], x[(long long)n * ldx + i], s);
+    dw[t] = s;
+    if (db && i == 0) {
+      float sb = 0.f;
+      for (int n = 0; n < N; ++n) sb += dy[(long long)n * ldy + o];
+      db[o] = sb;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_act_bwd(int N, int COLS, float* __restrict__ g, int ldg,
+                                                 const float* __restrict__ y, int ldy, float scale) {
+  const long long total = (long long)N * COLS;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int c = (int)(t % COLS), n = (int)(t / COLS);
+    float* gp = g + (long long)n * ldg + c;
+    *gp = y[(long long)n * ldy + c] > 0.f ? *gp * scale : 0.f;
+  }
+}
+
+// counter-based RNG (splitmix64 finaliser over seed/counter/index)
+TSPM_DEV uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_dropout_mask(long long count, float p, uint64_t seed,
+                                                      const uint64_t* __restrict__ ctr, uint8_t* __restrict__ keep) {
+  const uint64_t c = ctr ? *ctr : 0ULL;
+  const uint64_t base = mix64(seed ^ mix64(c + 0x9e3779b97f4a7c15ULL));
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < count; i += (long long)gridDim.x * 256) {
+    const uint64_t h = mix64(base + (uint64_t)i * 0x9e3779b97f4a7c15ULL);
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    keep[i] = u >= p ? 1 : 0;
+  }
+}
+
+// one workgroup; rows strided over threads; deterministic tree reduction in double
+__global__ __launch_bounds__(256) void k_cross_entropy(int N, int K, const float* __restrict__ logits,
+                                                       const int64_t* __restrict__ labels, float* __restrict__ loss,
+                                                       float* __restrict__ dlogits, float gscale,
+                                                       float* __restrict__ stats) {
+  __shared__ double sl[256];
+  __shared__ int sc[256];
+  double lsum = 0.0;
+  int correct = 0;
+  const float invn = 1.0f / (float)N;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float* z = logits + (long long)n * K;
+    float mx = z[0];
+    int am = 0;
+    for (int k = 1; k < K; ++k)
+      if (z[k] > mx) { mx = z[k]; am = k; }
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += expf(z[k] - mx);
+    const float lse = logf(se);
+    const int lab = (int)labels[n];
+    lsum += (double)(lse - (z[lab] - mx));
+    correct += (am == lab) ? 1 : 0;
+    if (dlogits) {
+      float* d = dlogits + (long long)n * K;
+      for (int k = 0; k < K; ++k) {
+        const float pk = expf(z[k] - mx) / se;
+        d[k] = (pk - (k == lab ? 1.f : 0.f)) * invn * gscale;
+      }
+    }
+  }
+  sl[threadIdx.x] = lsum;
+  sc[threadIdx.x] = correct;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) { sl[threadIdx.x] += sl[threadIdx.x + s]; sc[threadIdx.x] += sc[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float l = (float)(sl[0] / (double)N);
+    if (loss) loss[0] = l;
+    if (stats) {
+      stats[0] += (float)sl[0];
+      stats[1] += (float)sc[0];
+      stats[2] += (float)N;
+    }
+  }
+}
+
+__global__ void k_adam_begin(tspm_adam_hyper* h) { h->step += 1; }
+
+__global__ __launch_bounds__(256) void k_adam(long long count, float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              const tspm_adam_hyper* __restrict__ hp) {
+  __shared__ float sh[8];
+  if (threadIdx.x == 0) {
+    const tspm_adam_hyper h = *hp;
+    const double bc1 = 1.0 - pow(h.beta1, (double)h.step);
+    const double bc2 = 1.0 - pow(h.beta2, (double)h.step);
+    sh[0] = (float)(h.lr / bc1);          // step_size
+    sh[1] = (float)sqrt(bc2);             // bias_correction2_sqrt
+    sh[2] = (float)(1.0 - h.beta1);       // lerp weight
+    sh[3] = (float)h.beta2;
+    sh[4] = (float)(1.0 - h.beta2);
+    sh[5] = (float)h.eps;
+    sh[6] = (float)h.weight_decay;
+    sh[7] = (float)h.grad_scale;
+  }
+  __syncthreads();
+  const float step_size = sh[0], bc2s = sh[1], w1 = sh[2], b2 = sh[3], omb2 = sh[4], eps = sh[5], wd = sh[6],
+              gs = sh[7];
+  auto upd = [&](float& pp, float gg, float& mm, float& vv) {
+    gg = gg * gs;
+    if (wd != 0.f) gg = gg + wd * pp;
+    mm = mm + w1 * (gg - mm);
+    vv = vv * b2;
+    vv = vv + omb2 * gg * gg;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pp = pp + (-step_size) * (mm / denom);
+  };
+  const long long n4 = count >> 2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    f32x4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = pp[j], b = mm[j], c = vv[j];
+      upd(a, gg[j], b, c);
+      pp[j] = a; mm[j] = b; vv[j] = c;
+    }
+    st4(p + 4 * i, pp);
+    st4(m + 4 * i, mm);
+    st4(v + 4 * i, vv);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (count & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    float a = p[i], b = m[i], c = v[i];
+    upd(a, g[i], b, c);
+    p[i] = a; m[i] = b; v[i] = c;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_image_lut(long long count, const uint8_t* __restrict__ u8,
+                                                   const uint8_t* __restrict__ lut, float* __restrict__ out) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < count; i += (long long)gridDim.x * 256)
+    out[i] = (float)lut[u8[i]] * (1.0f / 255.0f);
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int tspm_linear_fwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* w,
+                               const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
+                               int32_t ldy, tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !w || !y) return TSPM_ERR_INVALID;
+  if ((in & 3) == 0 && (ldx & 3) == 0 && !(aligned16(x) && aligned16(w))) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_linear_fwd, dim3(grid_for((long long)n * out)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     n, in, out, x, ldx, w, b, relu, keep, keep_scale, y, ldy);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,
+                                    float* dx, int32_t ldx, tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !dy || !w || !dx) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_linear_bwd_data, dim3(grid_for((long long)n * in)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, in, out, dy, ldy, w, dx, ldx);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy,
+                                      int32_t ldy, float* dw, float* db, tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !dy || !dw) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_linear_bwd_weight, dim3(grid_for((long long)out * in)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, in, out, x, ldx, dy, ldy, dw, db);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,
+                            tspm_stream_t stream) {
+  if (n <= 0 || cols <= 0 || ldg < cols || ldy < cols || !g || !y) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_act_bwd, dim3(grid_for((long long)n * cols)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     n, cols, g, ldg, y, ldy, scale);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_dropout_mask(int64_t count, float p, uint64_t seed, const uint64_t* counter, uint8_t* keep,
+                                 tspm_stream_t stream) {
+  if (count < 0 || !keep || p < 0.f || p >= 1.f) return TSPM_ERR_INVALID;
+  if (count == 0) return TSPM_OK;
+  hipLaunchKernelGGL(k_dropout_mask, dim3(grid_for(count)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (long long)count, p, (unsigned long long)seed, counter, keep);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const int64_t* labels, float* loss,
+                                  float* dlogits, float grad_scale, float* stats, tspm_stream_t stream) {
+  if (n <= 0 || classes <= 0 || !logits || !labels) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_cross_entropy, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), n, classes, logits,
+                     labels, loss, dlogits, grad_scale, stats);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream) {
+  if (!hyper) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_adam_begin, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), hyper);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              const tspm_adam_hyper* hyper, tspm_stream_t stream) {
+  if (count < 0 || !param || !grad || !exp_avg || !exp_avg_sq || !hyper) return TSPM_ERR_INVALID;
+  if (!aligned16(param) || !aligned16(grad) || !aligned16(exp_avg) || !aligned16(exp_avg_sq)) return TSPM_ERR_INVALID;
+  if (count == 0) return TSPM_OK;
+  long long blocks = cdiv64(count / 4 + 1, 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_adam, dim3((int)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)count, param,
+                     grad, exp_avg, exp_avg_sq, hyper);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* lut, float* out, tspm_stream_t stream) {
+  if (count < 0 || !u8 || !lut || !out) return TSPM_ERR_INVALID;
+  if (count == 0) return TSPM_OK;
+  hipLaunchKernelGGL(k_image_lut, dim3(grid_for(count)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     (long long)count, u8, lut, out);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_abi_version(void) { return 2; }
+
+extern "C" const char* tspm_status_string(int status) {
+  switch (status) {
+    case TSPM_OK: return "ok";
+    case TSPM_ERR_INVALID: return "invalid argument";
+    case TSPM_ERR_LAUNCH: return "kernel launch failed";
+    case TSPM_ERR_WORKSPACE: return "workspace too small";
+    default: return "unknown status";
+  }
+}

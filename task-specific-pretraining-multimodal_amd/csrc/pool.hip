@@ -1,0 +1,156 @@
+// Max pooling (nn.MaxPool2d(3, 2, 1), MML_Suite/models/msa/networks/resnet.py:140,208) and global
+// average pooling (nn.AdaptiveAvgPool2d((1,1)) + flatten, resnet.py:149,215-216) on HWNC tensors.
+// HBM-bound; one thread per 4 channels of one output element, 16-byte loads/stores.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_maxpool_fwd(int N, int H, int W, int C, int k, int st, int pad, int P,
+                                                     int Q, const float* __restrict__ x, float* __restrict__ y,
+                                                     uint8_t* __restrict__ idx) {
+  const int L = C >> 2;
+  const long long total = (long long)P * Q * N * L;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    long long row = i / L;  // (p, q, n)
+    const int n = (int)(row % N);
+    const int pos = (int)(row / N);
+    const int p = pos / Q, q = pos - p * Q;
+    f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {0, 0, 0, 0};
+    for (int kh = 0; kh < k; ++kh) {
+      const int h = p * st - pad + kh;
+      if (h < 0 || h >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int w = q * st - pad + kw;
+        if (w < 0 || w >= W) continue;
+        const f32x4 v = ld4(x + (((long long)h * W + w) * N + n) * C + 4 * c4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (v[j] > best[j] || isnan(v[j])) { best[j] = v[j]; bi[j] = kh * k + kw; }
+      }
+    }
+    st4(y + row * C + 4 * c4, best);
+    uchar4 u;
+    u.x = (uint8_t)bi[0]; u.y = (uint8_t)bi[1]; u.z = (uint8_t)bi[2]; u.w = (uint8_t)bi[3];
+    *reinterpret_cast<uchar4*>(idx + row * C + 4 * c4) = u;
+  }
+}
+
+// gather form: every input element sums dy over the windows that picked it (deterministic order)
+__global__ __launch_bounds__(256) void k_maxpool_bwd(int N, int H, int W, int C, int k, int st, int pad, int P,
+                                                     int Q, const float* __restrict__ dy,
+                                                     const uint8_t* __restrict__ idx, float* __restrict__ dx) {
+  const int L = C >> 2;
+  const long long total = (long long)H * W * N * L;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    long long row = i / L;
+    const int n = (int)(row % N);
+    const int pos = (int)(row / N);
+    const int h = pos / W, w = pos - h * W;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // p such that 0 <= h - (p*st - pad) < k
+    const int p_lo = max(0, (h + pad - k + st) / st), p_hi = min(P - 1, (h + pad) / st);
+    const int q_lo = max(0, (w + pad - k + st) / st), q_hi = min(Q - 1, (w + pad) / st);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int kh = h - (p * st - pad);
+      if (kh < 0 || kh >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int kw = w - (q * st - pad);
+        if (kw < 0 || kw >= k) continue;
+        const long long o = (((long long)p * Q + q) * N + n) * C + 4 * c4;
+        const uchar4 u = *reinterpret_cast<const uchar4*>(idx + o);
+        const f32x4 g = ld4(dy + o);
+        const int tap = kh * k + kw;
+        if (u.x == tap) acc[0] += g[0];
+        if (u.y == tap) acc[1] += g[1];
+        if (u.z == tap) acc[2] += g[2];
+        if (u.w == tap) acc[3] += g[3];
+      }
+    }
+    st4(dx + row * C + 4 * c4, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_avgpool_fwd(int npos, int N, int C, const float* __restrict__ x,
+                                                     float* __restrict__ y) {
+  const int L = C >> 2;
+  const long long total = (long long)N * L;
+  const float inv = 1.0f / (float)npos;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < npos; ++p) s += ld4(x + (long long)p * N * C + 4 * i);
+    // ATen's CPU adaptive_avg_pool2d: sum over the window then divide by its size
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = s[j] / (float)npos;
+    (void)inv;
+    st4(y + 4 * i, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_avgpool_bwd(int npos, int N, int C, const float* __restrict__ dy, int ldy,
+                                                     float* __restrict__ dx) {
+  const int L = C >> 2;
+  const long long total = (long long)npos * N * L;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    const long long row = i / L;
+    const int n = (int)(row % N);
+    f32x4 g = ld4(dy + (long long)n * ldy + 4 * c4);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = g[j] / (float)npos;
+    st4(dx + row * C + 4 * c4, o);
+  }
+}
+
+int grid_for(long long work) {
+  long long b = cdiv64(work, 256);
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" int tspm_maxpool_fwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
+                                int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, tspm_stream_t stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 || k <= 0 || k > 15 || stride <= 0 || pad < 0 || !x || !y || !idx)
+    return TSPM_ERR_INVALID;
+  if (p != (h + 2 * pad - k) / stride + 1 || q != (w + 2 * pad - k) / stride + 1 || p <= 0 || q <= 0)
+    return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long long)p * q * n * c / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, x, y, idx);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
+                                int32_t p, int32_t q, const float* dy, const uint8_t* idx, float* dx,
+                                tspm_stream_t stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 || k <= 0 || k > 15 || stride <= 0 || pad < 0 || !dy || !idx || !dx)
+    return TSPM_ERR_INVALID;
+  if (p != (h + 2 * pad - k) / stride + 1 || q != (w + 2 * pad - k) / stride + 1) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long long)h * w * n * c / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, dy, idx, dx);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_avgpool_fwd(int32_t npos, int32_t n, int32_t c, const float* x, float* y, tspm_stream_t stream) {
+  if (npos <= 0 || n <= 0 || c <= 0 || c % 4 || !x || !y) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3(grid_for((long long)n * c / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), npos, n, c, x, y);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_avgpool_bwd(int32_t npos, int32_t n, int32_t c, const float* dy, int32_t ldy, float* dx,
+                                tspm_stream_t stream) {
+  if (npos <= 0 || n <= 0 || c <= 0 || c % 4 || ldy < c || ldy % 4 || !dy || !dx) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for((long long)npos * n * c / 4)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), npos, n, c, dy, ldy, dx);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}

@@ -1,0 +1,447 @@
+"""Per-encoder execution plan: the ResNet18/34 encoder forward/backward as a fixed schedule of
+libtspm kernels over pre-allocated HWNC buffers.
+
+Mirrors ``ResNetEncoder.forward`` (MML_Suite/models/msa/networks/resnet.py:199-219) and
+``BasicBlock.forward`` (:37-54) and their autograd backward.  All launches go to the caller's
+current stream through the C ABI; nothing allocates inside ``forward_train``/``backward``, so the
+whole step can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib as L
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def _out_hw(h: int, w: int, k: int, s: int, p: int) -> Tuple[int, int]:
+    return (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+
+
+@dataclass
+class ConvOp:
+    module: torch.nn.Conv2d
+    shape: L.ConvShape
+    algo_fwd: L.ConvAlgo = field(default_factory=L.ConvAlgo)
+    algo_dgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
+    algo_wgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
+
+    @property
+    def rows_out(self) -> int:
+        s = self.shape
+        return s.p * s.q * s.n
+
+    @property
+    def rows_in(self) -> int:
+        s = self.shape
+        return s.h * s.w * s.n
+
+    def ws_bytes(self, need_dgrad: bool) -> int:
+        lib = L.lib()
+        b = max(lib.tspm_conv_fwd_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd)),
+                lib.tspm_conv_wgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_wgrad)))
+        if need_dgrad:
+            b = max(b, lib.tspm_conv_dgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_dgrad)))
+        return b
+
+
+@dataclass
+class BNOp:
+    module: torch.nn.BatchNorm2d
+    rows: int
+    channels: int
+    mean: Optional[torch.Tensor] = None      # save_mean  [C]
+    invstd: Optional[torch.Tensor] = None    # save_invstd [C]
+
+
+@dataclass
+class BlockPlan:
+    conv1: ConvOp
+    bn1: BNOp
+    conv2: ConvOp
+    bn2: BNOp
+    ds_conv: Optional[ConvOp]
+    ds_bn: Optional[BNOp]
+    # buffers (HWNC)
+    y1: torch.Tensor = None
+    a1: torch.Tensor = None
+    y2: torch.Tensor = None
+    yd: Optional[torch.Tensor] = None
+    out: torch.Tensor = None
+
+
+class EncoderEngine:
+    """Execution plan of one ResNetEncoder for a fixed (batch, H, W)."""
+
+    def __init__(self, encoder: torch.nn.Module, batch: int, height: int, width: int, device: torch.device,
+                 grad_of: Optional[Callable[[torch.Tensor], torch.Tensor]] = None):
+        self.enc = encoder
+        self.N, self.H, self.W = batch, height, width
+        self.device = device
+        self.grad_of = grad_of or _default_grad_of
+        self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
+        self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
+        N = batch
+        f32 = dict(device=device, dtype=torch.float32)
+        c1 = encoder.conv1
+        cin = c1.in_channels
+        self.cin = cin
+        p1, q1 = _out_hw(height, width, 7, 2, 3)
+        self.stem = ConvOp(c1, L.ConvShape(N, height, width, cin, c1.out_channels, 7, 7, 2, 3, p1, q1))
+        self.stem_bn = BNOp(encoder.bn1, p1 * q1 * N, c1.out_channels)
+        p2, q2 = _out_hw(p1, q1, 3, 2, 1)
+        self.mp_shape = (p1, q1, p2, q2)
+        C0 = c1.out_channels
+        self.y0 = torch.empty(p1 * q1 * N, C0, **f32)
+        self.a0 = torch.empty(p1 * q1 * N, C0, **f32)
+        self.mp = torch.empty(p2 * q2 * N, C0, **f32)
+        self.mp_idx = torch.empty(p2 * q2 * N, C0, device=device, dtype=torch.uint8)
+
+        self.blocks: List[BlockPlan] = []
+        h, w, c = p2, q2, C0
+        for layer in (encoder.layer1, encoder.layer2, encoder.layer3, encoder.layer4):
+            for blk in layer:
+                st = blk.conv1.stride[0]
+                planes = blk.conv1.out_channels
+                ho, wo = _out_hw(h, w, 3, st, 1)
+                conv1 = ConvOp(blk.conv1, L.ConvShape(N, h, w, c, planes, 3, 3, st, 1, ho, wo))
+                conv2 = ConvOp(blk.conv2, L.ConvShape(N, ho, wo, planes, planes, 3, 3, 1, 1, ho, wo))
+                rows = ho * wo * N
+                bp = BlockPlan(conv1, BNOp(blk.bn1, rows, planes), conv2, BNOp(blk.bn2, rows, planes), None, None)
+                if blk.downsample is not None:
+                    dc = blk.downsample[0]
+                    dst = dc.stride[0]
+                    bp.ds_conv = ConvOp(dc, L.ConvShape(N, h, w, c, planes, 1, 1, dst, 0, ho, wo))
+                    bp.ds_bn = BNOp(blk.downsample[1], rows, planes)
+                bp.y1 = torch.empty(rows, planes, **f32)
+                bp.a1 = torch.empty(rows, planes, **f32)
+                bp.y2 = torch.empty(rows, planes, **f32)
+                bp.out = torch.empty(rows, planes, **f32)
+                if bp.ds_conv is not None:
+                    bp.yd = torch.empty(rows, planes, **f32)
+                self.blocks.append(bp)
+                h, w, c = ho, wo, planes
+        self.final_hw = (h, w)
+        self.final_c = c
+        self.pooled = torch.empty(N, c, **f32)
+        self.hidden = encoder.fc.out_features
+
+        # BN saved statistics
+        for bn in self.all_bns():
+            bn.mean = torch.empty(bn.channels, **f32)
+            bn.invstd = torch.empty(bn.channels, **f32)
+
+        # backward scratch: grads of block outputs (ping-pong), dy buffers
+        max_blk = max(bp.out.numel() for bp in self.blocks)
+        max_blk = max(max_blk, self.mp.numel())
+        self.gA = torch.empty(max_blk, **f32)
+        self.gB = torch.empty(max_blk, **f32)
+        self.d1 = torch.empty(max_blk, **f32)
+        self.d2 = torch.empty(max_blk, **f32)
+        self.dd = torch.empty(max_blk, **f32)
+        self.da1 = torch.empty(max_blk, **f32)
+        self.g_stem = torch.empty(self.a0.numel(), **f32)
+        self.dy_stem = torch.empty(self.a0.numel(), **f32)
+        self.g_pooled = torch.empty(N, c, **f32)
+        self.g_final = torch.empty(h * w * N * c, **f32)
+        self._alloc_workspace()
+
+    # ---------------------------------------------------------------------------------------
+    def all_convs(self) -> List[ConvOp]:
+        ops = [self.stem]
+        for bp in self.blocks:
+            ops += [bp.conv1, bp.conv2] + ([bp.ds_conv] if bp.ds_conv is not None else [])
+        return ops
+
+    def all_bns(self) -> List[BNOp]:
+        ops = [self.stem_bn]
+        for bp in self.blocks:
+            ops += [bp.bn1, bp.bn2] + ([bp.ds_bn] if bp.ds_bn is not None else [])
+        return ops
+
+    def _alloc_workspace(self) -> None:
+        lib = L.lib()
+        conv_ws = max(op.ws_bytes(op is not self.stem) for op in self.all_convs())
+        bn_ws = 0
+        for bn in self.all_bns():
+            bn_ws = max(bn_ws, lib.tspm_bn_stats_workspace(bn.rows, bn.channels),
+                        lib.tspm_bn_bwd_workspace(bn.rows, bn.channels))
+        self.ws_conv_bytes = max(conv_ws, 256)
+        self.ws_bn_bytes = max(bn_ws, 256)
+        self.ws_conv = torch.empty(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        self.ws_bn = torch.empty(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
+
+    def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
+        """Override tile configs: key (kind, n,h,w,c,k,r,s,stride) -> (tm, tn, wm, wn, splits)."""
+        for op in self.all_convs():
+            s = op.shape
+            base = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride)
+            for kind in ("fwd", "dgrad", "wgrad"):
+                v = table.get((kind,) + base)
+                if v is not None:
+                    setattr(op, f"algo_{kind}", L.ConvAlgo(*v))
+        self._alloc_workspace()
+
+    # ---------------------------------------------------------------------------------------
+    @staticmethod
+    def _w(op: ConvOp) -> torch.Tensor:
+        w = op.module.weight
+        if not w.is_contiguous(memory_format=torch.channels_last):
+            raise L.TspmError("conv weight must be OHWI (channels_last); call prepare_encoder_layout() first")
+        return w
+
+    def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> int:
+        """Run the conv; returns the number of slabs written (slabs live in ws_conv)."""
+        lib = L.lib()
+        s, a = op.shape, op.algo_fwd
+        need = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a))
+        if self.conv_timer:
+            self.conv_timer.begin(op, "fwd")
+        L.check(lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x_ptr, ctypes.byref(strides), self._w(op).data_ptr(),
+                                  y.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_fwd")
+        if self.conv_timer:
+            self.conv_timer.end()
+        if need == 0:
+            return 1
+        return need // (op.rows_out * s.k * 4)
+
+    def _bn_stats(self, bn: BNOp, y: torch.Tensor, nslab: int, sh: int) -> None:
+        lib = L.lib()
+        m = bn.module
+        src = self.ws_conv if nslab > 1 else y
+        L.check(lib.tspm_bn_stats(bn.rows, bn.channels, src.data_ptr(), nslab, bn.rows * bn.channels, y.data_ptr(),
+                                  L.ptr(m.running_mean), L.ptr(m.running_var), BN_MOMENTUM if m.momentum is None else m.momentum,
+                                  m.eps, bn.mean.data_ptr(), bn.invstd.data_ptr(), self.ws_bn.data_ptr(),
+                                  self.ws_bn_bytes, sh), "bn_stats")
+
+    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
+        nslab = self._conv_fwd(op, x_ptr, strides, y, sh)
+        self._bn_stats(bn, y, nslab, sh)
+
+    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True):
+        lib = L.lib()
+        m = bn.module
+        if train:
+            L.check(lib.tspm_bn_apply(bn.rows, bn.channels, y.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                      m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res),
+                                      L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
+                                      L.ptr(bn2.module.weight) if bn2 else None, L.ptr(bn2.module.bias) if bn2 else None,
+                                      1 if relu else 0, out.data_ptr(), sh), "bn_apply")
+        else:
+            m2 = bn2.module if bn2 else None
+            L.check(lib.tspm_bn_apply_eval(bn.rows, bn.channels, y.data_ptr(), m.running_mean.data_ptr(),
+                                           m.running_var.data_ptr(), m.eps, m.weight.data_ptr(), m.bias.data_ptr(),
+                                           res_mode, L.ptr(res), L.ptr(m2.running_mean) if m2 else None,
+                                           L.ptr(m2.running_var) if m2 else None, L.ptr(m2.weight) if m2 else None,
+                                           L.ptr(m2.bias) if m2 else None, 1 if relu else 0, out.data_ptr(), sh),
+                    "bn_apply_eval")
+
+    # ---------------------------------------------------------------------------------------
+    def input_strides(self, x: torch.Tensor) -> L.Strides4:
+        """Strides of the reference's NCHW ([N,H,W] or [N,1,H,W]) input, read in place by the stem."""
+        if x.dim() == 3:
+            sn, sh_, sw = x.stride()
+            sc = 0
+        else:
+            sn, sc, sh_, sw = x.stride()
+        return L.Strides4(sn, sh_, sw, sc)
+
+    def check_input(self, x: torch.Tensor) -> None:
+        L.require_cuda_f32(x, "encoder input")
+        shp = tuple(x.shape)
+        want3 = (self.N, self.H, self.W)
+        want4 = (self.N, self.cin, self.H, self.W)
+        if shp != want3 and shp != want4:
+            raise L.TspmError(f"encoder input shape {shp} != planned {want4}")
+        if x.dim() == 3 and self.cin != 1:
+            raise L.TspmError("3-D input requires in_channels == 1 (resnet.py:201-203)")
+
+    def forward(self, x: torch.Tensor, emb: torch.Tensor, ld_emb: int, train: bool = True,
+                bump_batches_tracked: bool = True) -> None:
+        """x: reference-layout input [N,H,W] / [N,C,H,W] fp32 on device; emb: [N, >=hidden] output view
+        (row stride ld_emb) that receives the fc output.  In training mode every BatchNorm's
+        num_batches_tracked is incremented (nn.BatchNorm2d semantics) unless the caller does it."""
+        self.check_input(x)
+        if train and bump_batches_tracked:
+            nbt = [bn.module.num_batches_tracked for bn in self.all_bns() if bn.module.num_batches_tracked is not None]
+            if nbt:
+                torch._foreach_add_(nbt, 1)
+        sh = L.stream_handle()
+        lib = L.lib()
+        N = self.N
+        self.x_in = x
+        xs = self.input_strides(x)
+        p1, q1, p2, q2 = self.mp_shape
+        C0 = self.stem.shape.k
+        if train:
+            self._conv_bn(self.stem, self.stem_bn, x.data_ptr(), xs, self.y0, sh)
+        else:
+            self._conv_fwd_eval(self.stem, x.data_ptr(), xs, self.y0, sh)
+        self._apply(self.stem_bn, self.y0, self.a0, relu=True, sh=sh, train=train)
+        L.check(lib.tspm_maxpool_fwd(N, p1, q1, C0, 3, 2, 1, p2, q2, self.a0.data_ptr(), self.mp.data_ptr(),
+                                     self.mp_idx.data_ptr(), sh), "maxpool_fwd")
+        xin = self.mp
+        for bp in self.blocks:
+            s1 = bp.conv1.shape
+            xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
+            if train:
+                self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
+            else:
+                self._conv_fwd_eval(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
+            self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
+            s2 = bp.conv2.shape
+            xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
+            if train:
+                self._conv_bn(bp.conv2, bp.bn2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
+            else:
+                self._conv_fwd_eval(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
+            if bp.ds_conv is not None:
+                if train:
+                    self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
+                else:
+                    self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train)
+            else:
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train)
+            xin = bp.out
+        h, w = self.final_hw
+        L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh), "avgpool_fwd")
+        fc = self.enc.fc
+        L.check(lib.tspm_linear_fwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
+                                    fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb, sh),
+                "linear_fwd(fc)")
+
+    def _conv_fwd_eval(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
+        nslab = self._conv_fwd(op, x_ptr, strides, y, sh)
+        if nslab > 1:
+            L.check(L.lib().tspm_reduce_slabs(op.rows_out * op.shape.k, nslab, op.rows_out * op.shape.k,
+                                              self.ws_conv.data_ptr(), y.data_ptr(), sh), "reduce_slabs")
+
+    # ---------------------------------------------------------------------------------------
+    def _grad(self, p: torch.Tensor) -> torch.Tensor:
+        return self.grad_of(p)
+
+    def _bn_bwd(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None, sh=0):
+        lib = L.lib()
+        m = bn.module
+        gw, gb = self._grad(m.weight), self._grad(m.bias)
+        if bn2 is not None:
+            m2 = bn2.module
+            gw2, gb2 = self._grad(m2.weight), self._grad(m2.bias)
+        L.check(lib.tspm_bn_bwd(bn.rows, bn.channels, g.data_ptr(), L.ptr(out_mask), y.data_ptr(), bn.mean.data_ptr(),
+                                bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
+                                L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
+                                L.ptr(bn2.module.weight) if bn2 else None, L.ptr(gw2) if bn2 else None,
+                                L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), self.ws_bn.data_ptr(),
+                                self.ws_bn_bytes, sh), "bn_bwd")
+
+    def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int) -> None:
+        lib = L.lib()
+        gw = self._grad(op.module.weight)
+        if not gw.is_contiguous(memory_format=torch.channels_last):
+            raise L.TspmError("conv weight grad must be OHWI (channels_last)")
+        if self.conv_timer:
+            self.conv_timer.begin(op, "wgrad")
+        L.check(lib.tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides),
+                                    dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh),
+                "conv_wgrad")
+        if self.conv_timer:
+            self.conv_timer.end()
+
+    def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
+        if self.conv_timer:
+            self.conv_timer.begin(op, "dgrad")
+        L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
+                                        self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
+                                        self.ws_conv_bytes, sh), "conv_dgrad")
+        if self.conv_timer:
+            self.conv_timer.end()
+
+    def backward(self, g_emb: torch.Tensor, ld_g: int) -> None:
+        """g_emb: [N, hidden] gradient of the fc output (row stride ld_g).  Writes every parameter
+        gradient of the encoder (overwrite semantics) through ``grad_of``."""
+        sh = L.stream_handle()
+        lib = L.lib()
+        N = self.N
+        fc = self.enc.fc
+        L.check(lib.tspm_linear_bwd_weight(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
+                                           g_emb.data_ptr(), ld_g, self._grad(fc.weight).data_ptr(),
+                                           self._grad(fc.bias).data_ptr() if fc.bias is not None else None, sh),
+                "linear_bwd_weight(fc)")
+        L.check(lib.tspm_linear_bwd_data(N, self.final_c, self.hidden, g_emb.data_ptr(), ld_g, fc.weight.data_ptr(),
+                                         self.g_pooled.data_ptr(), self.final_c, sh), "linear_bwd_data(fc)")
+        h, w = self.final_hw
+        G, Gn = self.gA, self.gB
+        L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(), sh),
+                "avgpool_bwd")
+        for i in range(len(self.blocks) - 1, -1, -1):
+            bp = self.blocks[i]
+            xin = self.blocks[i - 1].out if i > 0 else self.mp
+            s1 = bp.conv1.shape
+            xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
+            n_out = bp.out.numel()
+            n_in = xin.numel()
+            Gv = G[:n_out]
+            Gnv = Gn[:n_in]
+            d2 = self.d2[:n_out]
+            if bp.ds_conv is not None:
+                dd = self.dd[:n_out]
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+            else:
+                # identity residual: g' goes straight to the block-input gradient buffer
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
+            s2 = bp.conv2.shape
+            self._wgrad(bp.conv2, bp.a1.data_ptr(), L.hwnc_strides(N, s2.h, s2.w, s2.c), d2, sh)
+            da1 = self.da1[:n_out]
+            self._dgrad(bp.conv2, d2, da1, 0, sh)
+            d1 = self.d1[:n_out]
+            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
+            if self.debug_hook is not None:
+                self.debug_hook(f"block{i}.g_out", Gv)
+                self.debug_hook(f"block{i}.d_y2", d2)
+                self.debug_hook(f"block{i}.d_a1", da1)
+                self.debug_hook(f"block{i}.d_y1", d1)
+            self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
+            if bp.ds_conv is not None:
+                self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
+                self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
+            self._dgrad(bp.conv1, d1, Gnv, 1, sh)
+            G, Gn = Gn, G
+        # stem: maxpool -> relu/bn -> conv1 (weight grad only)
+        p1, q1, p2, q2 = self.mp_shape
+        C0 = self.stem.shape.k
+        L.check(lib.tspm_maxpool_bwd(N, p1, q1, C0, 3, 2, 1, p2, q2, G.data_ptr(), self.mp_idx.data_ptr(),
+                                     self.g_stem.data_ptr(), sh), "maxpool_bwd")
+        self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
+        self._wgrad(self.stem, self.x_in.data_ptr(), self.input_strides(self.x_in), self.dy_stem, sh)
+
+
+def _default_grad_of(p: torch.Tensor) -> torch.Tensor:
+    """Return p.grad, (re)allocating it in p's memory format when absent."""
+    g = p.grad
+    if g is None or g.shape != p.shape:
+        fmt = torch.channels_last if (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last)
+                                      and not p.is_contiguous()) else torch.contiguous_format
+        if p.dim() == 4:
+            fmt = torch.channels_last
+        g = torch.empty_like(p, memory_format=fmt)
+        p.grad = g
+    return g
+
+
+def prepare_encoder_layout(encoder: torch.nn.Module) -> None:
+    """Re-lay every conv weight of the encoder as OHWI (channels_last view of the OIHW parameter).
+    Shapes, values and state_dict keys are unchanged."""
+    for m in encoder.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            w = m.weight
+            if not w.is_contiguous(memory_format=torch.channels_last):
+                w.data = w.data.contiguous(memory_format=torch.channels_last)
+            if w.grad is not None and not w.grad.is_contiguous(memory_format=torch.channels_last):
+                w.grad = w.grad.contiguous(memory_format=torch.channels_last)

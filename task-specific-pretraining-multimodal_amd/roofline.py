@@ -1,0 +1,71 @@
+"""Algorithmic work accounting for the roofline numbers.
+
+* Nominal dense conv FLOPs: 2 * P*Q*N * K * R*S*C per pass (fwd, dgrad, wgrad; no dgrad for the
+  1-channel stems) — 1,049,740,032 FLOP/sample for the late-fusion step including the linears.
+* Valid-tap FLOPs: only (output position, tap) pairs whose input pixel is inside the image —
+  641,174,016 FLOP/sample.  The HIP kernels skip padding taps, so achieved MFMA throughput is
+  quoted on the valid-tap count (it cannot exceed what the hardware executed).
+"""
+from __future__ import annotations
+
+from typing import Iterable, Tuple
+
+
+def _valid_1d(size_in: int, size_out: int, k: int, stride: int, pad: int) -> int:
+    """Number of (output index, tap) pairs along one axis whose input index is in range."""
+    n = 0
+    for o in range(size_out):
+        base = o * stride - pad
+        for t in range(k):
+            if 0 <= base + t < size_in:
+                n += 1
+    return n
+
+
+def conv_macs(n, h, w, c, k, r, s, stride, pad) -> Tuple[int, int]:
+    """(nominal MACs, valid-tap MACs) of one pass of a conv."""
+    p = (h + 2 * pad - r) // stride + 1
+    q = (w + 2 * pad - s) // stride + 1
+    nominal = p * q * n * k * r * s * c
+    valid = _valid_1d(h, p, r, stride, pad) * _valid_1d(w, q, s, stride, pad) * n * k * c
+    return nominal, valid
+
+
+def encoder_convs(layers, h: int, w: int, cin: int = 1):
+    """Yield (name, conv shape tuple without batch) for a ResNet18/34 encoder on an h x w input."""
+    def out(hh, ww, k, st, p):
+        return (hh + 2 * p - k) // st + 1, (ww + 2 * p - k) // st + 1
+    yield "stem", (h, w, cin, 64, 7, 7, 2, 3)
+    h, w = out(h, w, 7, 2, 3)
+    h, w = out(h, w, 3, 2, 1)
+    c = 64
+    for li, (planes, nb) in enumerate(zip((64, 128, 256, 512), layers)):
+        for b in range(nb):
+            st = 2 if (b == 0 and li > 0) else 1
+            ho, wo = out(h, w, 3, st, 1)
+            yield f"layer{li + 1}.{b}.conv1", (h, w, c, planes, 3, 3, st, 1)
+            yield f"layer{li + 1}.{b}.conv2", (ho, wo, planes, planes, 3, 3, 1, 1)
+            if b == 0 and (st != 1 or c != planes):
+                yield f"layer{li + 1}.{b}.downsample", (h, w, c, planes, 1, 1, st, 0)
+            h, w, c = ho, wo, planes
+
+
+def step_flops_per_sample(audio_hw=(32, 94), image_hw=(28, 28), audio_hidden=64, image_hidden=128,
+                          head_hidden=128) -> Tuple[int, int]:
+    """(nominal, valid-tap) train-step FLOPs per sample: fwd + dgrad + wgrad, no stem dgrad."""
+    nom = val = 0
+    for layers, (h, w) in (((2, 2, 2, 2), audio_hw), ((3, 4, 6, 3), image_hw)):
+        for name, (hh, ww, c, k, r, s, st, p) in encoder_convs(layers, h, w):
+            a, b = conv_macs(1, hh, ww, c, k, r, s, st, p)
+            passes = 2 if name == "stem" else 3
+            nom += 2 * passes * a
+            val += 2 * passes * b
+    lin = 512 * audio_hidden + 512 * image_hidden + (audio_hidden + image_hidden) * head_hidden \
+        + head_hidden * (head_hidden // 2) + (head_hidden // 2) * 10
+    nom += 2 * 3 * lin
+    val += 2 * 3 * lin
+    return nom, val
+
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak

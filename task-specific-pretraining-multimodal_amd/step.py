@@ -1,0 +1,250 @@
+"""FusedTrainStep — the whole AVMNIST late-fusion train step as one HIP-graph replay.
+
+Replaces the per-batch body of MML_Suite/models/avmnist.py:269-310 (zero_grad → forward →
+LossFunctionGroup(CE) → backward → Adam.step) and the backward/optimizer loop of
+train_multimodal.py:469-488:
+
+    s0: audio ResNet18 fwd ─┐            ┌─ audio ResNet18 bwd ─┐
+    s1: image ResNet34 fwd ─┴─ head fwd ─ CE ─ head bwd ─┴─ image ResNet34 bwd ─┴─ [RCCL] ─ Adam
+
+The two encoders are independent until the fusion concat, so they run as parallel graph branches
+on two HIP streams.  Every buffer is allocated once; the first call runs eagerly, the second call
+captures the graph, later calls only copy the batch into the static input buffers and replay.
+Weight gradients are written straight into FusedAdam's flat gradient buffer (overwrite — no
+zero_grad pass); with world_size > 1 the flat buffer is all-reduced between backward and Adam
+(``ddp.GradAllReduce``) and 1/world is folded into Adam's gradient scale.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib as L
+from .engine import EncoderEngine, prepare_encoder_layout
+from .optim import FusedAdam
+
+NUM_CLASSES = 10
+
+
+def _ce_weight(loss_functions) -> Optional[float]:
+    """Weight of the single cross-entropy term of a LossFunctionGroup (experiment_utils/loss.py:83-148),
+    or None when the group is anything else (then the step follows the generic autograd path)."""
+    if loss_functions is None:
+        return 1.0
+    try:
+        items = list(loss_functions.items())
+    except AttributeError:
+        return None
+    if len(items) != 1:
+        return None
+    term = items[0][1]
+    fn = getattr(term, "loss_fn", None)
+    w = getattr(term, "weight", 1.0)
+    if not isinstance(fn, torch.nn.CrossEntropyLoss):
+        return None
+    if fn.weight is not None or fn.reduction != "mean" or fn.label_smoothing != 0.0:
+        return None
+    return float(w)
+
+
+def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: torch.Tensor) -> bool:
+    if os.environ.get("TSPM_DISABLE_FUSED_STEP"):
+        return False
+    if not isinstance(optimizer, FusedAdam):
+        return False
+    if _ce_weight(loss_functions) is None:
+        return False
+    if not (A.is_cuda and I.is_cuda):
+        return False
+    return A.shape[0] == I.shape[0]
+
+
+class FusedTrainStep:
+    def __init__(self, model, optimizer: FusedAdam, loss_functions, batch: int, audio_hw=(32, 94), image_hw=(28, 28),
+                 use_graph: bool = True, allreduce=None):
+        self.model = model
+        self.opt = optimizer
+        self.loss_functions = loss_functions
+        self.ce_weight = _ce_weight(loss_functions)
+        self.N = batch
+        self.use_graph = use_graph and not os.environ.get("TSPM_NO_GRAPH")
+        self.allreduce = allreduce
+        p0 = next(model.parameters())
+        dev = p0.device
+        self.device = dev
+        model.train()
+        prepare_encoder_layout(model.audio_encoder)
+        prepare_encoder_layout(model.image_encoder)
+        # flat grads must exist for every parameter (FusedAdam set them as views)
+        for p in model.parameters():
+            if p.requires_grad and p.grad is None:
+                raise L.TspmError("FusedTrainStep: parameter without a FusedAdam gradient view")
+        self.eng_a = EncoderEngine(model.audio_encoder, batch, audio_hw[0], audio_hw[1], dev)
+        self.eng_i = EncoderEngine(model.image_encoder, batch, image_hw[0], image_hw[1], dev)
+        f32 = dict(device=dev, dtype=torch.float32)
+        ea, ei = model.embd_size_A, model.embd_size_I
+        self.F = ea + ei
+        hd = model.hidden_dim
+        self.hd, self.h2 = hd, hd // 2
+        self.A = torch.empty(batch, audio_hw[0], audio_hw[1], **f32)
+        self.I = torch.empty(batch, 1, image_hw[0], image_hw[1], **f32)
+        self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.fused = torch.empty(batch, self.F, **f32)
+        self.h1 = torch.empty(batch, hd, **f32)
+        self.hh = torch.empty(batch, self.h2, **f32)
+        self.logits = torch.empty(batch, NUM_CLASSES, **f32)
+        self.dlogits = torch.empty(batch, NUM_CLASSES, **f32)
+        self.dh = torch.empty(batch, self.h2, **f32)
+        self.dh1 = torch.empty(batch, hd, **f32)
+        self.dfused = torch.empty(batch, self.F, **f32)
+        self.keep = torch.ones(batch, hd, dtype=torch.uint8, device=dev)
+        self.loss = torch.zeros(1, **f32)
+        self.stats = torch.zeros(4, **f32)  # loss*n, correct, n (accumulated on device)
+        self.keep_override: Optional[torch.Tensor] = None
+        # BN num_batches_tracked of both encoders in one int64 buffer (one add per step)
+        bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+        self.nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+        for i, m in enumerate(bns):
+            self.nbt[i] = m.num_batches_tracked.to(dev)
+            m.num_batches_tracked = self.nbt[i]
+        self.side = torch.cuda.Stream(device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
+        self.calls = 0
+        self._sig = (id(optimizer), id(loss_functions), batch)
+        # dropout RNG counter = FusedAdam's device step counter (distinct per step, graph-safe)
+        fgs = optimizer.flat_groups()
+        self._rng_ctr_ptr = fgs[0].hyper.data_ptr() + L.HYPER_STEP_OFFSET if fgs else None
+
+    def matches(self, A, I, optimizer, loss_functions) -> bool:
+        return self._sig == (id(optimizer), id(loss_functions), A.shape[0]) and tuple(A.shape[1:]) in (
+            tuple(self.A.shape[1:]),) and tuple(I.shape[-2:]) == tuple(self.I.shape[-2:])
+
+    # ------------------------------------------------------------------------------------------
+    def _head_fwd(self, sh: int) -> None:
+        lib = L.lib()
+        n, F, hd, h2 = self.N, self.F, self.hd, self.h2
+        net = self.model.net
+        p = self.model.dropout_p
+        keep = None
+        scale = 1.0
+        if p > 0:
+            scale = 1.0 / (1.0 - p)
+            if self.keep_override is None:
+                L.check(lib.tspm_dropout_mask(n * hd, p, self.model._rng_seed, self._rng_ctr_ptr, self.keep.data_ptr(),
+                                              sh), "dropout_mask")
+            keep = self.keep
+        L.check(lib.tspm_linear_fwd(n, F, hd, self.fused.data_ptr(), F, net[0].weight.data_ptr(), net[0].bias.data_ptr(),
+                                    1, L.ptr(keep), scale, self.h1.data_ptr(), hd, sh), "head fc0")
+        L.check(lib.tspm_linear_fwd(n, hd, h2, self.h1.data_ptr(), hd, net[3].weight.data_ptr(), net[3].bias.data_ptr(),
+                                    1, None, 1.0, self.hh.data_ptr(), h2, sh), "head fc3")
+        L.check(lib.tspm_linear_fwd(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, net[5].weight.data_ptr(),
+                                    net[5].bias.data_ptr(), 0, None, 1.0, self.logits.data_ptr(), NUM_CLASSES, sh),
+                "head fc5")
+        self._scale = scale
+
+    def _head_bwd(self, sh: int) -> None:
+        lib = L.lib()
+        n, F, hd, h2 = self.N, self.F, self.hd, self.h2
+        net = self.model.net
+        g = lambda p: p.grad  # noqa: E731  (flat views)
+        L.check(lib.tspm_linear_bwd_weight(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, self.dlogits.data_ptr(),
+                                           NUM_CLASSES, g(net[5].weight).data_ptr(), g(net[5].bias).data_ptr(), sh),
+                "head fc5 wgrad")
+        L.check(lib.tspm_linear_bwd_data(n, h2, NUM_CLASSES, self.dlogits.data_ptr(), NUM_CLASSES,
+                                         net[5].weight.data_ptr(), self.dh.data_ptr(), h2, sh), "head fc5 dgrad")
+        L.check(lib.tspm_act_bwd(n, h2, self.dh.data_ptr(), h2, self.hh.data_ptr(), h2, 1.0, sh), "head relu")
+        L.check(lib.tspm_linear_bwd_weight(n, hd, h2, self.h1.data_ptr(), hd, self.dh.data_ptr(), h2,
+                                           g(net[3].weight).data_ptr(), g(net[3].bias).data_ptr(), sh), "head fc3 wgrad")
+        L.check(lib.tspm_linear_bwd_data(n, hd, h2, self.dh.data_ptr(), h2, net[3].weight.data_ptr(),
+                                         self.dh1.data_ptr(), hd, sh), "head fc3 dgrad")
+        L.check(lib.tspm_act_bwd(n, hd, self.dh1.data_ptr(), hd, self.h1.data_ptr(), hd, self._scale, sh),
+                "head relu+dropout")
+        L.check(lib.tspm_linear_bwd_weight(n, F, hd, self.fused.data_ptr(), F, self.dh1.data_ptr(), hd,
+                                           g(net[0].weight).data_ptr(), g(net[0].bias).data_ptr(), sh), "head fc0 wgrad")
+        L.check(lib.tspm_linear_bwd_data(n, F, hd, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
+                                         self.dfused.data_ptr(), F, sh), "head fc0 dgrad")
+
+    def _fwd_bwd(self) -> None:
+        """Enqueue forward + loss + backward on the current stream (+ the side stream)."""
+        main = torch.cuda.current_stream()
+        ea = self.model.embd_size_A
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
+        self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
+        main.wait_stream(self.side)
+        sh = main.cuda_stream
+        self._head_fwd(sh)
+        L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
+                                           self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
+                                           self.stats.data_ptr(), sh), "cross_entropy")
+        self._head_bwd(sh)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.eng_i.backward(self.dfused[:, ea:], self.F)
+        self.eng_a.backward(self.dfused, self.F)
+        main.wait_stream(self.side)
+        self.nbt.add_(1)
+
+    def _opt(self) -> None:
+        self.opt.launch(torch.cuda.current_stream().cuda_stream)
+
+    def _enqueue_all(self) -> None:
+        self._fwd_bwd()
+        if self.allreduce is None:
+            self._opt()
+
+    # ------------------------------------------------------------------------------------------
+    def load_batch(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor) -> None:
+        if A.data_ptr() != self.A.data_ptr():
+            self.A.copy_(A.reshape(self.A.shape), non_blocking=True)
+        if I.data_ptr() != self.I.data_ptr():
+            self.I.copy_(I.reshape(self.I.shape), non_blocking=True)
+        if labels.data_ptr() != self.labels.data_ptr():
+            self.labels.copy_(labels, non_blocking=True)
+
+    def step(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor) -> Dict[str, torch.Tensor]:
+        self.load_batch(A, I, labels)
+        self.run()
+        return {"loss": self.loss, "logits": self.logits}
+
+    def run(self) -> None:
+        """One training step on the batch currently in the static input buffers."""
+        self.model.train()
+        self.opt.sync_hyper()
+        if self.keep_override is not None:
+            self.keep.copy_(self.keep_override.reshape(self.keep.shape).to(torch.uint8), non_blocking=True)
+        if not self.use_graph or self.calls == 0:
+            self._enqueue_all()
+        else:
+            if self.graph is None:
+                self._capture()
+            self.graph.replay()
+        if self.allreduce is not None:
+            self.allreduce()
+            if self.use_graph and self.graph_opt is not None:
+                self.graph_opt.replay()
+            else:
+                self._opt()
+                if self.use_graph and self.calls >= 1 and self.graph_opt is None:
+                    pass
+        self.opt.note_steps(1)
+        self.calls += 1
+
+    def _capture(self) -> None:
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            if self.allreduce is None:
+                self._enqueue_all()
+            else:
+                self._fwd_bwd()
+        self.graph = g
+        if self.allreduce is not None:
+            go = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(go):
+                self._opt()
+            self.graph_opt = go

@@ -1,0 +1,76 @@
+"""The C-ABI library loads and exports exactly what include/tspm.h declares (no GPU needed: only
+symbol lookup, version / status queries, workspace-size queries and argument validation that
+returns before any HIP call)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import tspm_amd
+from tspm_amd import _lib as L
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "tspm.h")
+
+
+def header_prototypes():
+    src = open(HEADER).read()
+    return dict(re.findall(r"\n(?:int|size_t|const char\*)\s+(tspm_\w+)\(([^;]*?)\);", src, re.S))
+
+
+def test_library_loads_and_version():
+    lib = L.load()
+    assert lib.tspm_abi_version() == L.ABI_VERSION
+    assert lib.tspm_status_string(0) == b"ok"
+    assert lib.tspm_status_string(3) == b"workspace too small"
+
+
+def test_every_header_symbol_is_exported_and_bound():
+    protos = header_prototypes()
+    assert len(protos) >= 28
+    lib = ctypes.CDLL(L.LIB_PATH)
+    for name, params in protos.items():
+        assert hasattr(lib, name), f"{name} declared in tspm.h but not exported"
+        assert name in L._SIGS, f"{name} has no ctypes binding"
+        n = 0 if params.strip() in ("void", "") else len(params.split(","))
+        assert n == len(L._SIGS[name][1]), f"{name}: header has {n} params, binding {len(L._SIGS[name][1])}"
+    assert set(L._SIGS) == set(protos)
+
+
+def test_no_unexpected_exports():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T tspm_" in l}
+    assert exported == set(header_prototypes())
+
+
+def test_invalid_arguments_are_rejected_before_launch():
+    lib = L.load()
+    s = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 7, 8)  # wrong p
+    a = L.ConvAlgo()
+    assert lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), 1, None, 1, 1, None, 0, None) == 1
+    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a)) == 0
+    good = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, 0, None) == 1
+    bad_algo = L.ConvAlgo(3, 1, 4, 1, 1)
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, 0, None) == 1
+    # dgrad needs K % 8 == 0
+    odd = L.ConvShape(2, 8, 8, 64, 12, 3, 3, 1, 1, 8, 8)
+    assert lib.tspm_conv_dgrad(ctypes.byref(odd), ctypes.byref(a), 16, 16, 16, 0, None, 0, None) == 1
+    assert lib.tspm_bn_stats(0, 64, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 1 << 20, None) == 1
+    assert lib.tspm_bn_stats(128, 66, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 1 << 20, None) == 1
+    assert lib.tspm_bn_stats(128, 64, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 0, None) == 3
+    assert lib.tspm_maxpool_fwd(2, 8, 8, 64, 3, 2, 1, 5, 4, 16, 16, 16, None) == 1
+    assert lib.tspm_adam_step(10, 17, 16, 16, 16, 16, None) == 1   # misaligned
+    assert lib.tspm_dropout_mask(10, 1.0, 0, None, 16, None) == 1   # p must be < 1
+
+
+def test_workspace_queries():
+    lib = L.load()
+    s = L.ConvShape(128, 7, 7, 64, 64, 3, 3, 1, 1, 7, 7)
+    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 4, 1, 1))) == 0
+    w3 = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 4, 1, 3)))
+    assert w3 == 3 * 7 * 7 * 128 * 64 * 4
+    assert lib.tspm_bn_stats_workspace(6272, 64) > 0
+    assert lib.tspm_bn_bwd_workspace(6272, 64) >= lib.tspm_bn_stats_workspace(6272, 64)
