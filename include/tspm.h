@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);
+int tspm_abi_version(void);  /* 3 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -54,10 +54,13 @@ typedef struct tspm_conv_shape {
 } tspm_conv_shape;
 
 /* Tile / split configuration.  tm, tn: 32x32 MFMA tiles per wave along M (rows) and N (columns);
- * wm * wn == 4 waves per 256-thread workgroup; splits: reduction split (>1 uses workspace slabs,
- * combined deterministically in slab order).  All-zero fields select the built-in heuristic. */
+ * a workgroup holds wn x wk waves: wn neighbouring column tiles of the same rows and wk waves that
+ * split the reduction of one tile and combine through LDS in fixed order (deterministic, no
+ * workspace).  splits: additional split of the wgrad reduction over workgroups (fp32 slabs, summed
+ * in slab order).  Supported: (tm,tn) in {(1,1),(1,2),(2,2)}, wn in {1,2,4}, wk in {1,2,4,8},
+ * wn*wk <= 8.  All-zero fields select the built-in heuristic. */
 typedef struct tspm_conv_algo {
-  int32_t tm, tn, wm, wn, splits;
+  int32_t tm, tn, wn, wk, splits;
 } tspm_conv_algo;
 
 /* Element strides (n, h, w, c) of a conv input tensor.  HWNC tensors: {c, w*n*c, n*c, 1}.
@@ -66,13 +69,19 @@ typedef struct tspm_strides4 {
   int64_t sn, sh, sw, sc;
 } tspm_strides4;
 
-/* y[P,Q,N,K] = conv(x, w).  y is HWNC. */
+/* y[P,Q,N,K] = conv(x, w).  y is HWNC.  If bn_partial != NULL the epilogue also writes BatchNorm
+ * partial statistics of y (3 planes of [tiles][K] floats: tile shift, mean offset, M2; tiles and
+ * rows per tile from the two queries below) for tspm_bn_finalize — the conv output is not re-read. */
 int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
-                  const tspm_strides4* x_strides, const float* w, float* y, void* workspace,
-                  size_t workspace_bytes, tspm_stream_t stream);
+                  const tspm_strides4* x_strides, const float* w, float* y, float* bn_partial,
+                  tspm_stream_t stream);
+int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+/* Always 0 (kept for ABI symmetry: the forward needs no workspace). */
 size_t tspm_conv_fwd_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
-/* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}. */
+/* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}.  Needs no
+ * workspace (the workspace arguments are accepted and ignored). */
 int tspm_conv_dgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy,
                     const float* w, float* dx, int32_t beta, void* workspace, size_t workspace_bytes,
                     tspm_stream_t stream);
@@ -97,6 +106,13 @@ int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab, int64_t s
                   float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
                   tspm_stream_t stream);
 size_t tspm_bn_stats_workspace(int64_t m, int32_t c);
+
+/* Merge per-tile partial statistics (3 planes of [ntiles][c]: tile shift K, mean-K, M2; tile t
+ * holds min(rows_per_tile, m - t*rows_per_tile) rows) into save_mean / save_invstd and the running
+ * statistics — the tail of tspm_bn_stats, and the consumer of tspm_conv_fwd's bn_partial. */
+int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t rows_per_tile, const float* partial,
+                     float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                     float* save_invstd, tspm_stream_t stream);
 
 /* out = act( gamma*(y-mean)*invstd + beta  [+ residual] ), act = ReLU if relu != 0.
  * res_mode 0: no residual; 1: residual = res (raw tensor, same [M,C]); 2: residual =

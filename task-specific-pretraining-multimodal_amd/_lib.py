@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class TspmLibraryError(RuntimeError):
@@ -33,7 +33,7 @@ class ConvShape(Structure):
 
 
 class ConvAlgo(Structure):
-    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wm", "wn", "splits")]
+    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits")]
 
 
 class Strides4(Structure):
@@ -53,7 +53,9 @@ _P = c_void_p
 _SIGS = {
     "tspm_abi_version": (c_int32, []),
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
-    "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, c_size_t, _P]),
+    "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, _P]),
+    "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_dgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, _P, _P, c_int32, _P, c_size_t, _P]),
     "tspm_conv_dgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
@@ -62,6 +64,7 @@ _SIGS = {
     "tspm_bn_stats": (c_int32, [c_int64, c_int32, _P, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P,
                                 c_size_t, _P]),
     "tspm_bn_stats_workspace": (c_size_t, [c_int64, c_int32]),
+    "tspm_bn_finalize": (c_int32, [c_int64, c_int32, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P]),
     "tspm_bn_apply": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P]),
     "tspm_bn_apply_eval": (c_int32, [c_int64, c_int32, _P, _P, _P, c_float, _P, _P, c_int32, _P, _P, _P, _P, _P,
                                      c_int32, _P, _P]),

@@ -3,53 +3,54 @@
 // Replaces nn.BatchNorm2d at MML_Suite/models/msa/networks/resnet.py:26,31,138,177 together with the
 // ReLU (:27,42,52,139) and the residual add (:51) that follow it.
 //
-// Statistics: each workgroup computes its rows' mean and sum of squared deviations in two passes
-// (the second from L2), and a per-channel finalisation merges them in double in block order
-// (deterministic).  No E[y^2] - E[y]^2 cancellation — the audio stem produces |y| ~ 1e8 and border
-// positions of tiny feature maps sit many standard deviations from the channel mean.
+// Statistics are carried as per-tile partials {K (a data value of the tile), mean-K, M2 (sum of
+// squared deviations from the tile mean)}: produced either by the conv epilogue (tspm_conv_fwd with
+// bn_partial, no re-read of the conv output) or by a shifted two-pass kernel over a [rows x 64-chan]
+// tile (tspm_bn_stats).  tspm_bn_finalize merges them per channel in double with a fixed-order
+// parallel reduction: mean = sum(n_t * mean_t)/n, M2 = sum(M2_t + n_t (mean_t - mean)^2).  No
+// E[y^2] - E[y]^2 cancellation anywhere: the audio stem produces |y| ~ 1e8, and border positions of
+// tiny feature maps sit many standard deviations away from the channel mean.
 #include "common.h"
 
 namespace {
 
-constexpr int kElemsPerBlock = 16384;
+constexpr int kChanPerBlock = 64;  // 16 float4 lanes
+constexpr int kRowGroups = 16;     // 256 threads = 16 lanes x 16 row groups
 
-int stats_blocks(long long m, int c) {
-  long long g = cdiv64(m * c, kElemsPerBlock);
+int row_blocks(long long m, int c) {
+  const long long cg = cdiv64(c, kChanPerBlock);
+  long long g = cdiv64(1024, cg);
+  const long long max_g = cdiv64(m, kRowGroups);
+  if (g > max_g) g = max_g;
   if (g < 1) g = 1;
-  if (g > 1024) g = 1024;
-  if (g > m) g = m;
   return (int)g;
 }
 
 // ------------------------------------------------------------------------------------------------
-// forward statistics: per-workgroup two-pass (block mean, then sum of squared deviations from it —
-// the second pass re-reads the block's rows from L2), merged across workgroups with Chan's formula
-// in double.  Numerically as good as ATen's two-pass CPU kernel even when the channel mean is many
-// standard deviations away from any single sample (border positions of 1x3 / 2x2 feature maps).
+// standalone forward statistics partials (shifted two-pass per [rows x 64 channels] tile)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bn_stats_partial(long long M, int C, const float* __restrict__ y,
                                                           int nslab, long long slab_stride, float* __restrict__ y_out,
                                                           long long rows_per_block, float* __restrict__ part) {
-  __shared__ f32x4 sh[256];
-  __shared__ f32x4 smean[256];
-  const int L = C >> 2;            // threads per row
-  const int RP = 256 / L;          // rows per pass
+  __shared__ f32x4 sh[256], sh2[256];
+  __shared__ f32x4 soff[16];
   const int t = threadIdx.x;
-  const int c4 = t % L, rg = t / L;
+  const int lane = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + lane;
+  const bool cok = 4 * c4 < C;
   const long long r_begin = blockIdx.x * rows_per_block;
   const long long r_end = min(M, r_begin + rows_per_block);
-  const float inv_n = 1.0f / (float)(r_end - r_begin);
+  const double n = (double)(r_end - r_begin);
+  const float inv_n = (float)(1.0 / n);
   auto load = [&](long long off) -> f32x4 {
     f32x4 v = ld4(y + off);
     for (int z = 1; z < nslab; ++z) v += ld4(y + z * slab_stride + off);
     return v;
   };
-  // pass 1: block sums shifted by the block's first row K (an exact data value), so the fp32 sum
-  // carries the spread of the data, not its offset (channels can sit at 1e7 with a spread of 1e-2)
-  f32x4 s1 = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 K = load(r_begin * C + 4 * c4);
-  if (rg < RP) {
-    for (long long row = r_begin + rg; row < r_end; row += RP) {
+  f32x4 K = {0.f, 0.f, 0.f, 0.f}, s1 = K;
+  if (cok) {
+    K = load(r_begin * C + 4 * c4);
+    for (long long row = r_begin + rg; row < r_end; row += kRowGroups) {
       const long long off = row * C + 4 * c4;
       const f32x4 v = load(off);
       if (nslab > 1) st4(y_out + off, v);
@@ -59,68 +60,93 @@ __global__ __launch_bounds__(256) void k_bn_stats_partial(long long M, int C, co
   sh[t] = s1;
   __syncthreads();
   if (rg == 0) {
-    for (int k = 1; k < RP; ++k) s1 += sh[k * L + c4];
-    smean[c4] = s1 * inv_n;  // block mean minus K (small)
+    for (int k = 1; k < kRowGroups; ++k) s1 += sh[k * 16 + lane];
+    soff[lane] = s1 * inv_n;
   }
   __syncthreads();
-  // pass 2 (rows are L2-resident): d = (v - K) - off; mean_b = K + off + sum(d)/n and
-  // M2_b = sum(d^2) - sum(d)^2/n (corrected two-pass; the final correction in double)
-  f32x4 s2 = {0.f, 0.f, 0.f, 0.f}, sd = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 off = smean[c4];
-  if (rg < RP) {
-    for (long long row = r_begin + rg; row < r_end; row += RP) {
+  const f32x4 off = soff[lane];
+  f32x4 sd = {0.f, 0.f, 0.f, 0.f}, s2 = sd;
+  if (cok) {
+    for (long long row = r_begin + rg; row < r_end; row += kRowGroups) {
       const f32x4 d = (load(row * C + 4 * c4) - K) - off;
       sd += d;
       s2 += d * d;
     }
   }
-  __shared__ f32x4 sh2[256];
+  __syncthreads();
   sh[t] = sd;
   sh2[t] = s2;
   __syncthreads();
-  if (rg == 0) {
-    for (int k = 1; k < RP; ++k) { sd += sh[k * L + c4]; s2 += sh2[k * L + c4]; }
-    const double n = (double)(r_end - r_begin);
+  if (rg == 0 && cok) {
+    for (int k = 1; k < kRowGroups; ++k) { sd += sh[k * 16 + lane]; s2 += sh2[k * 16 + lane]; }
     f32x4 lo, m2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       lo[j] = (float)((double)off[j] + (double)sd[j] / n);
       m2[j] = (float)((double)s2[j] - (double)sd[j] * (double)sd[j] / n);
     }
-    const long long G = gridDim.x;
+    const long long plane = (long long)gridDim.x * C;
     st4(part + (long long)blockIdx.x * C + 4 * c4, K);
-    st4(part + (G + blockIdx.x) * C + 4 * c4, lo);
-    st4(part + (2 * G + blockIdx.x) * C + 4 * c4, m2);
+    st4(part + plane + (long long)blockIdx.x * C + 4 * c4, lo);
+    st4(part + 2 * plane + (long long)blockIdx.x * C + 4 * c4, m2);
   }
 }
 
-__global__ __launch_bounds__(256) void k_bn_stats_final(long long M, int C, int G, long long rows_per_block,
-                                                        const float* __restrict__ part, float* __restrict__ rmean,
-                                                        float* __restrict__ rvar, float momentum, float eps,
-                                                        float* __restrict__ smean, float* __restrict__ sinv) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  // Chan et al. pairwise-free merge in block order: (n, mean, M2) += (n_b, mean_b, M2_b)
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int g = 0; g < G; ++g) {
-    const double nb = (double)min(rows_per_block, M - (long long)g * rows_per_block);
-    const double mb = (double)part[(long long)g * C + c] + (double)part[((long long)G + g) * C + c];
-    const double m2b = (double)part[(2LL * G + g) * C + c];
-    const double tot = n + nb;
-    const double delta = mb - mean;
-    mean += delta * (nb / tot);
-    m2 += m2b + delta * delta * (n * nb / tot);
-    n = tot;
+// per-channel merge of G partial tiles (8 channels x 32 tile-groups per workgroup, double)
+__global__ __launch_bounds__(256) void k_bn_finalize(long long M, int C, int G, long long rows_per_tile,
+                                                     const float* __restrict__ part, float* __restrict__ rmean,
+                                                     float* __restrict__ rvar, float momentum, float eps,
+                                                     float* __restrict__ smean, float* __restrict__ sinv) {
+  __shared__ double red[256];
+  __shared__ double smu[8];
+  const int t = threadIdx.x;
+  const int cl = t & 7, gg = t >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  const bool cok = c < C;
+  const long long plane = (long long)G * C;
+  double s = 0.0;
+  if (cok)
+    for (int g = gg; g < G; g += 32) {
+      const double nb = (double)min(rows_per_tile, M - (long long)g * rows_per_tile);
+      const double mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
+      s += nb * mb;
+    }
+  red[t] = s;
+  __syncthreads();
+  for (int w = 16; w > 0; w >>= 1) {
+    if (gg < w) red[t] += red[t + w * 8];
+    __syncthreads();
   }
-  double var = m2 / n;
-  if (var < 0.0) var = 0.0;
-  const float fmean = (float)mean, fvar = (float)var;
-  smean[c] = fmean;
-  sinv[c] = 1.0f / sqrtf(fvar + eps);
-  if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
-  if (rvar) {
-    const float unb = M > 1 ? (float)(m2 / (n - 1.0)) : fvar;
-    rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+  if (gg == 0) smu[cl] = red[cl] / (double)M;
+  __syncthreads();
+  const double mean = smu[cl];
+  double q = 0.0;
+  if (cok)
+    for (int g = gg; g < G; g += 32) {
+      const double nb = (double)min(rows_per_tile, M - (long long)g * rows_per_tile);
+      const double mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
+      const double m2b = (double)part[2 * plane + (long long)g * C + c];
+      q += m2b + nb * (mb - mean) * (mb - mean);
+    }
+  __syncthreads();
+  red[t] = q;
+  __syncthreads();
+  for (int w = 16; w > 0; w >>= 1) {
+    if (gg < w) red[t] += red[t + w * 8];
+    __syncthreads();
+  }
+  if (gg == 0 && cok) {
+    const double n = (double)M;
+    double var = red[cl] / n;
+    if (var < 0.0) var = 0.0;
+    const float fmean = (float)mean, fvar = (float)var;
+    smean[c] = fmean;
+    sinv[c] = 1.0f / sqrtf(fvar + eps);
+    if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
+    if (rvar) {
+      const float unb = M > 1 ? (float)(red[cl] / (n - 1.0)) : fvar;
+      rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+    }
   }
 }
 
@@ -171,7 +197,7 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
 }
 
 // ------------------------------------------------------------------------------------------------
-// backward: partial sums of g', g'*(y-mean) [, g'*(y2-mean2)]
+// backward: partial sums of g', g'*(y-mean) [, g'*(y2-mean2)] over [rows x 64 channels] tiles
 // ------------------------------------------------------------------------------------------------
 template <bool HAS_OUT, bool TWO>
 __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
@@ -180,16 +206,17 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
                                                         const float* __restrict__ mean2, long long rows_per_block,
                                                         float* __restrict__ part) {
   __shared__ f32x4 sh[3][256];
-  const int L = C >> 2, RP = 256 / L;
   const int t = threadIdx.x;
-  const int c4 = t % L, rg = t / L;
+  const int lane = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + lane;
+  const bool cok = 4 * c4 < C;
   const long long r_begin = blockIdx.x * rows_per_block;
   const long long r_end = min(M, r_begin + rows_per_block);
   f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sx = sg, sx2 = sg;
-  if (rg < RP) {
+  if (cok) {
     const f32x4 mu = ld4(mean + 4 * c4);
     const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (long long row = r_begin + rg; row < r_end; row += RP) {
+    for (long long row = r_begin + rg; row < r_end; row += kRowGroups) {
       const long long off = row * C + 4 * c4;
       f32x4 gv = ld4(g + off);
       if (HAS_OUT) {
@@ -206,34 +233,55 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
   sh[1][t] = sx;
   if (TWO) sh[2][t] = sx2;
   __syncthreads();
-  if (rg == 0) {
-    for (int k = 1; k < RP; ++k) {
-      sg += sh[0][k * L + c4];
-      sx += sh[1][k * L + c4];
-      if (TWO) sx2 += sh[2][k * L + c4];
+  if (rg == 0 && cok) {
+    for (int k = 1; k < kRowGroups; ++k) {
+      sg += sh[0][k * 16 + lane];
+      sx += sh[1][k * 16 + lane];
+      if (TWO) sx2 += sh[2][k * 16 + lane];
     }
-    const long long G = gridDim.x;
+    const long long plane = (long long)gridDim.x * C;
     st4(part + (long long)blockIdx.x * C + 4 * c4, sg);
-    st4(part + (G + blockIdx.x) * C + 4 * c4, sx);
-    if (TWO) st4(part + (2 * G + blockIdx.x) * C + 4 * c4, sx2);
+    st4(part + plane + (long long)blockIdx.x * C + 4 * c4, sx);
+    if (TWO) st4(part + 2 * plane + (long long)blockIdx.x * C + 4 * c4, sx2);
   }
 }
 
-// coef layout [6][C]: ca, cb, cm (first BN), ca2, cb2, cm2 (second BN)
+// coef layout [6][C]: ca, cb, cm (first BN), ca2, cb2, cm2 (second BN); 8 channels x 32 groups
 __global__ __launch_bounds__(256) void k_bn_bwd_final(long long M, int C, int G, int two, const float* __restrict__ part,
                                                       const float* __restrict__ inv, const float* __restrict__ gamma,
                                                       const float* __restrict__ inv2, const float* __restrict__ gamma2,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       float* __restrict__ dgamma2, float* __restrict__ dbeta2,
                                                       float* __restrict__ coef) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ double red[3][256];
+  const int t = threadIdx.x;
+  const int cl = t & 7, gg = t >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  const bool cok = c < C;
+  const long long plane = (long long)G * C;
   double sg = 0.0, sx = 0.0, sx2 = 0.0;
-  for (int g = 0; g < G; ++g) {
-    sg += (double)part[(long long)g * C + c];
-    sx += (double)part[((long long)G + g) * C + c];
-    if (two) sx2 += (double)part[(2LL * G + g) * C + c];
+  if (cok)
+    for (int g = gg; g < G; g += 32) {
+      sg += (double)part[(long long)g * C + c];
+      sx += (double)part[plane + (long long)g * C + c];
+      if (two) sx2 += (double)part[2 * plane + (long long)g * C + c];
+    }
+  red[0][t] = sg;
+  red[1][t] = sx;
+  red[2][t] = sx2;
+  __syncthreads();
+  for (int w = 16; w > 0; w >>= 1) {
+    if (gg < w) {
+      red[0][t] += red[0][t + w * 8];
+      red[1][t] += red[1][t + w * 8];
+      red[2][t] += red[2][t + w * 8];
+    }
+    __syncthreads();
   }
+  if (gg != 0 || !cok) return;
+  sg = red[0][cl];
+  sx = red[1][cl];
+  sx2 = red[2][cl];
   const double n = (double)M;
   {
     const double iv = inv[c], ga = gamma[c];
@@ -293,13 +341,26 @@ int ew_blocks(long long n4) {
   return (int)(b < 1 ? 1 : b);
 }
 
-bool c_ok(int C) { return C >= 4 && C % 4 == 0 && C <= 1024; }
+bool c_ok(int C) { return C >= 4 && C % 4 == 0; }
 
 }  // namespace
 
+extern "C" int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t rows_per_tile, const float* partial,
+                                float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                                float* save_invstd, tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || ntiles <= 0 || rows_per_tile <= 0 || !partial || !save_mean || !save_invstd)
+    return TSPM_ERR_INVALID;
+  if ((long long)ntiles * rows_per_tile < m || (long long)(ntiles - 1) * rows_per_tile >= m) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, 8)), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)m, c,
+                     ntiles, (long long)rows_per_tile, partial, running_mean, running_var, momentum, eps, save_mean,
+                     save_invstd);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
 extern "C" size_t tspm_bn_stats_workspace(int64_t m, int32_t c) {
   if (m <= 0 || !c_ok(c)) return 0;
-  return (size_t)3 * stats_blocks(m, c) * c * sizeof(float);
+  return (size_t)3 * row_blocks(m, c) * c * sizeof(float);
 }
 
 extern "C" int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab, int64_t slab_stride, float* y_out,
@@ -309,17 +370,15 @@ extern "C" int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab
   if (nslab > 1 && !y_out) return TSPM_ERR_INVALID;
   if (!ws || ws_bytes < tspm_bn_stats_workspace(m, c)) return TSPM_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int G = stats_blocks(m, c);
+  const int G = row_blocks(m, c);
   const long long rpb = cdiv64(m, G);
   const int Greal = (int)cdiv64(m, rpb);
   float* part = static_cast<float*>(ws);
-  hipLaunchKernelGGL(k_bn_stats_partial, dim3(Greal), dim3(256), 0, st, (long long)m, c, y, nslab,
-                     (long long)slab_stride, y_out, rpb, part);
+  hipLaunchKernelGGL(k_bn_stats_partial, dim3(Greal, cdiv(c, kChanPerBlock)), dim3(256), 0, st, (long long)m, c, y,
+                     nslab, (long long)slab_stride, y_out, rpb, part);
   TSPM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_stats_final, dim3(cdiv(c, 256)), dim3(256), 0, st, (long long)m, c, Greal, rpb, part,
-                     running_mean, running_var, momentum, eps, save_mean, save_invstd);
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
+  return tspm_bn_finalize(m, c, Greal, rpb, part, running_mean, running_var, momentum, eps, save_mean, save_invstd,
+                          stream);
 }
 
 #define BN_APPLY_LAUNCH(RES, RELU, EVAL)                                                                   \
@@ -369,7 +428,7 @@ extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const fl
 
 extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
   if (m <= 0 || !c_ok(c)) return 0;
-  return ((size_t)3 * stats_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
+  return ((size_t)3 * row_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
 }
 
 extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y, const float* mean,
@@ -382,20 +441,21 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
   if (!ws || ws_bytes < tspm_bn_bwd_workspace(m, c)) return TSPM_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int G = stats_blocks(m, c);
+  const int G = row_blocks(m, c);
   const long long rpb = cdiv64(m, G);
   const int Greal = (int)cdiv64(m, rpb);
   float* part = static_cast<float*>(ws);
   float* coef = part + (size_t)3 * G * c;
   const bool ho = out != nullptr;
-#define BNB_P(HO, TW)                                                                                           \
-  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW>), dim3(Greal), dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
+  const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
+#define BNB_P(HO, TW)                                                                                     \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
                      y2, mean2, rpb, part)
   if (ho) { if (two) BNB_P(true, true); else BNB_P(true, false); }
   else { if (two) BNB_P(false, true); else BNB_P(false, false); }
 #undef BNB_P
   TSPM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 256)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
+  hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 8)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
                      invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, coef);
   TSPM_LAUNCH_CHECK();
   const long long n4 = (long long)m * c / 4;

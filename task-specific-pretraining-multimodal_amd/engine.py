@@ -44,11 +44,16 @@ class ConvOp:
 
     def ws_bytes(self, need_dgrad: bool) -> int:
         lib = L.lib()
-        b = max(lib.tspm_conv_fwd_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd)),
-                lib.tspm_conv_wgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_wgrad)))
+        b = lib.tspm_conv_wgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_wgrad))
         if need_dgrad:
             b = max(b, lib.tspm_conv_dgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_dgrad)))
         return b
+
+    def stat_tiles(self) -> Tuple[int, int]:
+        """(tiles, rows per tile) of the BN partial statistics the forward epilogue emits."""
+        lib = L.lib()
+        return (lib.tspm_conv_fwd_tiles(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd)),
+                lib.tspm_conv_fwd_tile_rows(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd)))
 
 
 @dataclass
@@ -176,6 +181,8 @@ class EncoderEngine:
         self.ws_bn_bytes = max(bn_ws, 256)
         self.ws_conv = torch.empty(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.empty(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
+        part = max(3 * op.stat_tiles()[0] * op.shape.k for op in self.all_convs())
+        self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
 
     def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
         """Override tile configs: key (kind, n,h,w,c,k,r,s,stride) -> (tm, tn, wm, wn, splits)."""
@@ -196,33 +203,26 @@ class EncoderEngine:
             raise L.TspmError("conv weight must be OHWI (channels_last); call prepare_encoder_layout() first")
         return w
 
-    def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> int:
-        """Run the conv; returns the number of slabs written (slabs live in ws_conv)."""
+    def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
+                  bn_partial: Optional[torch.Tensor] = None) -> None:
         lib = L.lib()
         s, a = op.shape, op.algo_fwd
-        need = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a))
         if self.conv_timer:
             self.conv_timer.begin(op, "fwd")
         L.check(lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x_ptr, ctypes.byref(strides), self._w(op).data_ptr(),
-                                  y.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_fwd")
+                                  y.data_ptr(), L.ptr(bn_partial), sh), "conv_fwd")
         if self.conv_timer:
             self.conv_timer.end()
-        if need == 0:
-            return 1
-        return need // (op.rows_out * s.k * 4)
-
-    def _bn_stats(self, bn: BNOp, y: torch.Tensor, nslab: int, sh: int) -> None:
-        lib = L.lib()
-        m = bn.module
-        src = self.ws_conv if nslab > 1 else y
-        L.check(lib.tspm_bn_stats(bn.rows, bn.channels, src.data_ptr(), nslab, bn.rows * bn.channels, y.data_ptr(),
-                                  L.ptr(m.running_mean), L.ptr(m.running_var), BN_MOMENTUM if m.momentum is None else m.momentum,
-                                  m.eps, bn.mean.data_ptr(), bn.invstd.data_ptr(), self.ws_bn.data_ptr(),
-                                  self.ws_bn_bytes, sh), "bn_stats")
 
     def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
-        nslab = self._conv_fwd(op, x_ptr, strides, y, sh)
-        self._bn_stats(bn, y, nslab, sh)
+        """conv forward whose epilogue emits BN partial statistics, then the per-channel merge."""
+        self._conv_fwd(op, x_ptr, strides, y, sh, self.bn_part)
+        tiles, rows = op.stat_tiles()
+        m = bn.module
+        L.check(L.lib().tspm_bn_finalize(bn.rows, bn.channels, tiles, rows, self.bn_part.data_ptr(),
+                                         L.ptr(m.running_mean), L.ptr(m.running_var),
+                                         BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
+                                         bn.invstd.data_ptr(), sh), "bn_finalize")
 
     def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True):
         lib = L.lib()
@@ -318,10 +318,7 @@ class EncoderEngine:
                 "linear_fwd(fc)")
 
     def _conv_fwd_eval(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
-        nslab = self._conv_fwd(op, x_ptr, strides, y, sh)
-        if nslab > 1:
-            L.check(L.lib().tspm_reduce_slabs(op.rows_out * op.shape.k, nslab, op.rows_out * op.shape.k,
-                                              self.ws_conv.data_ptr(), y.data_ptr(), sh), "reduce_slabs")
+        self._conv_fwd(op, x_ptr, strides, y, sh, None)
 
     # ---------------------------------------------------------------------------------------
     def _grad(self, p: torch.Tensor) -> torch.Tensor:

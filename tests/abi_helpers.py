@@ -45,14 +45,35 @@ def conv_fwd(x_nchw: torch.Tensor, w_oihw: torch.Tensor, stride: int, pad: int, 
     wd = w_oihw.contiguous(memory_format=torch.channels_last)
     y = torch.empty(shp.p * shp.q * n, k, device=dev)
     lib = L.lib()
-    wsb = lib.tspm_conv_fwd_workspace(ctypes.byref(shp), ctypes.byref(a))
-    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
     L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
-                              y.data_ptr(), ws.data_ptr(), wsb, sh()), "conv_fwd")
-    if wsb:
-        nsl = wsb // (y.numel() * 4)
-        L.check(lib.tspm_reduce_slabs(y.numel(), nsl, y.numel(), ws.data_ptr(), y.data_ptr(), sh()), "reduce")
+                              y.data_ptr(), None, sh()), "conv_fwd")
     return from_hwnc(y, n, shp.p, shp.q, k)
+
+
+def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0)):
+    """conv forward whose epilogue emits BN partials, merged by tspm_bn_finalize: returns
+    (y NCHW, mean, invstd)."""
+    n, c, h, w = x_nchw.shape
+    k, _, r, s = w_oihw.shape
+    shp = shape(n, h, w, c, k, r, s, stride, pad)
+    a = L.ConvAlgo(*algo)
+    dev = x_nchw.device
+    xd = to_hwnc(x_nchw)
+    st = L.hwnc_strides(n, h, w, c)
+    wd = w_oihw.contiguous(memory_format=torch.channels_last)
+    m = shp.p * shp.q * n
+    y = torch.empty(m, k, device=dev)
+    lib = L.lib()
+    tiles = lib.tspm_conv_fwd_tiles(ctypes.byref(shp), ctypes.byref(a))
+    rows = lib.tspm_conv_fwd_tile_rows(ctypes.byref(shp), ctypes.byref(a))
+    part = torch.empty(3 * tiles * k, device=dev)
+    L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
+                              y.data_ptr(), part.data_ptr(), sh()), "conv_fwd")
+    mean = torch.empty(k, device=dev)
+    inv = torch.empty(k, device=dev)
+    L.check(lib.tspm_bn_finalize(m, k, tiles, rows, part.data_ptr(), None, None, 0.1, 1e-5, mean.data_ptr(),
+                                 inv.data_ptr(), sh()), "bn_finalize")
+    return from_hwnc(y, n, shp.p, shp.q, k), mean, inv
 
 
 def conv_dgrad(dy_nchw: torch.Tensor, w_oihw: torch.Tensor, in_hw, stride: int, pad: int, algo=(0, 0, 0, 0, 0),

@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "tspm.h")
 
 def header_prototypes():
     src = open(HEADER).read()
-    return dict(re.findall(r"\n(?:int|size_t|const char\*)\s+(tspm_\w+)\(([^;]*?)\);", src, re.S))
+    return dict(re.findall(r"\n(?:int|int32_t|size_t|const char\*)\s+(tspm_\w+)\(([^;]*?)\);", src, re.S))
 
 
 def test_library_loads_and_version():
@@ -49,12 +49,14 @@ def test_invalid_arguments_are_rejected_before_launch():
     lib = L.load()
     s = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 7, 8)  # wrong p
     a = L.ConvAlgo()
-    assert lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), 1, None, 1, 1, None, 0, None) == 1
-    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a)) == 0
+    assert lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), 1, None, 1, 1, None, None) == 1
+    assert lib.tspm_conv_fwd_tiles(ctypes.byref(s), ctypes.byref(a)) == 0
     good = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
-    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, 0, None) == 1
-    bad_algo = L.ConvAlgo(3, 1, 4, 1, 1)
-    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, 0, None) == 1
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, None) == 1
+    for bad in [(3, 1, 1, 1, 1), (2, 1, 1, 1, 1), (1, 1, 3, 1, 1), (1, 1, 2, 8, 1), (1, 1, 1, 16, 1)]:
+        bad_algo = L.ConvAlgo(*bad)
+        assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, None) == 1, bad
+    assert lib.tspm_bn_finalize(128, 64, 2, 32, 16, None, None, 0.1, 1e-5, 16, 16, None) == 1  # tiles*rows < m
     # dgrad needs K % 8 == 0
     odd = L.ConvShape(2, 8, 8, 64, 12, 3, 3, 1, 1, 8, 8)
     assert lib.tspm_conv_dgrad(ctypes.byref(odd), ctypes.byref(a), 16, 16, 16, 0, None, 0, None) == 1
@@ -69,8 +71,10 @@ def test_invalid_arguments_are_rejected_before_launch():
 def test_workspace_queries():
     lib = L.load()
     s = L.ConvShape(128, 7, 7, 64, 64, 3, 3, 1, 1, 7, 7)
-    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 4, 1, 1))) == 0
-    w3 = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 4, 1, 3)))
-    assert w3 == 3 * 7 * 7 * 128 * 64 * 4
+    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 1))) == 0
+    assert lib.tspm_conv_fwd_tiles(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 1))) == 7 * 7 * 128 // 32
+    assert lib.tspm_conv_fwd_tile_rows(ctypes.byref(s), ctypes.byref(L.ConvAlgo(2, 2, 1, 1, 1))) == 64
+    w3 = lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 3)))
+    assert w3 == 3 * 64 * 9 * 64 * 4
     assert lib.tspm_bn_stats_workspace(6272, 64) > 0
     assert lib.tspm_bn_bwd_workspace(6272, 64) >= lib.tspm_bn_stats_workspace(6272, 64)

@@ -34,7 +34,8 @@ CONV_CASES = [
     (128, 256, 2, 2, 256, 3, 3, 1, 1),
     (128, 64, 7, 7, 64, 3, 3, 1, 1),
 ]
-ALGOS = [(0, 0, 0, 0, 0), (1, 1, 4, 1, 1), (2, 2, 2, 2, 3), (1, 2, 1, 4, 2), (2, 1, 4, 1, 5)]
+# (tm, tn, wn, wk, splits): tile shape, waves along N per workgroup, in-workgroup split-K, wgrad split
+ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1, 1, 4, 2, 1), (1, 2, 2, 4, 1)]
 
 
 def _check(out, ref, bound, what):
@@ -59,7 +60,7 @@ def test_conv_fwd(gpu, case, algo):
 
 
 @pytest.mark.parametrize("case", [(4, 1, 32, 94), (8, 1, 28, 28), (3, 1, 13, 9)])
-@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 4, 1, 1), (1, 2, 2, 2, 4)])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 1, 1, 1), (1, 2, 2, 4, 1)])
 def test_stem_fwd_nchw_input(gpu, case, algo):
     """7x7/2 stem reading the reference's NCHW input in place; spectrogram-like dynamic range."""
     n, c, h, w = case
@@ -72,7 +73,7 @@ def test_stem_fwd_nchw_input(gpu, case, algo):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS[:3])
+@pytest.mark.parametrize("algo", ALGOS[:4])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_conv_dgrad(gpu, case, algo, beta):
     n, c, h, w, k, r, s, st, pad = case
@@ -92,7 +93,7 @@ def test_conv_dgrad(gpu, case, algo, beta):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS[:3] + [(1, 1, 1, 4, 7)])
+@pytest.mark.parametrize("algo", ALGOS[:3] + [(1, 1, 1, 4, 7), (2, 2, 2, 2, 3), (1, 2, 4, 1, 16)])
 def test_conv_wgrad(gpu, case, algo):
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(13)
@@ -117,6 +118,27 @@ def test_stem_wgrad_nchw_input(gpu, case):
     bound = torch.nn.grad.conv2d_weight(x.double().abs(), (64, c, 7, 7), dy.double().abs(), 2, 3)
     out = conv_wgrad(x.to(gpu), dy.to(gpu), (7, 7), 2, 3, nchw_input=True)
     _check(out, ref, bound, f"stem wgrad {case}")
+
+
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 5, 6, 8, 12)])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 2, 2, 1), (1, 1, 1, 8, 1)])
+@pytest.mark.parametrize("offset", [0.0, 3e4])
+def test_conv_fwd_epilogue_bn_statistics(gpu, case, algo, offset):
+    """BatchNorm batch statistics of the conv output from the conv epilogue's per-tile partials."""
+    from abi_helpers import conv_fwd_with_stats
+    n, c, h, w, k, r, s, st, pad = case
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(n, c, h, w, generator=g) + offset / 100
+    wt = torch.randn(k, c, r, s, generator=g) * 0.05
+    wt[:, :, r // 2, s // 2] += offset / (c * 100)  # push channel means far from zero
+    y, mean, inv = conv_fwd_with_stats(x.to(gpu), wt.to(gpu), st, pad, algo)
+    torch.cuda.synchronize()
+    yd = y.double().cpu()
+    mean_ref = yd.mean((0, 2, 3))
+    var_ref = yd.var((0, 2, 3), unbiased=False)
+    scale = yd.abs().amax((0, 2, 3)) + 1
+    assert ((mean.double().cpu() - mean_ref).abs() <= 1e-6 * scale).all()
+    assert torch.allclose(inv.double().cpu(), 1 / torch.sqrt(var_ref + 1e-5), rtol=1e-4)
 
 
 # ------------------------------------------------------------------------------------------------
