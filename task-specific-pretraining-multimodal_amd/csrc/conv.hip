@@ -560,51 +560,53 @@ struct Algo {
 int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 int pow2_floor(int v) { int p = 1; while (p * 2 <= v) p *= 2; return p; }
 
-// heuristic: aim for >= ~2048 waves in flight with >= 4 reduction iterations per wave
+// heuristic (used when no tuned table entry exists): spread over >= ~256 workgroups (one per CU)
+// with >= 4 waves each, 32x32 tiles when the output is small, >= 4 reduction iterations per wave
 Algo pick(const tspm_conv_algo* user, long long rows, long long cols, long long red_iters, bool allow_global) {
-  Algo a{1, cols >= 64 ? 2 : 1, 1, 1, 1};
+  Algo a{1, 1, 1, 1, 1};
   if (user && user->tm > 0) {
     a.tm = user->tm; a.tn = user->tn; a.wn = user->wn > 0 ? user->wn : 1; a.wk = user->wk > 0 ? user->wk : 1;
     a.splits = user->splits > 0 ? user->splits : 1;
     return a;
   }
-  if (rows >= 16384 && cols >= 64) a.tm = 2;
-  const long long tiles_n = cdiv64(cols, 32 * a.tn);
-  a.wn = tiles_n >= 2 ? 2 : 1;
-  const long long tiles = cdiv64(rows, 32 * a.tm) * tiles_n;
-  long long want = cdiv64(2048, tiles);
-  int wk = pow2_floor((int)std::min<long long>(want, 8));
-  while (wk > 1 && red_iters / wk < 4) wk /= 2;
-  if (a.wn * wk > 8) wk = 8 / a.wn;
+  if (cols >= 64 && rows * cols >= (long long)256 * 32 * 64) a.tn = 2;
+  if (a.tn == 2 && rows * cols >= (long long)512 * 64 * 64) a.tm = 2;
+  const long long tiles = cdiv64(rows, 32 * a.tm) * cdiv64(cols, 32 * a.tn);
+  int wk = 1;
+  while (wk < 8 && tiles * wk < 1024 && red_iters / (wk * 2) >= 4) wk *= 2;
   a.wk = wk;
+  a.wn = 1;
   if (allow_global) {
-    long long rem = cdiv64(want, wk);
-    int sp = (int)std::min<long long>(rem, 64);
-    while (sp > 1 && red_iters / (sp * wk) < 8) --sp;
+    long long want = cdiv64(1024, tiles * wk);
+    int sp = (int)std::min<long long>(want, 64);
+    while (sp > 1 && red_iters / ((long long)sp * wk) < 8) --sp;
     a.splits = sp < 1 ? 1 : sp;
   }
   return a;
 }
 
+size_t lds_bytes(const Algo& a) { return (size_t)(a.wk - 1) * a.wn * a.tm * a.tn * 16 * 64 * sizeof(float); }
+
 bool algo_supported(const Algo& a) {
   if (a.splits < 1) return false;
   if (!((a.tm == 1 && a.tn == 1) || (a.tm == 1 && a.tn == 2) || (a.tm == 2 && a.tn == 2))) return false;
   if (!(a.wn == 1 || a.wn == 2 || a.wn == 4)) return false;
-  if (!(a.wk == 1 || a.wk == 2 || a.wk == 4 || a.wk == 8)) return false;
-  return a.wn * a.wk <= 8;
+  if (!(a.wk == 1 || a.wk == 2 || a.wk == 4 || a.wk == 8 || a.wk == 16)) return false;
+  if (a.wk == 16 && a.wn != 1) return false;
+  if (a.wn * a.wk > 16 || (a.wn > 1 && a.wn * a.wk > 8)) return false;
+  return lds_bytes(a) <= 160 * 1024;
 }
-
-size_t lds_bytes(const Algo& a) { return (size_t)(a.wk - 1) * a.wn * a.tm * a.tn * 16 * 64 * sizeof(float); }
 
 #define TSPM_L(KERNEL, TM_, TN_, WN_, WK_, F_, ...) \
   hipLaunchKernelGGL((KERNEL<TM_, TN_, WN_, WK_, F_>), grid, dim3(64 * WN_ * WK_), lds, st, __VA_ARGS__)
 
-#define TSPM_WK_SWITCH(KERNEL, TM_, TN_, WN_, F_, ...)                 \
-  switch (al.wk) {                                                     \
-    case 1: TSPM_L(KERNEL, TM_, TN_, WN_, 1, F_, __VA_ARGS__); break;  \
-    case 2: TSPM_L(KERNEL, TM_, TN_, WN_, 2, F_, __VA_ARGS__); break;  \
-    case 4: TSPM_L(KERNEL, TM_, TN_, WN_, 4, F_, __VA_ARGS__); break;  \
-    default: TSPM_L(KERNEL, TM_, TN_, WN_, 8, F_, __VA_ARGS__); break; \
+#define TSPM_WK_SWITCH(KERNEL, TM_, TN_, WN_, F_, ...)                  \
+  switch (al.wk) {                                                      \
+    case 1: TSPM_L(KERNEL, TM_, TN_, WN_, 1, F_, __VA_ARGS__); break;   \
+    case 2: TSPM_L(KERNEL, TM_, TN_, WN_, 2, F_, __VA_ARGS__); break;   \
+    case 4: TSPM_L(KERNEL, TM_, TN_, WN_, 4, F_, __VA_ARGS__); break;   \
+    case 8: TSPM_L(KERNEL, TM_, TN_, WN_, 8, F_, __VA_ARGS__); break;   \
+    default: TSPM_L(KERNEL, TM_, TN_, WN_, 16, F_, __VA_ARGS__); break; \
   }
 
 #define TSPM_WN_SWITCH(KERNEL, TM_, TN_, F_, ...)                                             \

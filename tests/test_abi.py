@@ -53,7 +53,7 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.tspm_conv_fwd_tiles(ctypes.byref(s), ctypes.byref(a)) == 0
     good = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
     assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, None) == 1
-    for bad in [(3, 1, 1, 1, 1), (2, 1, 1, 1, 1), (1, 1, 3, 1, 1), (1, 1, 2, 8, 1), (1, 1, 1, 16, 1)]:
+    for bad in [(3, 1, 1, 1, 1), (2, 1, 1, 1, 1), (1, 1, 3, 1, 1), (1, 1, 2, 8, 1), (1, 1, 2, 16, 1), (2, 2, 1, 16, 1)]:
         bad_algo = L.ConvAlgo(*bad)
         assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, None) == 1, bad
     assert lib.tspm_bn_finalize(128, 64, 2, 32, 16, None, None, 0.1, 1e-5, 16, 16, None) == 1  # tiles*rows < m
