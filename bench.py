@@ -9,8 +9,8 @@ all in fp32 on the libtspm HIP kernels (graph-replayed).
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
   roofline     — the conv implicit-GEMM kernel family (dominant: ~90 % of step FLOPs): valid-tap
                  FLOPs of every conv launch of one step ÷ the summed device time of those launches,
-                 timed with HIP events on the launching streams in an instrumented step run right
-                 after the timed region; peak = fp32 MFMA 157.3 TF/s.
+                 timed with HIP events in an instrumented eager step run right after the timed
+                 region with every launch on one stream (no concurrent kernels inside a bracket); peak = fp32 MFMA 157.3 TF/s.
   cpu_baseline — the oracle (CPU fp32 restatement of the reference train step, bit-identical to it
                  on CPU) timed on this host at batch 128, rank 0 / N=1 only.
 """
@@ -159,10 +159,12 @@ def main() -> None:
         eng.conv_timer = timer
     saved = step.use_graph
     step.use_graph = False
+    step.serial = True  # one stream: each conv's event pair brackets that kernel alone
     a, im, lab = batches[0]
     step.load_batch(a, im, lab)
     step.run()
     step.use_graph = saved
+    step.serial = False
     torch.cuda.synchronize()
     for eng in (step.eng_a, step.eng_i):
         eng.conv_timer = None

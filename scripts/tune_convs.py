@@ -1,0 +1,172 @@
+"""Measure every supported conv tile configuration on every distinct conv launch of the bench
+workload and write the fastest per (kind, shape) as a table the engine loads at plan time.
+
+    python scripts/tune_convs.py --batch 128 --out task-specific-pretraining-multimodal_amd/tuned/mi355x.json
+
+Each candidate is checked against the default configuration's output (max |diff| <= 1e-5 x max |y|)
+before it may win; timings are HIP events around back-to-back launches on one stream.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import itertools
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tspm_amd  # noqa: E402
+from tspm_amd import _lib as L  # noqa: E402
+from tspm_amd.engine import EncoderEngine, prepare_encoder_layout  # noqa: E402
+
+TILES = [(1, 1), (1, 2), (2, 2)]
+WNS = [1, 2, 4]
+WKS = [1, 2, 4, 8, 16]
+SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
+
+
+def candidates(kind):
+    for (tm, tn), wn, wk in itertools.product(TILES, WNS, WKS):
+        sps = SPLITS if kind == "wgrad" else [1]
+        for sp in sps:
+            yield (tm, tn, wn, wk, sp)
+
+
+def distinct_ops(batch, dev):
+    """(kind, ConvShape, input strides) of every conv launch of the late-fusion step."""
+    out = {}
+    encs = [(tspm_amd.ResNet18(1, 64), 32, 94, True), (tspm_amd.ResNet34(1, 128), 28, 28, False)]
+    for enc, h, w, three_d in encs:
+        enc = enc.to(dev)
+        prepare_encoder_layout(enc)
+        eng = EncoderEngine(enc, batch, h, w, dev)
+        for op in eng.all_convs():
+            s = op.shape
+            key = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad)
+            if op is eng.stem:
+                xs = L.Strides4(h * w, w, 1, 0) if three_d else L.Strides4(h * w, h * w, w, 1)
+                kinds = ("fwd", "wgrad")
+            else:
+                xs = L.hwnc_strides(s.n, s.h, s.w, s.c)
+                kinds = ("fwd", "dgrad", "wgrad")
+            for kind in kinds:
+                out.setdefault((kind,) + key, (s, xs, op is eng.stem))
+    return out
+
+
+class Bufs:
+    def __init__(self, s, stem, dev):
+        g = torch.Generator(device="cpu").manual_seed(0)
+        n_in = s.n * s.h * s.w * s.c
+        self.x = torch.randn(n_in, generator=g).abs_().to(dev) if stem else torch.randn(n_in, generator=g).to(dev)
+        self.w = (torch.randn(s.k * s.r * s.s * s.c, generator=g) * 0.05).to(dev)
+        self.y = torch.empty(s.n * s.p * s.q * s.k, device=dev)
+        self.dy = torch.randn(s.n * s.p * s.q * s.k, generator=g).to(dev)
+        self.dx = torch.empty(n_in, device=dev)
+        self.dw = torch.empty(s.k * s.r * s.s * s.c, device=dev)
+        self.part = torch.empty(3 * (s.n * s.p * s.q // 32 + 1) * s.k, device=dev)
+        self.ws = torch.empty(1, dtype=torch.uint8, device=dev)
+
+
+def launcher(kind, s, xs, b, algo):
+    lib = L.lib()
+    a = L.ConvAlgo(*algo)
+    sh = L.stream_handle()
+    if kind == "wgrad":
+        need = lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(a))
+        if need > b.ws.numel():
+            b.ws = torch.empty(need, dtype=torch.uint8, device=b.x.device)
+        wsb = b.ws.numel()
+
+        def f():
+            return lib.tspm_conv_wgrad(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs),
+                                       b.dy.data_ptr(), b.dw.data_ptr(), b.ws.data_ptr(), wsb, sh)
+        return f, b.dw
+    if kind == "dgrad":
+        def f():
+            return lib.tspm_conv_dgrad(ctypes.byref(s), ctypes.byref(a), b.dy.data_ptr(), b.w.data_ptr(),
+                                       b.dx.data_ptr(), 0, None, 0, sh)
+        return f, b.dx
+
+    def f():
+        return lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs), b.w.data_ptr(),
+                                 b.y.data_ptr(), b.part.data_ptr(), sh)
+    return f, b.y
+
+
+def time_launch(f, reps):
+    for _ in range(2):
+        if f() != 0:
+            return None
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    ops = distinct_ops(args.batch, dev)
+    table = []
+    t0 = time.time()
+    tot_def, tot_best = 0.0, 0.0
+    for key, (s, xs, stem) in sorted(ops.items(), key=lambda kv: str(kv[0])):
+        kind = key[0]
+        b = Bufs(s, stem, dev)
+        f, out = launcher(kind, s, xs, b, (0, 0, 0, 0, 0))
+        t_def = time_launch(f, args.reps)
+        ref = out.clone()
+        scale = float(ref.abs().max()) + 1e-30
+        best = ((0, 0, 0, 0, 0), t_def)
+        n_ok = 0
+        for algo in candidates(kind):
+            f, out = launcher(kind, s, xs, b, algo)
+            out.fill_(float("nan"))
+            if f() != 0:
+                continue
+            torch.cuda.synchronize()
+            err = float((out - ref).abs().max())
+            if not err <= 1e-5 * scale:
+                print(f"  MISMATCH {kind} {tuple(key[1:])} {algo} err={err:.3e} scale={scale:.3e}", flush=True)
+                continue
+            t = time_launch(f, args.reps)
+            if t is None:
+                continue
+            n_ok += 1
+            if t < best[1]:
+                best = (algo, t)
+        # confirm the winner with a longer run
+        f, _ = launcher(kind, s, xs, b, best[0])
+        t_best = time_launch(f, 3 * args.reps)
+        tot_def += t_def
+        tot_best += t_best
+        table.append({"kind": kind, "shape": list(key[1:]), "algo": list(best[0]), "us": round(t_best, 2),
+                      "default_us": round(t_def, 2), "candidates": n_ok})
+        print(f"{kind:5s} {str(tuple(key[1:])):42s} default {t_def:7.1f} us  best {t_best:7.1f} us  {best[0]}  "
+              f"({n_ok} ok, {time.time() - t0:.0f}s)", flush=True)
+        del b
+    print(f"sum over distinct launches: default {tot_def:.0f} us, tuned {tot_best:.0f} us", flush=True)
+    doc = {"device": torch.cuda.get_device_name(0), "batch": args.batch, "entries": table}
+    if args.out:
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+        with open(args.out, "w") as fh:
+            json.dump(doc, fh, indent=1)
+        print("wrote", args.out)
+
+
+if __name__ == "__main__":
+    main()

@@ -11,61 +11,103 @@ int grid_for(long long work) {
   return (int)(b < 1 ? 1 : b);
 }
 
-// y[n,o] = act(x[n,:] . w[o,:] + b[o]) * keep-scale
-__global__ __launch_bounds__(256) void k_linear_fwd(int N, int IN, int OUT, const float* __restrict__ x, int ldx,
-                                                    const float* __restrict__ w, const float* __restrict__ b,
-                                                    int relu, const uint8_t* __restrict__ keep, float kscale,
-                                                    float* __restrict__ y, int ldy) {
-  const long long total = (long long)N * OUT;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int o = (int)(i % OUT), n = (int)(i / OUT);
-    const float* xr = x + (long long)n * ldx;
-    const float* wr = w + (long long)o * IN;
-    float s = 0.f;
-    if ((IN & 3) == 0 && (ldx & 3) == 0) {
-      f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < IN; k += 4) s4 += ld4(xr + k) * ld4(wr + k);
-      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-    } else {
-      for (int k = 0; k < IN; ++k) s = fmaf(xr[k], wr[k], s);
+// Small fp32 GEMM on MFMA for the encoder fc and the fusion head (at batch 128 the largest is
+// 128x512x128): C[m,n] = epi(sum_k A(m,k) B(k,n)) with arbitrary element strides, so the three
+// products of nn.Linear (forward, input grad, weight grad) are one kernel without transposes.
+// One workgroup per 32x32 tile; WK waves split K and combine through LDS in fixed order
+// (deterministic).  Optional epilogue: + bias[n], ReLU, dropout keep mask (keep[m*N+n] ? x*scale : 0),
+// and rowsum[m] = sum_k A(m,k) (the bias gradient of the weight-grad product).
+struct GemmArgs {
+  int M, N, K;
+  const float* A; long long sam, sak;
+  const float* B; long long sbk, sbn;
+  float* C; long long ldc;
+  const float* bias;
+  int relu;
+  const uint8_t* keep;
+  float kscale;
+  float* rowsum;
+};
+
+template <int WK>
+__global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles_n = cdiv_dev(g.N, 32);
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int row = lane & 31, kh = lane >> 5;
+  const int m = tm * 32 + row, col = tn * 32 + row;
+  const int kchunk = ((cdiv_dev(g.K, WK) + 7) / 8) * 8;
+  const int kb = wave * kchunk, ke = min(g.K, kb + kchunk);
+  const bool mok = m < g.M, nok = col < g.N;
+  const float* Ap = g.A + (mok ? (long long)m * g.sam : 0);
+  const float* Bp = g.B + (nok ? (long long)col * g.sbn : 0);
+  const bool want_rs = g.rowsum != nullptr && tn == 0;
+  f32x16 acc = {};
+  float rs = 0.f;
+  for (int k0 = kb; k0 < ke; k0 += 8) {
+    float a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + 2 * j + kh;
+      const bool kok = k < ke;
+      a[j] = (mok && kok) ? Ap[(long long)k * g.sak] : 0.f;
+      b[j] = (nok && kok) ? Bp[(long long)k * g.sbk] : 0.f;
     }
-    if (b) s += b[o];
-    if (relu) s = fmaxf(s, 0.f);
-    if (keep) s = keep[(long long)n * OUT + o] ? s * kscale : 0.f;
-    y[(long long)n * ldy + o] = s;
-  }
-}
-
-// dx[n,i] = sum_o dy[n,o] w[o,i]
-__global__ __launch_bounds__(256) void k_linear_bwd_data(int N, int IN, int OUT, const float* __restrict__ dy,
-                                                         int ldy, const float* __restrict__ w, float* __restrict__ dx,
-                                                         int ldx) {
-  const long long total = (long long)N * IN;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
-    const int i = (int)(t % IN), n = (int)(t / IN);
-    const float* g = dy + (long long)n * ldy;
-    float s = 0.f;
-    for (int o = 0; o < OUT; ++o) s = fmaf(g[o], w[(long long)o * IN + i], s);
-    dx[(long long)n * ldx + i] = s;
-  }
-}
-
-// dw[o,i] = sum_n dy[n,o] x[n,i];  db[o] = sum_n dy[n,o]
-__global__ __launch_bounds__(256) void k_linear_bwd_weight(int N, int IN, int OUT, const float* __restrict__ x, int ldx,
-                                                           const float* __restrict__ dy, int ldy,
-                                                           float* __restrict__ dw, float* __restrict__ db) {
-  const long long total = (long long)OUT * IN;
-  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
-    const int i = (int)(t % IN), o = (int)(t / IN);
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s = fmaf(dy[(long long)n * ldy + o], x[(long long)n * ldx + i], s);
-    dw[t] = s;
-    if (db && i == 0) {
-      float sb = 0.f;
-      for (int n = 0; n < N; ++n) sb += dy[(long long)n * ldy + o];
-      db[o] = sb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc = mfma32(a[j], b[j], acc);
+      rs += a[j];
     }
   }
+  if (want_rs) rs += __shfl_xor(rs, 32, 64);
+  if (WK > 1) {
+    if (wave > 0) {
+      float* dst = lds + (wave - 1) * (16 * 64 + 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[r * 64 + lane] = acc[r];
+      if (lane < 32) dst[16 * 64 + lane] = rs;
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int w = 1; w < WK; ++w) {
+      const float* src = lds + (w - 1) * (16 * 64 + 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += src[r * 64 + lane];
+      rs += src[16 * 64 + row];
+    }
+  }
+  const int ccol = tn * 32 + (lane & 31);
+  if (ccol < g.N) {
+    const float bv = g.bias ? g.bias[ccol] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int cm = tm * 32 + acc_row(r, lane);
+      if (cm >= g.M) continue;
+      float v = acc[r] + bv;
+      if (g.relu) v = fmaxf(v, 0.f);
+      if (g.keep) v = g.keep[(long long)cm * g.N + ccol] ? v * g.kscale : 0.f;
+      g.C[(long long)cm * g.ldc + ccol] = v;
+    }
+  }
+  if (want_rs && lane < 32 && mok) g.rowsum[m] = rs;
+}
+
+int gemm_small(const GemmArgs& g, hipStream_t st) {
+  const int tiles = cdiv(g.M, 32) * cdiv(g.N, 32);
+  int wk = 1;
+  while (wk < 16 && g.K / (wk * 2) >= 32) wk *= 2;
+  const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  switch (wk) {
+    case 1: hipLaunchKernelGGL(k_gemm_small<1>, dim3(tiles), dim3(64), lds, st, g); break;
+    case 2: hipLaunchKernelGGL(k_gemm_small<2>, dim3(tiles), dim3(128), lds, st, g); break;
+    case 4: hipLaunchKernelGGL(k_gemm_small<4>, dim3(tiles), dim3(256), lds, st, g); break;
+    case 8: hipLaunchKernelGGL(k_gemm_small<8>, dim3(tiles), dim3(512), lds, st, g); break;
+    default: hipLaunchKernelGGL(k_gemm_small<16>, dim3(tiles), dim3(1024), lds, st, g); break;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
 }
 
 __global__ __launch_bounds__(256) void k_act_bwd(int N, int COLS, float* __restrict__ g, int ldg,
@@ -210,29 +252,25 @@ extern "C" int tspm_linear_fwd(int32_t n, int32_t in, int32_t out, const float* 
                                const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
                                int32_t ldy, tspm_stream_t stream) {
   if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !w || !y) return TSPM_ERR_INVALID;
-  if ((in & 3) == 0 && (ldx & 3) == 0 && !(aligned16(x) && aligned16(w))) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_linear_fwd, dim3(grid_for((long long)n * out)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     n, in, out, x, ldx, w, b, relu, keep, keep_scale, y, ldy);
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
+  // y[n,o] = sum_i x[n,i] w[o,i]:  A = x (m=n, k=i), B(k=i, n=o) = w[o,i]
+  GemmArgs g{n, out, in, x, ldx, 1, w, 1, in, y, ldy, b, relu, keep, keep_scale, nullptr};
+  return gemm_small(g, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,
                                     float* dx, int32_t ldx, tspm_stream_t stream) {
   if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !dy || !w || !dx) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_linear_bwd_data, dim3(grid_for((long long)n * in)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), n, in, out, dy, ldy, w, dx, ldx);
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
+  // dx[n,i] = sum_o dy[n,o] w[o,i]
+  GemmArgs g{n, in, out, dy, ldy, 1, w, in, 1, dx, ldx, nullptr, 0, nullptr, 1.f, nullptr};
+  return gemm_small(g, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy,
                                       int32_t ldy, float* dw, float* db, tspm_stream_t stream) {
   if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !dy || !dw) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_linear_bwd_weight, dim3(grid_for((long long)out * in)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), n, in, out, x, ldx, dy, ldy, dw, db);
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
+  // dw[o,i] = sum_n dy[n,o] x[n,i]  (A(m=o, k=n) = dy[n,o]);  db[o] = sum_n dy[n,o]
+  GemmArgs g{out, in, n, dy, 1, ldy, x, ldx, 1, dw, in, nullptr, 0, nullptr, 1.f, db};
+  return gemm_small(g, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,

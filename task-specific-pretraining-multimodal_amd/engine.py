@@ -9,6 +9,9 @@ whole step can be captured into a HIP graph.
 from __future__ import annotations
 
 import ctypes
+import glob
+import json
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -18,6 +21,26 @@ from . import _lib as L
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+
+
+_TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+_tuned_cache: Optional[Dict[Tuple, Tuple[int, int, int, int, int]]] = None
+
+
+def tuned_table() -> Dict[Tuple, Tuple[int, int, int, int, int]]:
+    """Measured tile configurations (scripts/tune_convs.py output under ``tuned/``), keyed
+    (kind, n, h, w, c, k, r, s, stride).  ``TSPM_TUNED=0`` disables them (library heuristic)."""
+    global _tuned_cache
+    if os.environ.get("TSPM_TUNED", "1") == "0":
+        return {}
+    if _tuned_cache is None:
+        _tuned_cache = {}
+        for path in sorted(glob.glob(os.path.join(_TUNED_DIR, "*.json"))):
+            with open(path) as fh:
+                doc = json.load(fh)
+            for e in doc.get("entries", []):
+                _tuned_cache[(e["kind"],) + tuple(e["shape"][:8])] = tuple(e["algo"])
+    return _tuned_cache
 
 
 def _out_hw(h: int, w: int, k: int, s: int, p: int) -> Tuple[int, int]:
@@ -79,6 +102,11 @@ class BlockPlan:
     y2: torch.Tensor = None
     yd: Optional[torch.Tensor] = None
     out: torch.Tensor = None
+    # backward: per-block gradients of the conv outputs (read by the weight-grad convs, which may
+    # run on the auxiliary stream while the data-grad chain moves on to the next block)
+    g_y1: torch.Tensor = None
+    g_y2: torch.Tensor = None
+    g_yd: Optional[torch.Tensor] = None
 
 
 class EncoderEngine:
@@ -90,6 +118,9 @@ class EncoderEngine:
         self.N, self.H, self.W = batch, height, width
         self.device = device
         self.grad_of = grad_of or _default_grad_of
+        # optional second stream: weight-grad convs and the downsample branch run there, off the
+        # critical path (set by FusedTrainStep; None = everything on the caller's stream)
+        self.aux: Optional[torch.cuda.Stream] = None
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
@@ -128,8 +159,11 @@ class EncoderEngine:
                 bp.a1 = torch.empty(rows, planes, **f32)
                 bp.y2 = torch.empty(rows, planes, **f32)
                 bp.out = torch.empty(rows, planes, **f32)
+                bp.g_y1 = torch.empty(rows * planes, **f32)
+                bp.g_y2 = torch.empty(rows * planes, **f32)
                 if bp.ds_conv is not None:
                     bp.yd = torch.empty(rows, planes, **f32)
+                    bp.g_yd = torch.empty(rows * planes, **f32)
                 self.blocks.append(bp)
                 h, w, c = ho, wo, planes
         self.final_hw = (h, w)
@@ -147,15 +181,12 @@ class EncoderEngine:
         max_blk = max(max_blk, self.mp.numel())
         self.gA = torch.empty(max_blk, **f32)
         self.gB = torch.empty(max_blk, **f32)
-        self.d1 = torch.empty(max_blk, **f32)
-        self.d2 = torch.empty(max_blk, **f32)
-        self.dd = torch.empty(max_blk, **f32)
         self.da1 = torch.empty(max_blk, **f32)
         self.g_stem = torch.empty(self.a0.numel(), **f32)
         self.dy_stem = torch.empty(self.a0.numel(), **f32)
         self.g_pooled = torch.empty(N, c, **f32)
         self.g_final = torch.empty(h * w * N * c, **f32)
-        self._alloc_workspace()
+        self.set_algos(tuned_table())
 
     # ---------------------------------------------------------------------------------------
     def all_convs(self) -> List[ConvOp]:
@@ -183,6 +214,9 @@ class EncoderEngine:
         self.ws_bn = torch.empty(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
         part = max(3 * op.stat_tiles()[0] * op.shape.k for op in self.all_convs())
         self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
+        ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
+        part_ds = max([3 * op.stat_tiles()[0] * op.shape.k for op in ds] + [1])
+        self.bn_part_aux = torch.empty(part_ds, device=self.device, dtype=torch.float32)
 
     def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
         """Override tile configs: key (kind, n,h,w,c,k,r,s,stride) -> (tm, tn, wm, wn, splits)."""
@@ -214,12 +248,14 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
-    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
+    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
+                 part: Optional[torch.Tensor] = None) -> None:
         """conv forward whose epilogue emits BN partial statistics, then the per-channel merge."""
-        self._conv_fwd(op, x_ptr, strides, y, sh, self.bn_part)
+        part = self.bn_part if part is None else part
+        self._conv_fwd(op, x_ptr, strides, y, sh, part)
         tiles, rows = op.stat_tiles()
         m = bn.module
-        L.check(L.lib().tspm_bn_finalize(bn.rows, bn.channels, tiles, rows, self.bn_part.data_ptr(),
+        L.check(L.lib().tspm_bn_finalize(bn.rows, bn.channels, tiles, rows, part.data_ptr(),
                                          L.ptr(m.running_mean), L.ptr(m.running_var),
                                          BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
                                          bn.invstd.data_ptr(), sh), "bn_finalize")
@@ -290,6 +326,16 @@ class EncoderEngine:
         for bp in self.blocks:
             s1 = bp.conv1.shape
             xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
+            fork = bp.ds_conv is not None and self.aux is not None
+            if fork:  # downsample conv + BN statistics concurrently with conv1 -> bn1 -> conv2
+                main = torch.cuda.current_stream()
+                self.aux.wait_stream(main)
+                with torch.cuda.stream(self.aux):
+                    ash = self.aux.cuda_stream
+                    if train:
+                        self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, ash, self.bn_part_aux)
+                    else:
+                        self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, ash)
             if train:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
@@ -302,7 +348,9 @@ class EncoderEngine:
             else:
                 self._conv_fwd_eval(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             if bp.ds_conv is not None:
-                if train:
+                if fork:
+                    main.wait_stream(self.aux)
+                elif train:
                     self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
                 else:
                     self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
@@ -343,11 +391,20 @@ class EncoderEngine:
         gw = self._grad(op.module.weight)
         if not gw.is_contiguous(memory_format=torch.channels_last):
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
+        if self.aux is not None:  # off the critical path: only Adam consumes weight gradients
+            self.aux.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.aux):
+                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream)
+        else:
+            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh)
+
+    def _wgrad_launch(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, gw: torch.Tensor,
+                      sh: int) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "wgrad")
-        L.check(lib.tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides),
-                                    dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh),
-                "conv_wgrad")
+        L.check(L.lib().tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr,
+                                        ctypes.byref(strides), dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(),
+                                        self.ws_conv_bytes, sh), "conv_wgrad")
         if self.conv_timer:
             self.conv_timer.end()
 
@@ -386,9 +443,9 @@ class EncoderEngine:
             n_in = xin.numel()
             Gv = G[:n_out]
             Gnv = Gn[:n_in]
-            d2 = self.d2[:n_out]
+            d2 = bp.g_y2
             if bp.ds_conv is not None:
-                dd = self.dd[:n_out]
+                dd = bp.g_yd
                 self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
@@ -397,7 +454,7 @@ class EncoderEngine:
             self._wgrad(bp.conv2, bp.a1.data_ptr(), L.hwnc_strides(N, s2.h, s2.w, s2.c), d2, sh)
             da1 = self.da1[:n_out]
             self._dgrad(bp.conv2, d2, da1, 0, sh)
-            d1 = self.d1[:n_out]
+            d1 = bp.g_y1
             self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
             if self.debug_hook is not None:
                 self.debug_hook(f"block{i}.g_out", Gv)
@@ -417,6 +474,8 @@ class EncoderEngine:
                                      self.g_stem.data_ptr(), sh), "maxpool_bwd")
         self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
         self._wgrad(self.stem, self.x_in.data_ptr(), self.input_strides(self.x_in), self.dy_stem, sh)
+        if self.aux is not None:
+            torch.cuda.current_stream().wait_stream(self.aux)
 
 
 def _default_grad_of(p: torch.Tensor) -> torch.Tensor:

@@ -110,6 +110,11 @@ class FusedTrainStep:
             self.nbt[i] = m.num_batches_tracked.to(dev)
             m.num_batches_tracked = self.nbt[i]
         self.side = torch.cuda.Stream(device=dev)
+        # per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in all,
+        # matching the 4 hardware queues HIP gives a process by default
+        self.aux_a = torch.cuda.Stream(device=dev)
+        self.aux_i = torch.cuda.Stream(device=dev)
+        self.serial = False  # True: every launch on the caller's stream (per-kernel timing)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.calls = 0
@@ -171,22 +176,25 @@ class FusedTrainStep:
         """Enqueue forward + loss + backward on the current stream (+ the side stream)."""
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side = main if self.serial else self.side
+        self.eng_a.aux = None if self.serial else self.aux_a
+        self.eng_i.aux = None if self.serial else self.aux_i
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
         self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-        main.wait_stream(self.side)
+        main.wait_stream(side)
         sh = main.cuda_stream
         self._head_fwd(sh)
         L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
                                            self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
                                            self.stats.data_ptr(), sh), "cross_entropy")
         self._head_bwd(sh)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
             self.eng_i.backward(self.dfused[:, ea:], self.F)
         self.eng_a.backward(self.dfused, self.F)
-        main.wait_stream(self.side)
+        main.wait_stream(side)
         self.nbt.add_(1)
 
     def _opt(self) -> None:

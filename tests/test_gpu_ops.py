@@ -35,7 +35,8 @@ CONV_CASES = [
     (128, 64, 7, 7, 64, 3, 3, 1, 1),
 ]
 # (tm, tn, wn, wk, splits): tile shape, waves along N per workgroup, in-workgroup split-K, wgrad split
-ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1, 1, 4, 2, 1), (1, 2, 2, 4, 1)]
+ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1, 1, 4, 2, 1), (1, 2, 2, 4, 1),
+         (1, 1, 1, 16, 1), (1, 2, 1, 16, 1)]
 
 
 def _check(out, ref, bound, what):
@@ -73,7 +74,7 @@ def test_stem_fwd_nchw_input(gpu, case, algo):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS[:4])
+@pytest.mark.parametrize("algo", ALGOS[:4] + ALGOS[6:])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_conv_dgrad(gpu, case, algo, beta):
     n, c, h, w, k, r, s, st, pad = case
@@ -93,7 +94,8 @@ def test_conv_dgrad(gpu, case, algo, beta):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS[:3] + [(1, 1, 1, 4, 7), (2, 2, 2, 2, 3), (1, 2, 4, 1, 16)])
+@pytest.mark.parametrize("algo", ALGOS[:3] + [(1, 1, 1, 4, 7), (2, 2, 2, 2, 3), (1, 2, 4, 1, 16),
+                                             (1, 1, 1, 16, 5), (1, 2, 1, 16, 2)])
 def test_conv_wgrad(gpu, case, algo):
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(13)
@@ -332,7 +334,7 @@ def test_avgpool(gpu, npos, n, c):
 # ------------------------------------------------------------------------------------------------
 # linear / CE / Adam
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("n,i,o", [(128, 512, 64), (4, 192, 128), (33, 64, 10)])
+@pytest.mark.parametrize("n,i,o", [(128, 512, 64), (4, 192, 128), (33, 64, 10), (128, 512, 128), (1000, 7, 3)])
 def test_linear(gpu, n, i, o):
     from tspm_amd import _lib as L
     lib = L.lib()
@@ -436,3 +438,27 @@ def test_image_lut_and_dropout(gpu, lut):
     frac = keep.float().mean().item()
     assert 0.49 < frac < 0.51
     assert (keep != keep2).float().mean().item() > 0.4
+
+
+def test_linear_strided_rows(gpu):
+    """The head reads/writes column slices of the [N,192] concat buffer: ldx/ldy > width."""
+    from tspm_amd import _lib as L
+    lib = L.lib()
+    g = torch.Generator().manual_seed(5)
+    n, i, o, ldx, ldy = 96, 64, 40, 192, 200
+    xb = torch.randn(n, ldx, generator=g)
+    w = torch.randn(o, i, generator=g) * 0.1
+    xd, wd = xb.to(gpu), w.to(gpu)
+    y = torch.full((n, ldy), 7.0, device=gpu)
+    L.check(lib.tspm_linear_fwd(n, i, o, xd[:, 64:].data_ptr(), ldx, wd.data_ptr(), None, 0, None, 1.0,
+                                y.data_ptr(), ldy, sh()), "lin fwd")
+    gy = torch.randn(n, ldy, generator=g)
+    gyd = gy.to(gpu)
+    dw = torch.empty(o, i, device=gpu)
+    L.check(lib.tspm_linear_bwd_weight(n, i, o, xd[:, 64:].data_ptr(), ldx, gyd.data_ptr(), ldy, dw.data_ptr(), None,
+                                       sh()), "lin wgrad")
+    torch.cuda.synchronize()
+    x = xb[:, 64:64 + i].double()
+    assert torch.allclose(y[:, :o].double().cpu(), x @ w.double().T, rtol=1e-5, atol=1e-4)
+    assert torch.equal(y[:, o:].cpu(), torch.full((n, ldy - o), 7.0))
+    assert torch.allclose(dw.double().cpu(), gy[:, :o].double().T @ x, rtol=1e-5, atol=1e-4)
