@@ -159,12 +159,13 @@ def main() -> None:
         eng.conv_timer = timer
     saved = step.use_graph
     step.use_graph = False
+    saved_serial = step.serial
     step.serial = True  # one stream: each conv's event pair brackets that kernel alone
     a, im, lab = batches[0]
     step.load_batch(a, im, lab)
     step.run()
     step.use_graph = saved
-    step.serial = False
+    step.serial = saved_serial
     torch.cuda.synchronize()
     for eng in (step.eng_a, step.eng_i):
         eng.conv_timer = None

@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 3 */
+int tspm_abi_version(void);  /* 5 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -57,8 +57,9 @@ typedef struct tspm_conv_shape {
  * a workgroup holds wn x wk waves: wn neighbouring column tiles of the same rows and wk waves that
  * split the reduction of one tile and combine through LDS in fixed order (deterministic, no
  * workspace).  splits: additional split of the wgrad reduction over workgroups (fp32 slabs, summed
- * in slab order).  Supported: (tm,tn) in {(1,1),(1,2),(2,2)}, wn in {1,2,4}, wk in {1,2,4,8},
- * wn*wk <= 8.  All-zero fields select the built-in heuristic. */
+ * in slab order).  Supported: (tm,tn) in {(1,1),(1,2),(2,2)}, wn in {1,2,4}, wk in {1,2,4,8,16},
+ * wn*wk <= 8 when wn > 1, wk == 16 only with wn == 1, at most 160 KiB of LDS for the combine.
+ * All-zero fields select the built-in heuristic. */
 typedef struct tspm_conv_algo {
   int32_t tm, tn, wn, wk, splits;
 } tspm_conv_algo;
@@ -69,11 +70,27 @@ typedef struct tspm_strides4 {
   int64_t sn, sh, sw, sc;
 } tspm_strides4;
 
-/* y[P,Q,N,K] = conv(x, w).  y is HWNC.  If bn_partial != NULL the epilogue also writes BatchNorm
- * partial statistics of y (3 planes of [tiles][K] floats: tile shift, mean offset, M2; tiles and
- * rows per tile from the two queries below) for tspm_bn_finalize — the conv output is not re-read. */
+/* BatchNorm statistics produced by the convolution epilogue (BatchNorm2d after every conv,
+ * resnet.py:25-26,30-31,137-138,176-177).  partial: 3 planes of [tiles][K] floats (tile shift K,
+ * mean offset, M2; tiles and rows per tile from the two queries below).  If counters != NULL the
+ * last workgroup to finish each column block merges the partials in-launch (no tspm_bn_finalize
+ * launch) and writes save_mean / save_invstd and the running statistics: counters = one uint32 per
+ * 32 output channels, zero before first use (left zero after every launch).  With counters == NULL
+ * only the partials are written (merge them with tspm_bn_finalize). */
+typedef struct tspm_bn_fuse {
+  float* partial;
+  uint32_t* counters;
+  float* running_mean; /* nullable */
+  float* running_var;  /* nullable */
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+} tspm_bn_fuse;
+
+/* y[P,Q,N,K] = conv(x, w).  y is HWNC.  bn: NULL, or the BatchNorm statistics to produce from the
+ * epilogue (see tspm_bn_fuse) — the conv output is never re-read for them. */
 int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
-                  const tspm_strides4* x_strides, const float* w, float* y, float* bn_partial,
+                  const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
                   tspm_stream_t stream);
 int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
@@ -87,11 +104,26 @@ int tspm_conv_dgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, co
                     tspm_stream_t stream);
 size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
-/* dw[K,R,S,C] (OHWI) = conv_weight_grad(x, dy[P,Q,N,K]); overwritten (zero_grad semantics). */
+/* dw[K,R,S,C] (OHWI) = conv_weight_grad(x, dy[P,Q,N,K]); overwritten (zero_grad semantics).
+ * With splits > 1 the workspace holds TSPM_COUNTER_BYTES of arrival counters followed by the fp32
+ * slabs; the last workgroup of each tile sums the slabs in slab order in-launch.  The counter
+ * header must be zero before the first call (it is left zero after every call), so one zeroed
+ * workspace can serve every wgrad shape. */
+#define TSPM_COUNTER_BYTES 65536
 int tspm_conv_wgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
                     const tspm_strides4* x_strides, const float* dy, float* dw, void* workspace,
                     size_t workspace_bytes, tspm_stream_t stream);
 size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+
+/* Transposed copies.  tspm_bn_apply (out_t), tspm_bn_bwd (dy_t, dy2_t) and tspm_maxpool_fwd (y_t)
+ * can also write their HWNC output transposed: t[c][ld_t] with the m = (h*W + w)*N + n rows of
+ * channel c contiguous (ld_t >= m, ld_t % 4 == 0, m % 4 == 0, 16-byte aligned).  That is the
+ * operand layout of tspm_conv_wgrad_t: both GEMM operands of the weight gradient become 16-byte
+ * loads of 4 consecutive rows.  Same result as tspm_conv_wgrad (same reduction order up to the
+ * fp32 rounding of the split sums); needs n % 8 == 0.  Workspace: tspm_conv_wgrad_workspace. */
+int tspm_conv_wgrad_t(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x_t,
+                      int64_t ldx, const float* dy_t, int64_t ldy, float* dw, void* workspace,
+                      size_t workspace_bytes, tspm_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * BatchNorm2d, training mode (batch statistics over N*H*W, biased variance for normalisation,
@@ -109,7 +141,8 @@ size_t tspm_bn_stats_workspace(int64_t m, int32_t c);
 
 /* Merge per-tile partial statistics (3 planes of [ntiles][c]: tile shift K, mean-K, M2; tile t
  * holds min(rows_per_tile, m - t*rows_per_tile) rows) into save_mean / save_invstd and the running
- * statistics — the tail of tspm_bn_stats, and the consumer of tspm_conv_fwd's bn_partial. */
+ * statistics — the tail of tspm_bn_stats, and the consumer of tspm_conv_fwd's partials when no
+ * counters are given. */
 int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t rows_per_tile, const float* partial,
                      float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
                      float* save_invstd, tspm_stream_t stream);
@@ -120,7 +153,8 @@ int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t rows_per_tile
 int tspm_bn_apply(int64_t m, int32_t c, const float* y, const float* mean, const float* invstd,
                   const float* gamma, const float* beta, int32_t res_mode, const float* res,
                   const float* res_mean, const float* res_invstd, const float* res_gamma,
-                  const float* res_beta, int32_t relu, float* out, tspm_stream_t stream);
+                  const float* res_beta, int32_t relu, float* out, float* out_t, int64_t ld_t,
+                  tspm_stream_t stream);
 
 /* Eval-mode BN (running statistics) with the same fusion options. */
 int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* running_mean,
@@ -134,12 +168,14 @@ int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* runnin
  *   dgamma = sum(g' * xhat), dbeta = sum(g')          (written, not accumulated)
  *   dy  = gamma*invstd*(g' - dbeta/M - xhat*dgamma/M)
  *   dy2 likewise for the second BN; if dres != NULL it receives g' (identity residual grad).
+ * dy_t / dy2_t (nullable): also write dy / dy2 transposed, [c][ld_t] (see "transposed copies").
  * Workspace: tspm_bn_bwd_workspace. */
 int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y,
                 const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                 float* dy, const float* y2, const float* mean2, const float* invstd2,
                 const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres,
-                void* workspace, size_t workspace_bytes, tspm_stream_t stream);
+                float* dy_t, float* dy2_t, int64_t ld_t, void* workspace, size_t workspace_bytes,
+                tspm_stream_t stream);
 size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
 
 /* ------------------------------------------------------------------------------------------------
@@ -148,7 +184,8 @@ size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
 /* y[P,Q,N,C] = maxpool(x[H,W,N,C]); argmax tap (0..k*k-1, first max in row-major window order,
  * as ATen's CPU kernel) stored in idx (uint8, same shape as y). */
 int tspm_maxpool_fwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
-                     int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, tspm_stream_t stream);
+                     int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, float* y_t, int64_t ld_t,
+                     tspm_stream_t stream);
 /* dx = scatter of dy to the argmax positions (gather form, deterministic); dx overwritten. */
 int tspm_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
                      int32_t p, int32_t q, const float* dy, const uint8_t* idx, float* dx,

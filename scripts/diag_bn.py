@@ -37,12 +37,12 @@ def bn_case(m, c):
                               ws.data_ptr(), wsb, sh()), "stats")
     out = torch.empty(m, c, device=dev)
     L.check(lib.tspm_bn_apply(m, c, y_.data_ptr(), mean.data_ptr(), inv.data_ptr(), gm.data_ptr(), bt.data_ptr(), 0,
-                              None, None, None, None, None, 1, out.data_ptr(), sh()), "apply")
+                              None, None, None, None, None, 1, out.data_ptr(), None, 0, sh()), "apply")
     dy = torch.empty(m, c, device=dev)
     gw, gb = torch.empty(c, device=dev), torch.empty(c, device=dev)
     L.check(lib.tspm_bn_bwd(m, c, g_.data_ptr(), out.data_ptr(), y_.data_ptr(), mean.data_ptr(), inv.data_ptr(),
                             gm.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(), None, None, None, None, None,
-                            None, None, None, ws.data_ptr(), wsb, sh()), "bwd")
+                            None, None, None, None, None, 0, ws.data_ptr(), wsb, sh()), "bwd")
     torch.cuda.synchronize()
     G = lib.tspm_bn_stats_workspace(m, c) // (2 * c * 4)
     # torch-on-gpu recomputation of the sums for comparison

@@ -31,7 +31,7 @@ SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64]
 
 def candidates(kind):
     for (tm, tn), wn, wk in itertools.product(TILES, WNS, WKS):
-        sps = SPLITS if kind == "wgrad" else [1]
+        sps = SPLITS if kind.startswith("wgrad") else [1]
         for sp in sps:
             yield (tm, tn, wn, wk, sp)
 
@@ -52,7 +52,7 @@ def distinct_ops(batch, dev):
                 kinds = ("fwd", "wgrad")
             else:
                 xs = L.hwnc_strides(s.n, s.h, s.w, s.c)
-                kinds = ("fwd", "dgrad", "wgrad")
+                kinds = ("fwd", "dgrad", "wgrad_t" if eng.use_t else "wgrad")
             for kind in kinds:
                 out.setdefault((kind,) + key, (s, xs, op is eng.stem))
     return out
@@ -69,22 +69,34 @@ class Bufs:
         self.dx = torch.empty(n_in, device=dev)
         self.dw = torch.empty(s.k * s.r * s.s * s.c, device=dev)
         self.part = torch.empty(3 * (s.n * s.p * s.q // 32 + 1) * s.k, device=dev)
-        self.ws = torch.empty(1, dtype=torch.uint8, device=dev)
+        # transposed operands of wgrad_t ([C][rows]); the values only matter for the cross-check
+        self.x_t = self.x.view(-1, s.c).t().contiguous() if not stem else None
+        self.dy_t = self.dy.view(-1, s.k).t().contiguous()
+        self.ws = torch.zeros(1, dtype=torch.uint8, device=dev)
+        self.cnt = torch.zeros(s.k // 32 + 1, dtype=torch.int32, device=dev)
+        self.mean = torch.empty(s.k, device=dev)
+        self.inv = torch.empty(s.k, device=dev)
 
 
 def launcher(kind, s, xs, b, algo):
     lib = L.lib()
     a = L.ConvAlgo(*algo)
     sh = L.stream_handle()
-    if kind == "wgrad":
+    if kind.startswith("wgrad"):
         need = lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(a))
         if need > b.ws.numel():
-            b.ws = torch.empty(need, dtype=torch.uint8, device=b.x.device)
+            b.ws = torch.zeros(need, dtype=torch.uint8, device=b.x.device)
         wsb = b.ws.numel()
 
-        def f():
-            return lib.tspm_conv_wgrad(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs),
-                                       b.dy.data_ptr(), b.dw.data_ptr(), b.ws.data_ptr(), wsb, sh)
+        if kind == "wgrad_t":
+            def f():
+                return lib.tspm_conv_wgrad_t(ctypes.byref(s), ctypes.byref(a), b.x_t.data_ptr(), b.x_t.shape[1],
+                                             b.dy_t.data_ptr(), b.dy_t.shape[1], b.dw.data_ptr(), b.ws.data_ptr(), wsb,
+                                             sh)
+        else:
+            def f():
+                return lib.tspm_conv_wgrad(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs),
+                                           b.dy.data_ptr(), b.dw.data_ptr(), b.ws.data_ptr(), wsb, sh)
         return f, b.dw
     if kind == "dgrad":
         def f():
@@ -92,9 +104,11 @@ def launcher(kind, s, xs, b, algo):
                                        b.dx.data_ptr(), 0, None, 0, sh)
         return f, b.dx
 
-    def f():
+    bnf = L.BnFuse(b.part.data_ptr(), b.cnt.data_ptr(), None, None, 0.1, 1e-5, b.mean.data_ptr(), b.inv.data_ptr())
+
+    def f():  # the engine's launch: conv + BN statistics merged in-launch
         return lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs), b.w.data_ptr(),
-                                 b.y.data_ptr(), b.part.data_ptr(), sh)
+                                 b.y.data_ptr(), ctypes.byref(bnf), sh)
     return f, b.y
 
 

@@ -17,7 +17,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 3
+ABI_VERSION = 5
+COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
 class TspmLibraryError(RuntimeError):
@@ -40,6 +41,13 @@ class Strides4(Structure):
     _fields_ = [(n, c_int64) for n in ("sn", "sh", "sw", "sc")]
 
 
+class BnFuse(Structure):
+    """tspm_bn_fuse: BatchNorm statistics produced by the conv forward epilogue."""
+    _fields_ = [("partial", c_void_p), ("counters", c_void_p), ("running_mean", c_void_p),
+                ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float), ("save_mean", c_void_p),
+                ("save_invstd", c_void_p)]
+
+
 class AdamHyper(Structure):
     _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("grad_scale", ctypes.c_double),
@@ -53,7 +61,8 @@ _P = c_void_p
 _SIGS = {
     "tspm_abi_version": (c_int32, []),
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
-    "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, _P]),
+    "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, POINTER(BnFuse),
+                                _P]),
     "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
@@ -61,17 +70,20 @@ _SIGS = {
     "tspm_conv_dgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_wgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, c_size_t, _P]),
     "tspm_conv_wgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_wgrad_t": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, c_int64, _P, c_int64, _P, _P, c_size_t,
+                                    _P]),
     "tspm_bn_stats": (c_int32, [c_int64, c_int32, _P, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P,
                                 c_size_t, _P]),
     "tspm_bn_stats_workspace": (c_size_t, [c_int64, c_int32]),
     "tspm_bn_finalize": (c_int32, [c_int64, c_int32, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P]),
-    "tspm_bn_apply": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P]),
+    "tspm_bn_apply": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P,
+                                c_int64, _P]),
     "tspm_bn_apply_eval": (c_int32, [c_int64, c_int32, _P, _P, _P, c_float, _P, _P, c_int32, _P, _P, _P, _P, _P,
                                      c_int32, _P, _P]),
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                              _P, c_size_t, _P]),
+                              _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
-    "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
+    "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),
     "tspm_avgpool_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P]),

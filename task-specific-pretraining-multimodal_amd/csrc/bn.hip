@@ -17,9 +17,9 @@ namespace {
 constexpr int kChanPerBlock = 64;  // 16 float4 lanes
 constexpr int kRowGroups = 16;     // 256 threads = 16 lanes x 16 row groups
 
-int row_blocks(long long m, int c) {
+int row_blocks(long long m, int c, int target = 1024) {
   const long long cg = cdiv64(c, kChanPerBlock);
-  long long g = cdiv64(1024, cg);
+  long long g = cdiv64(target, cg);
   const long long max_g = cdiv64(m, kRowGroups);
   if (g > max_g) g = max_g;
   if (g < 1) g = 1;
@@ -92,62 +92,17 @@ __global__ __launch_bounds__(256) void k_bn_stats_partial(long long M, int C, co
   }
 }
 
-// per-channel merge of G partial tiles (8 channels x 32 tile-groups per workgroup, double)
+// per-channel merge of G partial tiles: 4 channels x 64 tile groups per workgroup, double, fixed
+// order, 8 tile loads in flight per thread (bn_merge_block)
+constexpr int kFinChan = 4;
 __global__ __launch_bounds__(256) void k_bn_finalize(long long M, int C, int G, long long rows_per_tile,
                                                      const float* __restrict__ part, float* __restrict__ rmean,
                                                      float* __restrict__ rvar, float momentum, float eps,
                                                      float* __restrict__ smean, float* __restrict__ sinv) {
   __shared__ double red[256];
-  __shared__ double smu[8];
-  const int t = threadIdx.x;
-  const int cl = t & 7, gg = t >> 3;
-  const int c = blockIdx.x * 8 + cl;
-  const bool cok = c < C;
-  const long long plane = (long long)G * C;
-  double s = 0.0;
-  if (cok)
-    for (int g = gg; g < G; g += 32) {
-      const double nb = (double)min(rows_per_tile, M - (long long)g * rows_per_tile);
-      const double mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
-      s += nb * mb;
-    }
-  red[t] = s;
-  __syncthreads();
-  for (int w = 16; w > 0; w >>= 1) {
-    if (gg < w) red[t] += red[t + w * 8];
-    __syncthreads();
-  }
-  if (gg == 0) smu[cl] = red[cl] / (double)M;
-  __syncthreads();
-  const double mean = smu[cl];
-  double q = 0.0;
-  if (cok)
-    for (int g = gg; g < G; g += 32) {
-      const double nb = (double)min(rows_per_tile, M - (long long)g * rows_per_tile);
-      const double mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
-      const double m2b = (double)part[2 * plane + (long long)g * C + c];
-      q += m2b + nb * (mb - mean) * (mb - mean);
-    }
-  __syncthreads();
-  red[t] = q;
-  __syncthreads();
-  for (int w = 16; w > 0; w >>= 1) {
-    if (gg < w) red[t] += red[t + w * 8];
-    __syncthreads();
-  }
-  if (gg == 0 && cok) {
-    const double n = (double)M;
-    double var = red[cl] / n;
-    if (var < 0.0) var = 0.0;
-    const float fmean = (float)mean, fvar = (float)var;
-    smean[c] = fmean;
-    sinv[c] = 1.0f / sqrtf(fvar + eps);
-    if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
-    if (rvar) {
-      const float unb = M > 1 ? (float)(red[cl] / (n - 1.0)) : fvar;
-      rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
-    }
-  }
+  __shared__ double smu[kFinChan];
+  bn_merge_block(M, C, G, rows_per_tile, part, blockIdx.x * kFinChan, kFinChan, rmean, rvar, momentum, eps, smean,
+                 sinv, red, smu);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -196,9 +151,85 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
   }
 }
 
+// Transposed-store helper of the tiled kernels: a [64 rows x 64 channels] tile staged in LDS
+// (tile[row][65]) is written as dst[c][ld_t] rows-contiguous (the wgrad operand layout) with 16-byte
+// stores, 4 consecutive threads per channel.  Requires (m % 4 == 0) and 16-byte aligned dst/ld_t.
+TSPM_DEV void store_tile_t(const float (*tile)[65], long long r0, long long M, int c0, int C, float* dst,
+                           long long ld_t) {
+  const int t = threadIdx.x;
+  const int cl = t >> 2, qq = t & 3;
+  const int c = c0 + cl;
+  if (c >= C) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int rl = qq * 16 + 4 * k;
+    if (r0 + rl < M) {
+      const f32x4 v = {tile[rl][cl], tile[rl + 1][cl], tile[rl + 2][cl], tile[rl + 3][cl]};
+      st4(dst + (long long)c * ld_t + r0 + rl, v);
+    }
+  }
+}
+
+// Tiled train-mode apply: a workgroup owns [64 rows x 64 channels]; writes out (HWNC) and out_t
+// ([C][ld_t]) through an LDS transpose.
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void k_bn_apply_t(long long M, int C, const float* __restrict__ y,
+                                                    const float* __restrict__ mean, const float* __restrict__ inv,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    const float* __restrict__ res, const float* __restrict__ mean2,
+                                                    const float* __restrict__ inv2, const float* __restrict__ gamma2,
+                                                    const float* __restrict__ beta2, float* __restrict__ out,
+                                                    float* __restrict__ out_t, long long ld_t) {
+  __shared__ float tile[64][65];
+  const int t = threadIdx.x, l16 = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + l16;
+  const bool cok = 4 * c4 < C;
+  const long long r0 = (long long)blockIdx.x * 64;
+  f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sf = sc, sc2 = sc, sf2 = sc;
+  if (cok) {
+    sc = ld4(gamma + 4 * c4) * ld4(inv + 4 * c4);
+    sf = ld4(beta + 4 * c4) - ld4(mean + 4 * c4) * sc;
+    if (RES == 2) {
+      sc2 = ld4(gamma2 + 4 * c4) * ld4(inv2 + 4 * c4);
+      sf2 = ld4(beta2 + 4 * c4) - ld4(mean2 + 4 * c4) * sc2;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = rg + 16 * i;
+    const long long row = r0 + rl;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    if (cok && row < M) {
+      const long long off = row * C + 4 * c4;
+      const f32x4 v = ld4(y + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaf(v[j], sc[j], sf[j]);
+      if (RES == 1) o += ld4(res + off);
+      if (RES == 2) {
+        const f32x4 v2 = ld4(res + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += fmaf(v2[j], sc2[j], sf2[j]);
+      }
+      if (RELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+      }
+      st4(out + off, o);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[rl][4 * l16 + j] = o[j];
+  }
+  __syncthreads();
+  store_tile_t(tile, r0, M, blockIdx.y * 64, C, out_t, ld_t);
+}
+
 // ------------------------------------------------------------------------------------------------
 // backward: partial sums of g', g'*(y-mean) [, g'*(y2-mean2)] over [rows x 64 channels] tiles
 // ------------------------------------------------------------------------------------------------
+// backward pass 1: partial sums of g', g'*(y-mean) [, g'*(y2-mean2)] over [rows x 64 channels]
+// tiles (rows in batches of 4 per thread so their loads are in flight together).  An in-launch
+// merge by the last workgroup was measured slower than the parallel pass 2 below (the merge of
+// >= 64 tiles per channel block serialises on one CU), so pass 2 stays a launch.
 template <bool HAS_OUT, bool TWO>
 __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
                                                         const float* __restrict__ out, const float* __restrict__ y,
@@ -216,30 +247,47 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
   if (cok) {
     const f32x4 mu = ld4(mean + 4 * c4);
     const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (long long row = r_begin + rg; row < r_end; row += kRowGroups) {
-      const long long off = row * C + 4 * c4;
-      f32x4 gv = ld4(g + off);
-      if (HAS_OUT) {
-        const f32x4 ov = ld4(out + off);
+    constexpr int U = 4;  // rows per batch: all their loads in flight together
+    for (long long rb = r_begin + rg; rb < r_end; rb += U * kRowGroups) {
+      f32x4 gv[U], yv[U], y2v[U];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gv[j] = ov[j] > 0.f ? gv[j] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const long long row = rb + u * kRowGroups;
+        if (row < r_end) {
+          const long long off = row * C + 4 * c4;
+          gv[u] = ld4(g + off);
+          if (HAS_OUT) {
+            const f32x4 ov = ld4(out + off);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gv[u][j] = ov[j] > 0.f ? gv[u][j] : 0.f;
+          }
+          yv[u] = ld4(y + off);
+          if (TWO) y2v[u] = ld4(y2 + off);
+        } else {
+          gv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          yv[u] = mu;
+          if (TWO) y2v[u] = mu2;
+        }
       }
-      sg += gv;
-      sx += gv * (ld4(y + off) - mu);
-      if (TWO) sx2 += gv * (ld4(y2 + off) - mu2);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        sg += gv[u];
+        sx += gv[u] * (yv[u] - mu);
+        if (TWO) sx2 += gv[u] * (y2v[u] - mu2);
+      }
     }
   }
   sh[0][t] = sg;
   sh[1][t] = sx;
   if (TWO) sh[2][t] = sx2;
   __syncthreads();
+  const long long plane = (long long)gridDim.x * C;
   if (rg == 0 && cok) {
     for (int k = 1; k < kRowGroups; ++k) {
       sg += sh[0][k * 16 + lane];
       sx += sh[1][k * 16 + lane];
       if (TWO) sx2 += sh[2][k * 16 + lane];
     }
-    const long long plane = (long long)gridDim.x * C;
     st4(part + (long long)blockIdx.x * C + 4 * c4, sg);
     st4(part + plane + (long long)blockIdx.x * C + 4 * c4, sx);
     if (TWO) st4(part + 2 * plane + (long long)blockIdx.x * C + 4 * c4, sx2);
@@ -335,6 +383,62 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(long long n4, int C, const
   }
 }
 
+// Tiled backward apply: [64 rows x 64 channels] per workgroup; also writes dy_t (and dy2_t) in
+// the transposed wgrad operand layout through LDS.
+template <bool HAS_OUT, bool TWO, bool DRES>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_t(long long M, int C, const float* __restrict__ g,
+                                                        const float* __restrict__ out, const float* __restrict__ y,
+                                                        const float* __restrict__ mean, const float* __restrict__ y2,
+                                                        const float* __restrict__ mean2, const float* __restrict__ coef,
+                                                        float* __restrict__ dy, float* __restrict__ dy2,
+                                                        float* __restrict__ dres, float* __restrict__ dy_t,
+                                                        float* __restrict__ dy2_t, long long ld_t) {
+  __shared__ float tile[TWO ? 2 : 1][64][65];
+  const int t = threadIdx.x, l16 = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + l16;
+  const bool cok = 4 * c4 < C;
+  const long long r0 = (long long)blockIdx.x * 64;
+  f32x4 ca = {0.f, 0.f, 0.f, 0.f}, cb = ca, cm = ca, mu = ca, ca2 = ca, cb2 = ca, cm2 = ca, mu2 = ca;
+  if (cok) {
+    ca = ld4(coef + 4 * c4); cb = ld4(coef + C + 4 * c4); cm = ld4(coef + 2 * C + 4 * c4);
+    mu = ld4(mean + 4 * c4);
+    if (TWO) {
+      ca2 = ld4(coef + 3 * C + 4 * c4); cb2 = ld4(coef + 4 * C + 4 * c4); cm2 = ld4(coef + 5 * C + 4 * c4);
+      mu2 = ld4(mean2 + 4 * c4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = rg + 16 * i;
+    const long long row = r0 + rl;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f}, o2 = o;
+    if (cok && row < M) {
+      const long long off = row * C + 4 * c4;
+      f32x4 gv = ld4(g + off);
+      if (HAS_OUT) {
+        const f32x4 ov = ld4(out + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gv[j] = ov[j] > 0.f ? gv[j] : 0.f;
+      }
+      o = ca * gv - cm - cb * (ld4(y + off) - mu);
+      st4(dy + off, o);
+      if (TWO) {
+        o2 = ca2 * gv - cm2 - cb2 * (ld4(y2 + off) - mu2);
+        st4(dy2 + off, o2);
+      }
+      if (DRES) st4(dres + off, gv);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tile[0][rl][4 * l16 + j] = o[j];
+      if (TWO) tile[TWO ? 1 : 0][rl][4 * l16 + j] = o2[j];
+    }
+  }
+  __syncthreads();
+  store_tile_t(tile[0], r0, M, blockIdx.y * 64, C, dy_t, ld_t);
+  if (TWO && dy2_t) store_tile_t(tile[TWO ? 1 : 0], r0, M, blockIdx.y * 64, C, dy2_t, ld_t);
+}
+
 int ew_blocks(long long n4) {
   long long b = cdiv64(n4, 256);
   if (b > 2048) b = 2048;
@@ -351,7 +455,7 @@ extern "C" int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t ro
   if (m <= 0 || c <= 0 || ntiles <= 0 || rows_per_tile <= 0 || !partial || !save_mean || !save_invstd)
     return TSPM_ERR_INVALID;
   if ((long long)ntiles * rows_per_tile < m || (long long)(ntiles - 1) * rows_per_tile >= m) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, 8)), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)m, c,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, kFinChan)), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)m, c,
                      ntiles, (long long)rows_per_tile, partial, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd);
   TSPM_LAUNCH_CHECK();
@@ -385,15 +489,34 @@ extern "C" int tspm_bn_stats(int64_t m, int32_t c, const float* y, int32_t nslab
   hipLaunchKernelGGL((k_bn_apply<RES, RELU, EVAL>), dim3(ew_blocks(n4)), dim3(256), 0, st, n4, c, y, mean, \
                      inv, gamma, beta, res, mean2, inv2, gamma2, beta2, eps, out)
 
+static bool t_ok(long long m, const float* p, long long ld_t) {
+  return m % 4 == 0 && ld_t >= m && ld_t % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+}
+
+#define BN_APPLY_T_LAUNCH(RES, RELU)                                                                          \
+  hipLaunchKernelGGL((k_bn_apply_t<RES, RELU>), tgrid, dim3(256), 0, st, (long long)m, c, y, mean, inv, gamma, \
+                     beta, res, mean2, inv2, gamma2, beta2, out, out_t, (long long)ld_t)
+
 static int bn_apply_common(int64_t m, int32_t c, const float* y, const float* mean, const float* inv,
                            const float* gamma, const float* beta, int32_t res_mode, const float* res,
                            const float* mean2, const float* inv2, const float* gamma2, const float* beta2,
-                           int32_t relu, float* out, bool eval, float eps, tspm_stream_t stream) {
+                           int32_t relu, float* out, float* out_t, int64_t ld_t, bool eval, float eps,
+                           tspm_stream_t stream) {
   if (m <= 0 || !c_ok(c) || !y || !mean || !inv || !gamma || !beta || !out) return TSPM_ERR_INVALID;
   if (res_mode < 0 || res_mode > 2) return TSPM_ERR_INVALID;
   if (res_mode >= 1 && !res) return TSPM_ERR_INVALID;
   if (res_mode == 2 && (!mean2 || !inv2 || !gamma2 || !beta2)) return TSPM_ERR_INVALID;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (out_t) {
+    if (eval || !t_ok(m, out_t, ld_t)) return TSPM_ERR_INVALID;
+    const dim3 tgrid((unsigned)cdiv64(m, 64), cdiv(c, 64));
+    const bool r = relu != 0;
+    if (res_mode == 0) { if (r) BN_APPLY_T_LAUNCH(0, true); else BN_APPLY_T_LAUNCH(0, false); }
+    else if (res_mode == 1) { if (r) BN_APPLY_T_LAUNCH(1, true); else BN_APPLY_T_LAUNCH(1, false); }
+    else { if (r) BN_APPLY_T_LAUNCH(2, true); else BN_APPLY_T_LAUNCH(2, false); }
+    TSPM_LAUNCH_CHECK();
+    return TSPM_OK;
+  }
   const long long n4 = (long long)m * c / 4;
   const bool r = relu != 0;
   if (!eval) {
@@ -412,9 +535,10 @@ static int bn_apply_common(int64_t m, int32_t c, const float* y, const float* me
 extern "C" int tspm_bn_apply(int64_t m, int32_t c, const float* y, const float* mean, const float* invstd,
                              const float* gamma, const float* beta, int32_t res_mode, const float* res,
                              const float* res_mean, const float* res_invstd, const float* res_gamma,
-                             const float* res_beta, int32_t relu, float* out, tspm_stream_t stream) {
+                             const float* res_beta, int32_t relu, float* out, float* out_t, int64_t ld_t,
+                             tspm_stream_t stream) {
   return bn_apply_common(m, c, y, mean, invstd, gamma, beta, res_mode, res, res_mean, res_invstd, res_gamma,
-                         res_beta, relu, out, false, 0.f, stream);
+                         res_beta, relu, out, out_t, ld_t, false, 0.f, stream);
 }
 
 extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* running_mean,
@@ -423,7 +547,7 @@ extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const fl
                                   const float* res_gamma, const float* res_beta, int32_t relu, float* out,
                                   tspm_stream_t stream) {
   return bn_apply_common(m, c, y, running_mean, running_var, gamma, beta, res_mode, res, res_rmean, res_rvar,
-                         res_gamma, res_beta, relu, out, true, eps, stream);
+                         res_gamma, res_beta, relu, out, nullptr, 0, true, eps, stream);
 }
 
 extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
@@ -434,8 +558,8 @@ extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
 extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y, const float* mean,
                            const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dy,
                            const float* y2, const float* mean2, const float* invstd2, const float* gamma2,
-                           float* dgamma2, float* dbeta2, float* dy2, float* dres, void* ws, size_t ws_bytes,
-                           tspm_stream_t stream) {
+                           float* dgamma2, float* dbeta2, float* dy2, float* dres, float* dy_t, float* dy2_t,
+                           int64_t ld_t, void* ws, size_t ws_bytes, tspm_stream_t stream) {
   if (m <= 0 || !c_ok(c) || !g || !y || !mean || !invstd || !gamma || !dy) return TSPM_ERR_INVALID;
   const bool two = y2 != nullptr;
   if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
@@ -458,9 +582,27 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 8)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
                      invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, coef);
   TSPM_LAUNCH_CHECK();
+  const bool dr = dres != nullptr;
+  if (dy_t) {
+    if (!t_ok(m, dy_t, ld_t) || (two && dy2_t && !t_ok(m, dy2_t, ld_t)) || (!two && dy2_t)) return TSPM_ERR_INVALID;
+    const dim3 tgrid((unsigned)cdiv64(m, 64), cdiv(c, 64));
+#define BNB_AT(HO, TW, DR)                                                                                  \
+  hipLaunchKernelGGL((k_bn_bwd_apply_t<HO, TW, DR>), tgrid, dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
+                     y2, mean2, coef, dy, dy2, dres, dy_t, dy2_t, (long long)ld_t)
+    if (ho) {
+      if (two) { if (dr) BNB_AT(true, true, true); else BNB_AT(true, true, false); }
+      else { if (dr) BNB_AT(true, false, true); else BNB_AT(true, false, false); }
+    } else {
+      if (two) { if (dr) BNB_AT(false, true, true); else BNB_AT(false, true, false); }
+      else { if (dr) BNB_AT(false, false, true); else BNB_AT(false, false, false); }
+    }
+#undef BNB_AT
+    TSPM_LAUNCH_CHECK();
+    return TSPM_OK;
+  }
+  if (dy2_t) return TSPM_ERR_INVALID;
   const long long n4 = (long long)m * c / 4;
   const int nb = ew_blocks(n4);
-  const bool dr = dres != nullptr;
 #define BNB_A(HO, TW, DR)                                                                                          \
   hipLaunchKernelGGL((k_bn_bwd_apply<HO, TW, DR>), dim3(nb), dim3(256), 0, st, n4, c, g, out, y, mean, y2, mean2, \
                      coef, dy, dy2, dres)

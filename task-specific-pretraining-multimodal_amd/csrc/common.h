@@ -45,3 +45,109 @@ static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
     hipError_t e__ = hipGetLastError();                   \
     if (e__ != hipSuccess) return TSPM_ERR_LAUNCH;        \
   } while (0)
+
+// In-launch hand-off to the LAST arriving workgroup of a group (cdna_hip_programming.md §5,
+// "in-launch split-K reduction" recipe): every wave drains its global stores, the workgroup
+// releases at agent scope (per-XCD L2s are not coherent) and draws a ticket; the workgroup that
+// draws total-1 acquires at agent scope, re-arms the counter to 0 for the next launch and returns
+// true in every thread.  `flag` is one int of the kernel's (dynamic) LDS array.  Every thread of
+// the workgroup must call this (it contains barriers).  Counters must be zero before the first
+// launch that uses them.
+TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == total - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __syncthreads();
+  return last;
+}
+
+// Per-channel merge of BatchNorm partial statistics {K, mean-K, M2} of G row tiles (tile t holds
+// min(rpt, M - t*rpt) rows) for channels [c0, c0+CB), in double with a fixed-order reduction, by
+// ONE workgroup whose size is a power-of-two multiple of CB.  Writes save_mean / save_invstd and
+// updates the running statistics (momentum, unbiased variance) like nn.BatchNorm2d.
+// `red` must hold blockDim.x doubles, `smu` CB doubles (LDS).
+TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const float* part, int c0, int CB,
+                             float* rmean, float* rvar, float momentum, float eps, float* smean, float* sinv,
+                             double* red, double* smu) {
+  const int t = threadIdx.x, T = blockDim.x;
+  const int GG = T / CB, cl = t % CB, gg = t / CB;
+  const int c = c0 + cl;
+  const bool cok = c < C;
+  const long long plane = (long long)G * C;
+  // tiles gg, gg+GG, ... in batches of 8 independent loads (the reads follow an acquire: they
+  // miss in cache, so issue them together)
+  auto tile_mean = [&](int g, double& nb, double& mb) {
+    nb = (double)min(rpt, M - (long long)g * rpt);
+    mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
+  };
+  double s = 0.0;
+  if (cok)
+    for (int g0 = gg; g0 < G; g0 += 8 * GG) {
+      double nb[8], mb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int g = g0 + u * GG;
+        if (g < G) tile_mean(g, nb[u], mb[u]); else { nb[u] = 0.0; mb[u] = 0.0; }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += nb[u] * mb[u];
+    }
+  red[t] = s;
+  __syncthreads();
+  for (int w = GG >> 1; w > 0; w >>= 1) {
+    if (gg < w) red[t] += red[t + w * CB];
+    __syncthreads();
+  }
+  if (gg == 0) smu[cl] = red[cl] / (double)M;
+  __syncthreads();
+  const double mean = smu[cl];
+  double q = 0.0;
+  if (cok)
+    for (int g0 = gg; g0 < G; g0 += 8 * GG) {
+      double nb[8], mb[8], m2b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int g = g0 + u * GG;
+        if (g < G) {
+          tile_mean(g, nb[u], mb[u]);
+          m2b[u] = (double)part[2 * plane + (long long)g * C + c];
+        } else {
+          nb[u] = 0.0; mb[u] = mean; m2b[u] = 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q += m2b[u] + nb[u] * (mb[u] - mean) * (mb[u] - mean);
+    }
+  red[t] = q;
+  __syncthreads();
+  for (int w = GG >> 1; w > 0; w >>= 1) {
+    if (gg < w) red[t] += red[t + w * CB];
+    __syncthreads();
+  }
+  if (gg == 0 && cok) {
+    const double n = (double)M;
+    double var = red[cl] / n;
+    if (var < 0.0) var = 0.0;
+    const float fmean = (float)mean, fvar = (float)var;
+    smean[c] = fmean;
+    sinv[c] = 1.0f / sqrtf(fvar + eps);
+    if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
+    if (rvar) {
+      const float unb = M > 1 ? (float)(red[cl] / (n - 1.0)) : fvar;
+      rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+    }
+  }
+}

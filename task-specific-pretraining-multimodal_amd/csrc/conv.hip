@@ -33,6 +33,7 @@ struct ConvArgs {
   int splits;                // wgrad global split
   long long slab;            // elements per split slab
   int beta;                  // dgrad accumulate
+  unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
 };
 
 template <int TM, int TN>
@@ -143,13 +144,50 @@ struct Acc {
 
 TSPM_DEV int split_lo(int T, int z, int S) { return (int)(((long long)T * z) / S); }
 
+// wgrad tail with split-K over workgroups: the last of the `splits` workgroups of this tile sums
+// the slabs in slab order (bitwise equal to tspm_reduce_slabs) and writes dw.
+template <int TM, int TN, int WN>
+TSPM_DEV void slab_tail(const ConvArgs& g, const float* slabs, float* dw_final, int RSC, float* lds) {
+  if (!last_arriver(g.cnt + (blockIdx.y * gridDim.x + blockIdx.x), g.splits, reinterpret_cast<int*>(lds))) return;
+  const int r0 = blockIdx.x * (TM * 32), rn = min(TM * 32, g.k - r0);
+  const int cb0 = blockIdx.y * (WN * TN * 32), cn = min(WN * TN * 32, RSC - cb0);
+  for (int e = threadIdx.x; e < rn * cn; e += blockDim.x) {
+    const int rr = e / cn, cc = e - rr * cn;
+    const long long off = (long long)(r0 + rr) * RSC + cb0 + cc;
+    float sum = 0.f;
+    int zz = 0;
+    for (; zz + 8 <= g.splits; zz += 8) {  // 8 independent loads in flight, summed in slab order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slabs[(zz + u) * g.slab + off];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; zz < g.splits; ++zz) sum += slabs[zz * g.slab + off];
+    dw_final[off] = sum;
+  }
+}
+
+// Forward tail with in-launch BatchNorm: the last workgroup of each column block (all row tiles
+// of its WN*TN*32 channels have written their partials) merges them (no finalize launch).
+template <int TM, int TN, int WN>
+TSPM_DEV void fwd_bn_tail(const ConvArgs& g, const tspm_bn_fuse& bf, float* lds) {
+  if (!bf.counters) return;
+  if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(lds))) return;
+  constexpr int CB = WN * TN * 32;
+  double* red = reinterpret_cast<double*>(lds) + 2;
+  double* smu = red + blockDim.x;
+  bn_merge_block(g.m, g.k, gridDim.x, TM * 32, bf.partial, blockIdx.y * CB, CB, bf.running_mean, bf.running_var,
+                 bf.momentum, bf.eps, bf.save_mean, bf.save_invstd, red, smu);
+}
+
 // =============================================================================================
 // Forward, vector path: HWNC input, C % 8 == 0.
 // =============================================================================================
 template <int TM, int TN, int WN, int WK, bool F_>
 __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const float* __restrict__ x,
                                                               const float* __restrict__ w, float* __restrict__ y,
-                                                              float* __restrict__ part) {
+                                                              tspm_bn_fuse bf) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -255,8 +293,9 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     acc.store(y, row0, col0, g.m, g.k, g.k, lane, false);
-    if (part) acc.bn_partials(part, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
+    if (bf.partial) acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
   }
+  fwd_bn_tail<TM, TN, WN>(g, bf, lds);
 }
 
 // =============================================================================================
@@ -266,7 +305,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
 template <int TM, int TN, int WN, int WK, bool F_>
 __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_gather(ConvArgs g, const float* __restrict__ x,
                                                                  const float* __restrict__ w, float* __restrict__ y,
-                                                                 float* __restrict__ part) {
+                                                                 tspm_bn_fuse bf) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -323,8 +362,9 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_gather(ConvArgs g, co
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     acc.store(y, row0, col0, g.m, g.k, g.k, lane, false);
-    if (part) acc.bn_partials(part, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
+    if (bf.partial) acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
   }
+  fwd_bn_tail<TM, TN, WN>(g, bf, lds);
 }
 
 // =============================================================================================
@@ -439,7 +479,8 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const f
 // =============================================================================================
 template <int TM, int TN, int WN, int WK, bool FAST>
 __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const float* __restrict__ x,
-                                                            const float* __restrict__ dy, float* __restrict__ dw) {
+                                                            const float* __restrict__ dy, float* __restrict__ dw,
+                                                            float* __restrict__ dw_final) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -522,7 +563,107 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const f
     float* out = g.splits > 1 ? dw + (long long)z * g.slab : dw;
     acc.store(out, row0, col0, K, RSC, RSC, lane, false);
   }
+  if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
 }
+
+// =============================================================================================
+// Weight gradient from TRANSPOSED operands (the layout tspm_bn_apply / tspm_bn_bwd /
+// tspm_maxpool_fwd write as their optional *_t outputs): xT[c][ldx] holds input rows (h,w,n)
+// contiguously per channel, dyT[co][ldy] output rows (p,q,n).  Both MFMA operands are then one
+// 16-byte load of 4 consecutive rows per lane (MFMA j reduces rows {mbase+j, mbase+4+j}), like the
+// forward kernel — instead of 8 gathered dwords per 4 MFMAs.  Requires N % 8 == 0: an 8-row
+// chunk shares one output position, so a 32-column tile inside one tap skips invalid chunks whole.
+// =============================================================================================
+template <int TM, int TN, int WN, int WK, bool F_>
+__global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad_t(ConvArgs g, const float* __restrict__ xT, long long ldx,
+                                                              const float* __restrict__ dyT, long long ldy,
+                                                              float* __restrict__ dw, float* __restrict__ dw_final) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave % WN, wk = wave / WN;
+  const int K = g.k, C = g.c, N = g.n;
+  const int RSC = g.r * g.s * C;
+  const int row0 = blockIdx.x * (TM * 32);              // co
+  const int col0 = (blockIdx.y * WN + wn) * (TN * 32);  // kidx
+  const bool active = col0 < RSC;
+  const int z = blockIdx.z;
+  const int li = lane & 31, hh = lane >> 5;
+  const int Mout = g.p * g.q * N;
+
+  Acc<TM, TN> acc;
+  acc.zero();
+  if (active) {
+    const float* ap[TM];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) ap[a] = dyT + (long long)min(row0 + a * 32 + li, K - 1) * ldy + 4 * hh;
+    int kr[TN], ks[TN];
+    bool kok[TN];
+    const float* bp[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      int kidx = col0 + b * 32 + li;
+      kok[b] = kidx < RSC;
+      kidx = min(kidx, RSC - 1);
+      const int tap = kidx / C, kc = kidx - tap * C;
+      kr[b] = tap / g.s;
+      ks[b] = tap - kr[b] * g.s;
+      bp[b] = xT + (long long)kc * ldx + 4 * hh;
+    }
+    const int tap_first = col0 / C, tap_last = (min(col0 + TN * 32, RSC) - 1) / C;
+    const bool one_tap = tap_first == tap_last;
+    const int r1 = tap_first / g.s, s1 = tap_first - r1 * g.s;
+    const int T = Mout / 8;
+    const int S = g.splits * WK, zz = z * WK + wk;
+    const int it0 = split_lo(T, zz, S), it1 = split_lo(T, zz + 1, S);
+    // first chunk >= it whose (uniform) tap is inside the input, for one-tap tiles
+    auto advance = [&](int it) -> int {
+      if (!one_tap) return it;
+      while (it < it1) {
+        const int pos = (it * 8) / N;
+        const int pp = pos / g.q, qq = pos - pp * g.q;
+        const int hi = pp * g.st - g.pad + r1, wi = qq * g.st - g.pad + s1;
+        if (hi >= 0 && hi < g.h && wi >= 0 && wi < g.w) break;
+        it = (pos + 1) * N / 8;  // next position
+      }
+      return it;
+    };
+    auto load = [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
+      const int mbase = it * 8;
+      const int pos = mbase / N, n0 = mbase - pos * N;
+      const int pp = pos / g.q, qq = pos - pp * g.q;
+#pragma unroll
+      for (int a = 0; a < TM; ++a) A[a] = ld4(ap[a] + mbase);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int hi = pp * g.st - g.pad + kr[b], wi = qq * g.st - g.pad + ks[b];
+        const bool ok = kok[b] && hi >= 0 && hi < g.h && wi >= 0 && wi < g.w;
+        B[b] = ok ? ld4(bp[b] + ((long long)hi * g.w + wi) * N + n0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    int it = advance(it0);
+    f32x4 A[TM], B[TN];
+    if (it < it1) load(it, A, B);
+    while (it < it1) {
+      const int nit = advance(it + 1);
+      f32x4 An[TM], Bn[TN];
+      if (nit < it1) load(nit, An, Bn);
+      acc.mma4(A, B);
+#pragma unroll
+      for (int a = 0; a < TM; ++a) A[a] = An[a];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) B[b] = Bn[b];
+      it = nit;
+    }
+  }
+  acc.template combine<WN, WK>(lds, wn, wk, lane, active);
+  if (wk == 0 && active) {
+    float* out = g.splits > 1 ? dw + (long long)z * g.slab : dw;
+    acc.store(out, row0, col0, K, RSC, RSC, lane, false);
+  }
+  if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
+}
+
 
 __global__ __launch_bounds__(256) void k_reduce_slabs(long long count, int nslab, long long slab_stride,
                                                       const float* __restrict__ slabs, float* __restrict__ out,
@@ -635,9 +776,12 @@ ConvArgs make_args(const tspm_conv_shape* s) {
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = (long long)s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
-  g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0;
+  g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   return g;
 }
+
+constexpr int kMaxFusedSplits = 16;   // wgrad: in-launch slab reduction up to this many slabs
+constexpr int kMaxFusedMergeIters = 16;  // fwd: in-launch BN merge when each thread reads <= this many tiles
 
 bool is_hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
   if (!st) return true;
@@ -684,21 +828,36 @@ extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_
 }
 
 extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
-                             const tspm_strides4* xs, const float* w, float* y, float* bn_partial,
+                             const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn,
                              tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !w || !y) return TSPM_ERR_INVALID;
   Algo al = fwd_algo(s, user);
   if (!algo_supported(al)) return TSPM_ERR_INVALID;
+  tspm_bn_fuse bf{};
+  if (bn) {
+    bf = *bn;
+    if (!bf.partial && bf.counters) return TSPM_ERR_INVALID;
+    if (bf.counters && (!bf.save_mean || !bf.save_invstd)) return TSPM_ERR_INVALID;
+  }
   ConvArgs g = make_args(s);
   if (xs) { g.sn = xs->sn; g.sh = xs->sh; g.sw = xs->sw; g.sc = xs->sc; }
   g.m = s->p * s->q * s->n;
   hipStream_t st = static_cast<hipStream_t>(stream);
   dim3 grid(cdiv(g.m, al.tm * 32), cdiv(s->k, al.wn * al.tn * 32), 1);
-  const size_t lds = lds_bytes(al);
+  // in-launch merge only when the last arriver's per-thread read is short (tiles / thread groups);
+  // otherwise the parallel tspm_bn_finalize pass follows
+  const int tiles = (int)grid.x, groups = 2 * al.wk / al.tn;
+  const tspm_bn_fuse want = bf;
+  if (bf.counters && cdiv(tiles, groups) > kMaxFusedMergeIters) bf.counters = nullptr;
+  size_t lds = lds_bytes(al);
+  if (bf.counters) lds = std::max(lds, (size_t)16 + 8 * (size_t)(64 * al.wn * al.wk + 32 * al.wn * al.tn));
   const bool vec = is_hwnc(s, xs) && (s->c % 8 == 0);
-  if (vec) TSPM_DISPATCH(k_conv_fwd_vec, false, g, x, w, y, bn_partial);
-  else TSPM_DISPATCH(k_conv_fwd_gather, false, g, x, w, y, bn_partial);
+  if (vec) TSPM_DISPATCH(k_conv_fwd_vec, false, g, x, w, y, bf);
+  else TSPM_DISPATCH(k_conv_fwd_gather, false, g, x, w, y, bf);
   TSPM_LAUNCH_CHECK();
+  if (want.counters && !bf.counters)
+    return tspm_bn_finalize(g.m, s->k, tiles, al.tm * 32, want.partial, want.running_mean, want.running_var,
+                            want.momentum, want.eps, want.save_mean, want.save_invstd, stream);
   return TSPM_OK;
 }
 
@@ -730,7 +889,7 @@ extern "C" size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* s, const tspm
   if (!shape_ok(s)) return 0;
   Algo al = wgrad_algo(s, user);
   if (al.splits <= 1) return 0;
-  return (size_t)al.splits * s->k * s->r * s->s * s->c * sizeof(float);
+  return TSPM_COUNTER_BYTES + (size_t)al.splits * s->k * s->r * s->s * s->c * sizeof(float);
 }
 
 extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
@@ -747,20 +906,60 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   g.slab = (long long)s->k * RSC;
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* out = dw;
+  dim3 grid(cdiv(s->k, al.tm * 32), cdiv(RSC, al.wn * al.tn * 32), al.splits);
   if (al.splits > 1) {
     if (!ws || ws_bytes < tspm_conv_wgrad_workspace(s, user)) return TSPM_ERR_WORKSPACE;
-    out = static_cast<float*>(ws);
+    out = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+    // in-launch reduction when the last arriver's serial read is short; else a separate pass
+    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned))
+      g.cnt = static_cast<unsigned*>(ws);
   }
-  dim3 grid(cdiv(s->k, al.tm * 32), cdiv(RSC, al.wn * al.tn * 32), al.splits);
-  const size_t lds = lds_bytes(al);
-  if (s->n % 8 == 0) TSPM_DISPATCH(k_conv_wgrad, true, g, x, dy, out);
-  else TSPM_DISPATCH(k_conv_wgrad, false, g, x, dy, out);
+  const size_t lds = std::max(lds_bytes(al), (size_t)16);
+  if (s->n % 8 == 0) TSPM_DISPATCH(k_conv_wgrad, true, g, x, dy, out, dw);
+  else TSPM_DISPATCH(k_conv_wgrad, false, g, x, dy, out, dw);
   TSPM_LAUNCH_CHECK();
-  if (al.splits > 1) {
+  if (al.splits > 1 && !g.cnt) {  // separate slab reduction
     long long count = g.slab;
     int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
     hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, count, al.splits, g.slab,
-                       static_cast<const float*>(ws), dw, 0);
+                       static_cast<const float*>(out), dw, 0);
+    TSPM_LAUNCH_CHECK();
+  }
+  return TSPM_OK;
+}
+
+extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x_t, int64_t ldx,
+                                 const float* dy_t, int64_t ldy, float* dw, void* ws, size_t ws_bytes,
+                                 tspm_stream_t stream) {
+  if (!shape_ok(s) || !x_t || !dy_t || !dw) return TSPM_ERR_INVALID;
+  if (s->n % 8 != 0) return TSPM_ERR_INVALID;
+  if (ldx < (int64_t)s->h * s->w * s->n || ldy < (int64_t)s->p * s->q * s->n || (ldx & 3) || (ldy & 3))
+    return TSPM_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(dy_t)) & 15) return TSPM_ERR_INVALID;
+  Algo al = wgrad_algo(s, user);
+  if (!algo_supported(al)) return TSPM_ERR_INVALID;
+  ConvArgs g = make_args(s);
+  const int RSC = s->r * s->s * s->c;
+  g.m = s->k;
+  g.splits = al.splits;
+  g.slab = (long long)s->k * RSC;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* out = dw;
+  dim3 grid(cdiv(s->k, al.tm * 32), cdiv(RSC, al.wn * al.tn * 32), al.splits);
+  if (al.splits > 1) {
+    if (!ws || ws_bytes < tspm_conv_wgrad_workspace(s, user)) return TSPM_ERR_WORKSPACE;
+    out = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned))
+      g.cnt = static_cast<unsigned*>(ws);
+  }
+  const size_t lds = std::max(lds_bytes(al), (size_t)16);
+  TSPM_DISPATCH(k_conv_wgrad_t, false, g, x_t, (long long)ldx, dy_t, (long long)ldy, out, dw);
+  TSPM_LAUNCH_CHECK();
+  if (al.splits > 1 && !g.cnt) {
+    long long count = g.slab;
+    int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, count, al.splits, g.slab,
+                       static_cast<const float*>(out), dw, 0);
     TSPM_LAUNCH_CHECK();
   }
   return TSPM_OK;

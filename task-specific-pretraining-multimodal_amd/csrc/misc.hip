@@ -97,7 +97,7 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
 int gemm_small(const GemmArgs& g, hipStream_t st) {
   const int tiles = cdiv(g.M, 32) * cdiv(g.N, 32);
   int wk = 1;
-  while (wk < 16 && g.K / (wk * 2) >= 32) wk *= 2;
+  while (wk < 4 && g.K / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams
   const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
   switch (wk) {
     case 1: hipLaunchKernelGGL(k_gemm_small<1>, dim3(tiles), dim3(64), lds, st, g); break;
@@ -330,7 +330,7 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
-extern "C" int tspm_abi_version(void) { return 3; }
+extern "C" int tspm_abi_version(void) { return 5; }
 
 extern "C" const char* tspm_status_string(int status) {
   switch (status) {

@@ -37,6 +37,64 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(int N, int H, int W, int C,
   }
 }
 
+// Tiled variant for the transposed copy: [64 rows x 64 channels] per workgroup, y and idx as
+// above plus y_t[c][ld_t] (rows contiguous: the wgrad operand layout) through an LDS transpose.
+__global__ __launch_bounds__(256) void k_maxpool_fwd_t(int N, int H, int W, int C, int k, int st, int pad, int P,
+                                                       int Q, const float* __restrict__ x, float* __restrict__ y,
+                                                       uint8_t* __restrict__ idx, float* __restrict__ y_t,
+                                                       long long ld_t) {
+  __shared__ float tile[64][65];
+  const int t = threadIdx.x, l16 = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + l16;
+  const bool cok = 4 * c4 < C;
+  const long long M = (long long)P * Q * N;
+  const long long r0 = (long long)blockIdx.x * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = rg + 16 * i;
+    const long long row = r0 + rl;
+    f32x4 best = {0.f, 0.f, 0.f, 0.f};
+    if (cok && row < M) {
+      const int n = (int)(row % N);
+      const int pos = (int)(row / N);
+      const int p = pos / Q, q = pos - p * Q;
+      best = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      int bi[4] = {0, 0, 0, 0};
+      for (int kh = 0; kh < k; ++kh) {
+        const int h = p * st - pad + kh;
+        if (h < 0 || h >= H) continue;
+        for (int kw = 0; kw < k; ++kw) {
+          const int w = q * st - pad + kw;
+          if (w < 0 || w >= W) continue;
+          const f32x4 v = ld4(x + (((long long)h * W + w) * N + n) * C + 4 * c4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (v[j] > best[j] || isnan(v[j])) { best[j] = v[j]; bi[j] = kh * k + kw; }
+        }
+      }
+      st4(y + row * C + 4 * c4, best);
+      uchar4 u;
+      u.x = (uint8_t)bi[0]; u.y = (uint8_t)bi[1]; u.z = (uint8_t)bi[2]; u.w = (uint8_t)bi[3];
+      *reinterpret_cast<uchar4*>(idx + row * C + 4 * c4) = u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[rl][4 * l16 + j] = best[j];
+  }
+  __syncthreads();
+  const int cl = t >> 2, qq = t & 3;
+  const int c = blockIdx.y * 64 + cl;
+  if (c < C) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int rl = qq * 16 + 4 * kk;
+      if (r0 + rl < M) {
+        const f32x4 v = {tile[rl][cl], tile[rl + 1][cl], tile[rl + 2][cl], tile[rl + 3][cl]};
+        st4(y_t + (long long)c * ld_t + r0 + rl, v);
+      }
+    }
+  }
+}
+
 // gather form: every input element sums dy over the windows that picked it (deterministic order)
 __global__ __launch_bounds__(256) void k_maxpool_bwd(int N, int H, int W, int C, int k, int st, int pad, int P,
                                                      int Q, const float* __restrict__ dy,
@@ -115,11 +173,21 @@ int grid_for(long long work) {
 }  // namespace
 
 extern "C" int tspm_maxpool_fwd(int32_t n, int32_t h, int32_t w, int32_t c, int32_t k, int32_t stride, int32_t pad,
-                                int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, tspm_stream_t stream) {
+                                int32_t p, int32_t q, const float* x, float* y, uint8_t* idx, float* y_t,
+                                int64_t ld_t, tspm_stream_t stream) {
   if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 || k <= 0 || k > 15 || stride <= 0 || pad < 0 || !x || !y || !idx)
     return TSPM_ERR_INVALID;
   if (p != (h + 2 * pad - k) / stride + 1 || q != (w + 2 * pad - k) / stride + 1 || p <= 0 || q <= 0)
     return TSPM_ERR_INVALID;
+  if (y_t) {
+    const long long M = (long long)p * q * n;
+    if (M % 4 || ld_t < M || ld_t % 4 || (reinterpret_cast<uintptr_t>(y_t) & 15)) return TSPM_ERR_INVALID;
+    hipLaunchKernelGGL(k_maxpool_fwd_t, dim3((unsigned)cdiv64(M, 64), cdiv(c, 64)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, x, y, idx, y_t,
+                       (long long)ld_t);
+    TSPM_LAUNCH_CHECK();
+    return TSPM_OK;
+  }
   hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long long)p * q * n * c / 4)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, x, y, idx);
   TSPM_LAUNCH_CHECK();

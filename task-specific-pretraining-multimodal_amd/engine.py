@@ -107,6 +107,13 @@ class BlockPlan:
     g_y1: torch.Tensor = None
     g_y2: torch.Tensor = None
     g_yd: Optional[torch.Tensor] = None
+    # transposed copies ([C][rows], tspm_conv_wgrad_t operands): a1, out (if a later block reads
+    # it), and the three conv-output gradients
+    a1_t: Optional[torch.Tensor] = None
+    out_t: Optional[torch.Tensor] = None
+    g_y1_t: Optional[torch.Tensor] = None
+    g_y2_t: Optional[torch.Tensor] = None
+    g_yd_t: Optional[torch.Tensor] = None
 
 
 class EncoderEngine:
@@ -121,6 +128,13 @@ class EncoderEngine:
         # optional second stream: weight-grad convs and the downsample branch run there, off the
         # critical path (set by FusedTrainStep; None = everything on the caller's stream)
         self.aux: Optional[torch.cuda.Stream] = None
+        # HIP graph capture (ROCm 7) crashes in hipStreamEndCapture when a forked stream is joined
+        # into another forked stream (scripts/capture_repro.py: "nested", "nested_double_join");
+        # joins into the capture origin work.  So: fork_ds (the downsample branch, which must join
+        # back into this encoder's stream) only when this encoder runs on the origin stream, and
+        # join_aux=False lets the caller join the weight-grad stream into the origin itself.
+        self.fork_ds = True
+        self.join_aux = True
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
@@ -168,6 +182,21 @@ class EncoderEngine:
                 h, w, c = ho, wo, planes
         self.final_hw = (h, w)
         self.final_c = c
+        # weight gradients from transposed operands (16-byte loads on both GEMM operands) whenever
+        # an 8-row chunk shares one output position
+        self.use_t = N % 8 == 0
+        self.mp_t = None
+        if self.use_t:
+            self.mp_t = torch.empty(C0, self.mp.shape[0], **f32)
+            for i, bp in enumerate(self.blocks):
+                rows, planes = bp.out.shape
+                bp.a1_t = torch.empty(planes, rows, **f32)
+                if i + 1 < len(self.blocks):
+                    bp.out_t = torch.empty(planes, rows, **f32)
+                bp.g_y1_t = torch.empty(planes, rows, **f32)
+                bp.g_y2_t = torch.empty(planes, rows, **f32)
+                if bp.ds_conv is not None:
+                    bp.g_yd_t = torch.empty(planes, rows, **f32)
         self.pooled = torch.empty(N, c, **f32)
         self.hidden = encoder.fc.out_features
 
@@ -210,8 +239,12 @@ class EncoderEngine:
                         lib.tspm_bn_bwd_workspace(bn.rows, bn.channels))
         self.ws_conv_bytes = max(conv_ws, 256)
         self.ws_bn_bytes = max(bn_ws, 256)
-        self.ws_conv = torch.empty(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
-        self.ws_bn = torch.empty(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
+        # zero-filled once: both workspaces start with arrival counters that every call leaves zero
+        self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
+        ncnt = max(op.shape.k for op in self.all_convs()) // 32 + 1
+        self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
+        self.bn_cnt_aux = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
         part = max(3 * op.stat_tiles()[0] * op.shape.k for op in self.all_convs())
         self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
         ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
@@ -223,8 +256,9 @@ class EncoderEngine:
         for op in self.all_convs():
             s = op.shape
             base = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride)
-            for kind in ("fwd", "dgrad", "wgrad"):
-                v = table.get((kind,) + base)
+            wkind = "wgrad_t" if (self.use_t and op is not self.stem) else "wgrad"
+            for kind, key in (("fwd", "fwd"), ("dgrad", "dgrad"), ("wgrad", wkind)):
+                v = table.get((key,) + base)
                 if v is not None:
                     setattr(op, f"algo_{kind}", L.ConvAlgo(*v))
         self._alloc_workspace()
@@ -238,29 +272,29 @@ class EncoderEngine:
         return w
 
     def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                  bn_partial: Optional[torch.Tensor] = None) -> None:
+                  bnf: Optional[L.BnFuse] = None) -> None:
         lib = L.lib()
         s, a = op.shape, op.algo_fwd
         if self.conv_timer:
             self.conv_timer.begin(op, "fwd")
         L.check(lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x_ptr, ctypes.byref(strides), self._w(op).data_ptr(),
-                                  y.data_ptr(), L.ptr(bn_partial), sh), "conv_fwd")
+                                  y.data_ptr(), None if bnf is None else ctypes.byref(bnf), sh), "conv_fwd")
         if self.conv_timer:
             self.conv_timer.end()
 
     def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                 part: Optional[torch.Tensor] = None) -> None:
-        """conv forward whose epilogue emits BN partial statistics, then the per-channel merge."""
-        part = self.bn_part if part is None else part
-        self._conv_fwd(op, x_ptr, strides, y, sh, part)
-        tiles, rows = op.stat_tiles()
+                 aux: bool = False) -> None:
+        """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
+        per channel block, merges them (save_mean/invstd + running statistics): one launch."""
         m = bn.module
-        L.check(L.lib().tspm_bn_finalize(bn.rows, bn.channels, tiles, rows, part.data_ptr(),
-                                         L.ptr(m.running_mean), L.ptr(m.running_var),
-                                         BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                                         bn.invstd.data_ptr(), sh), "bn_finalize")
+        part, cnt = (self.bn_part_aux, self.bn_cnt_aux) if aux else (self.bn_part, self.bn_cnt)
+        bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
+                       BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
+                       bn.invstd.data_ptr())
+        self._conv_fwd(op, x_ptr, strides, y, sh, bnf)
 
-    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True):
+    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
+               out_t: Optional[torch.Tensor] = None):
         lib = L.lib()
         m = bn.module
         if train:
@@ -268,7 +302,8 @@ class EncoderEngine:
                                       m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res),
                                       L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
                                       L.ptr(bn2.module.weight) if bn2 else None, L.ptr(bn2.module.bias) if bn2 else None,
-                                      1 if relu else 0, out.data_ptr(), sh), "bn_apply")
+                                      1 if relu else 0, out.data_ptr(), L.ptr(out_t),
+                                      bn.rows if out_t is not None else 0, sh), "bn_apply")
         else:
             m2 = bn2.module if bn2 else None
             L.check(lib.tspm_bn_apply_eval(bn.rows, bn.channels, y.data_ptr(), m.running_mean.data_ptr(),
@@ -320,27 +355,29 @@ class EncoderEngine:
         else:
             self._conv_fwd_eval(self.stem, x.data_ptr(), xs, self.y0, sh)
         self._apply(self.stem_bn, self.y0, self.a0, relu=True, sh=sh, train=train)
+        mp_t = self.mp_t if train else None
         L.check(lib.tspm_maxpool_fwd(N, p1, q1, C0, 3, 2, 1, p2, q2, self.a0.data_ptr(), self.mp.data_ptr(),
-                                     self.mp_idx.data_ptr(), sh), "maxpool_fwd")
+                                     self.mp_idx.data_ptr(), L.ptr(mp_t), self.mp.shape[0] if mp_t is not None else 0,
+                                     sh), "maxpool_fwd")
         xin = self.mp
         for bp in self.blocks:
             s1 = bp.conv1.shape
             xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
-            fork = bp.ds_conv is not None and self.aux is not None
+            fork = bp.ds_conv is not None and self.aux is not None and self.fork_ds
             if fork:  # downsample conv + BN statistics concurrently with conv1 -> bn1 -> conv2
                 main = torch.cuda.current_stream()
                 self.aux.wait_stream(main)
                 with torch.cuda.stream(self.aux):
                     ash = self.aux.cuda_stream
                     if train:
-                        self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, ash, self.bn_part_aux)
+                        self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, ash, aux=True)
                     else:
                         self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, ash)
             if train:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
                 self._conv_fwd_eval(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
-            self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
+            self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train, out_t=bp.a1_t if train else None)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             if train:
@@ -354,9 +391,11 @@ class EncoderEngine:
                     self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
                 else:
                     self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train,
+                            out_t=bp.out_t if train else None)
             else:
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train,
+                            out_t=bp.out_t if train else None)
             xin = bp.out
         h, w = self.final_hw
         L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh), "avgpool_fwd")
@@ -372,7 +411,8 @@ class EncoderEngine:
     def _grad(self, p: torch.Tensor) -> torch.Tensor:
         return self.grad_of(p)
 
-    def _bn_bwd(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None, sh=0):
+    def _bn_bwd(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None, sh=0,
+                dy_t=None, dy2_t=None):
         lib = L.lib()
         m = bn.module
         gw, gb = self._grad(m.weight), self._grad(m.bias)
@@ -383,10 +423,12 @@ class EncoderEngine:
                                 bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
                                 L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
                                 L.ptr(bn2.module.weight) if bn2 else None, L.ptr(gw2) if bn2 else None,
-                                L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), self.ws_bn.data_ptr(),
-                                self.ws_bn_bytes, sh), "bn_bwd")
+                                L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), L.ptr(dy_t), L.ptr(dy2_t),
+                                bn.rows if dy_t is not None else 0, self.ws_bn.data_ptr(), self.ws_bn_bytes, sh),
+                "bn_bwd")
 
-    def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int) -> None:
+    def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int,
+               x_t: Optional[torch.Tensor] = None, dy_t: Optional[torch.Tensor] = None) -> None:
         lib = L.lib()
         gw = self._grad(op.module.weight)
         if not gw.is_contiguous(memory_format=torch.channels_last):
@@ -394,15 +436,21 @@ class EncoderEngine:
         if self.aux is not None:  # off the critical path: only Adam consumes weight gradients
             self.aux.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.aux):
-                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream)
+                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream, x_t, dy_t)
         else:
-            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh)
+            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh, x_t, dy_t)
 
     def _wgrad_launch(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, gw: torch.Tensor,
-                      sh: int) -> None:
+                      sh: int, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor]) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "wgrad")
-        L.check(L.lib().tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr,
+        lib = L.lib()
+        if x_t is not None and dy_t is not None:
+            L.check(lib.tspm_conv_wgrad_t(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_t.data_ptr(),
+                                          x_t.shape[1], dy_t.data_ptr(), dy_t.shape[1], gw.data_ptr(),
+                                          self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_wgrad_t")
+        else:
+            L.check(lib.tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr,
                                         ctypes.byref(strides), dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(),
                                         self.ws_conv_bytes, sh), "conv_wgrad")
         if self.conv_timer:
@@ -446,24 +494,26 @@ class EncoderEngine:
             d2 = bp.g_y2
             if bp.ds_conv is not None:
                 dd = bp.g_yd
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh, dy_t=bp.g_y2_t,
+                             dy2_t=bp.g_yd_t)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh, dy_t=bp.g_y2_t)
             s2 = bp.conv2.shape
-            self._wgrad(bp.conv2, bp.a1.data_ptr(), L.hwnc_strides(N, s2.h, s2.w, s2.c), d2, sh)
+            self._wgrad(bp.conv2, bp.a1.data_ptr(), L.hwnc_strides(N, s2.h, s2.w, s2.c), d2, sh, bp.a1_t, bp.g_y2_t)
             da1 = self.da1[:n_out]
             self._dgrad(bp.conv2, d2, da1, 0, sh)
             d1 = bp.g_y1
-            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
+            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh, dy_t=bp.g_y1_t)
             if self.debug_hook is not None:
                 self.debug_hook(f"block{i}.g_out", Gv)
                 self.debug_hook(f"block{i}.d_y2", d2)
                 self.debug_hook(f"block{i}.d_a1", da1)
                 self.debug_hook(f"block{i}.d_y1", d1)
-            self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
+            xin_t = (self.blocks[i - 1].out_t if i > 0 else self.mp_t) if self.use_t else None
+            self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh, xin_t, bp.g_y1_t)
             if bp.ds_conv is not None:
-                self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
+                self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh, xin_t, bp.g_yd_t)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             self._dgrad(bp.conv1, d1, Gnv, 1, sh)
             G, Gn = Gn, G
@@ -474,7 +524,7 @@ class EncoderEngine:
                                      self.g_stem.data_ptr(), sh), "maxpool_bwd")
         self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
         self._wgrad(self.stem, self.x_in.data_ptr(), self.input_strides(self.x_in), self.dy_stem, sh)
-        if self.aux is not None:
+        if self.aux is not None and self.join_aux:
             torch.cuda.current_stream().wait_stream(self.aux)
 
 

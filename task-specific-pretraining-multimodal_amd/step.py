@@ -114,7 +114,11 @@ class FusedTrainStep:
         # matching the 4 hardware queues HIP gives a process by default
         self.aux_a = torch.cuda.Stream(device=dev)
         self.aux_i = torch.cuda.Stream(device=dev)
-        self.serial = False  # True: every launch on the caller's stream (per-kernel timing)
+        self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
+        # Off by default: measured on MI355X (ROCm 7), an eager step gains ~3 % from the auxiliary
+        # streams but a replayed HIP graph with their ~50 cross-stream edges runs ~30 % SLOWER than
+        # the two-branch graph (25.5k vs 36.4k samples/s at batch 128).  TSPM_AUX=1 turns them on.
+        self.use_aux = os.environ.get("TSPM_AUX", "0") == "1"
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.calls = 0
@@ -177,8 +181,12 @@ class FusedTrainStep:
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
-        self.eng_a.aux = None if self.serial else self.aux_a
-        self.eng_i.aux = None if self.serial else self.aux_i
+        self.eng_a.aux = None if self.serial or not self.use_aux else self.aux_a
+        self.eng_i.aux = None if self.serial or not self.use_aux else self.aux_i
+        # see EncoderEngine.fork_ds: the image encoder runs on a forked stream, so its helper
+        # stream may only join the origin (main) stream
+        self.eng_i.fork_ds = False
+        self.eng_i.join_aux = False
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
@@ -195,6 +203,9 @@ class FusedTrainStep:
             self.eng_i.backward(self.dfused[:, ea:], self.F)
         self.eng_a.backward(self.dfused, self.F)
         main.wait_stream(side)
+        if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
+            main.wait_stream(self.aux_a)
+            main.wait_stream(self.aux_i)
         self.nbt.add_(1)
 
     def _opt(self) -> None:

@@ -50,9 +50,14 @@ def conv_fwd(x_nchw: torch.Tensor, w_oihw: torch.Tensor, stride: int, pad: int, 
     return from_hwnc(y, n, shp.p, shp.q, k)
 
 
-def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0)):
-    """conv forward whose epilogue emits BN partials, merged by tspm_bn_finalize: returns
-    (y NCHW, mean, invstd)."""
+def zeroed_counters(k: int, dev) -> torch.Tensor:
+    return torch.zeros(k // 32 + 1, dtype=torch.int32, device=dev)
+
+
+def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0), fused=True, counters=None,
+                        running=None):
+    """conv forward whose epilogue emits BN partials — merged in-launch by the last workgroup of
+    each channel block (fused) or by tspm_bn_finalize — returns (y NCHW, mean, invstd)."""
     n, c, h, w = x_nchw.shape
     k, _, r, s = w_oihw.shape
     shp = shape(n, h, w, c, k, r, s, stride, pad)
@@ -67,12 +72,20 @@ def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0)):
     tiles = lib.tspm_conv_fwd_tiles(ctypes.byref(shp), ctypes.byref(a))
     rows = lib.tspm_conv_fwd_tile_rows(ctypes.byref(shp), ctypes.byref(a))
     part = torch.empty(3 * tiles * k, device=dev)
-    L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
-                              y.data_ptr(), part.data_ptr(), sh()), "conv_fwd")
     mean = torch.empty(k, device=dev)
     inv = torch.empty(k, device=dev)
-    L.check(lib.tspm_bn_finalize(m, k, tiles, rows, part.data_ptr(), None, None, 0.1, 1e-5, mean.data_ptr(),
-                                 inv.data_ptr(), sh()), "bn_finalize")
+    rm, rv = running if running is not None else (None, None)
+    if fused:
+        cnt = counters if counters is not None else zeroed_counters(k, dev)
+        bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(rm), L.ptr(rv), 0.1, 1e-5, mean.data_ptr(),
+                       inv.data_ptr())
+    else:
+        bnf = L.BnFuse(part.data_ptr(), None, None, None, 0.1, 1e-5, None, None)
+    L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
+                              y.data_ptr(), ctypes.byref(bnf), sh()), "conv_fwd")
+    if not fused:
+        L.check(lib.tspm_bn_finalize(m, k, tiles, rows, part.data_ptr(), L.ptr(rm), L.ptr(rv), 0.1, 1e-5,
+                                     mean.data_ptr(), inv.data_ptr(), sh()), "bn_finalize")
     return from_hwnc(y, n, shp.p, shp.q, k), mean, inv
 
 
@@ -117,7 +130,7 @@ def conv_wgrad(x_nchw: torch.Tensor, dy_nchw: torch.Tensor, rs, stride: int, pad
     dw = torch.empty(k, c, r, s, device=dev).contiguous(memory_format=torch.channels_last)
     lib = L.lib()
     wsb = lib.tspm_conv_wgrad_workspace(ctypes.byref(shp), ctypes.byref(a))
-    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=dev)  # counter header must start zero
     L.check(lib.tspm_conv_wgrad(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), dyd.data_ptr(),
                                 dw.data_ptr(), ws.data_ptr(), wsb, sh()), "conv_wgrad")
     return dw.contiguous()

@@ -63,7 +63,11 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.tspm_bn_stats(0, 64, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 1 << 20, None) == 1
     assert lib.tspm_bn_stats(128, 66, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 1 << 20, None) == 1
     assert lib.tspm_bn_stats(128, 64, 16, 1, 0, None, None, None, 0.1, 1e-5, 16, 16, 16, 0, None) == 3
-    assert lib.tspm_maxpool_fwd(2, 8, 8, 64, 3, 2, 1, 5, 4, 16, 16, 16, None) == 1
+    assert lib.tspm_maxpool_fwd(2, 8, 8, 64, 3, 2, 1, 5, 4, 16, 16, 16, None, 0, None) == 1
+    # wgrad_t: n % 8 != 0 and unaligned leading dimensions are rejected
+    s6 = L.ConvShape(6, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
+    assert lib.tspm_conv_wgrad_t(ctypes.byref(s6), ctypes.byref(a), 16, 384, 16, 384, 16, None, 0, None) == 1
+    assert lib.tspm_conv_wgrad_t(ctypes.byref(good), ctypes.byref(a), 16, 130, 16, 128, 16, None, 0, None) == 1
     assert lib.tspm_adam_step(10, 17, 16, 16, 16, 16, None) == 1   # misaligned
     assert lib.tspm_dropout_mask(10, 1.0, 0, None, 16, None) == 1   # p must be < 1
 
@@ -75,6 +79,6 @@ def test_workspace_queries():
     assert lib.tspm_conv_fwd_tiles(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 1))) == 7 * 7 * 128 // 32
     assert lib.tspm_conv_fwd_tile_rows(ctypes.byref(s), ctypes.byref(L.ConvAlgo(2, 2, 1, 1, 1))) == 64
     w3 = lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 3)))
-    assert w3 == 3 * 64 * 9 * 64 * 4
+    assert w3 == L.COUNTER_BYTES + 3 * 64 * 9 * 64 * 4
     assert lib.tspm_bn_stats_workspace(6272, 64) > 0
     assert lib.tspm_bn_bwd_workspace(6272, 64) >= lib.tspm_bn_stats_workspace(6272, 64)

@@ -125,15 +125,17 @@ def test_stem_wgrad_nchw_input(gpu, case):
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 5, 6, 8, 12)])
 @pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 2, 2, 1), (1, 1, 1, 8, 1)])
 @pytest.mark.parametrize("offset", [0.0, 3e4])
-def test_conv_fwd_epilogue_bn_statistics(gpu, case, algo, offset):
-    """BatchNorm batch statistics of the conv output from the conv epilogue's per-tile partials."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_conv_fwd_epilogue_bn_statistics(gpu, case, algo, offset, fused):
+    """BatchNorm batch statistics of the conv output from the conv epilogue's per-tile partials,
+    merged in-launch (fused) or by tspm_bn_finalize."""
     from abi_helpers import conv_fwd_with_stats
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(31)
     x = torch.randn(n, c, h, w, generator=g) + offset / 100
     wt = torch.randn(k, c, r, s, generator=g) * 0.05
     wt[:, :, r // 2, s // 2] += offset / (c * 100)  # push channel means far from zero
-    y, mean, inv = conv_fwd_with_stats(x.to(gpu), wt.to(gpu), st, pad, algo)
+    y, mean, inv = conv_fwd_with_stats(x.to(gpu), wt.to(gpu), st, pad, algo, fused=fused)
     torch.cuda.synchronize()
     yd = y.double().cpu()
     mean_ref = yd.mean((0, 2, 3))
@@ -148,7 +150,7 @@ def test_conv_fwd_epilogue_bn_statistics(gpu, case, algo, offset):
 # ------------------------------------------------------------------------------------------------
 def _bn_ws(lib, m, c, dev, bwd=False):
     b = (lib.tspm_bn_bwd_workspace if bwd else lib.tspm_bn_stats_workspace)(m, c)
-    return torch.empty(max(b, 16), dtype=torch.uint8, device=dev), b
+    return torch.zeros(max(b, 16), dtype=torch.uint8, device=dev), b  # counter header starts zero
 
 
 @pytest.mark.parametrize("m,c,offset", [(6272, 64, 0.0), (128, 512, 3.0), (96256, 64, 1e7), (4, 512, 0.5), (600, 128, -2e3)])
@@ -180,7 +182,7 @@ def test_bn_stats_and_apply(gpu, m, c, offset, nslab):
     out = torch.empty(m, c, device=gpu)
     d_gamma, d_beta = gamma.to(gpu), beta.to(gpu)  # keep alive: a freed temporary's block is reused at once
     L.check(lib.tspm_bn_apply(m, c, src.data_ptr(), mean.data_ptr(), inv.data_ptr(), d_gamma.data_ptr(),
-                              d_beta.data_ptr(), 0, None, None, None, None, None, 0, out.data_ptr(), sh()),
+                              d_beta.data_ptr(), 0, None, None, None, None, None, 0, out.data_ptr(), None, 0, sh()),
             "bn_apply")
     torch.cuda.synchronize()
     scale = ysum.abs().max(0).values + 1.0
@@ -256,7 +258,7 @@ def test_bn_block_fwd_bwd(gpu, m, c, mode):
     L.check(lib.tspm_bn_apply(m, c, dy_.data_ptr(), means[0].data_ptr(), invs[0].data_ptr(), dg.data_ptr(), db.data_ptr(),
                               mode, L.ptr(r), means[1].data_ptr() if mode == 2 else None,
                               invs[1].data_ptr() if mode == 2 else None, dg2.data_ptr() if mode == 2 else None,
-                              db2.data_ptr() if mode == 2 else None, 1, out.data_ptr(), sh()), "apply")
+                              db2.data_ptr() if mode == 2 else None, 1, out.data_ptr(), None, 0, sh()), "apply")
     torch.cuda.synchronize()
     assert torch.allclose(out.double().cpu(), out_ref.detach(), rtol=1e-4, atol=1e-4)
     # backward
@@ -273,7 +275,7 @@ def test_bn_block_fwd_bwd(gpu, m, c, mode):
                             dy2_.data_ptr() if two else None, means[1].data_ptr() if two else None,
                             invs[1].data_ptr() if two else None, dg2.data_ptr() if two else None,
                             gw2.data_ptr() if two else None, gb2.data_ptr() if two else None,
-                            L.ptr(dy2o), L.ptr(dreso), ws.data_ptr(), wsb, sh()), "bn_bwd")
+                            L.ptr(dy2o), L.ptr(dreso), None, None, 0, ws.data_ptr(), wsb, sh()), "bn_bwd")
     torch.cuda.synchronize()
     yl, gal, bel = leaves[:3]
     assert torch.allclose(dyo.double().cpu(), yl.grad, rtol=1e-3, atol=2e-5)
@@ -305,7 +307,18 @@ def test_maxpool(gpu, n, c, h, w):
     xd = to_hwnc(x.to(gpu))
     y = torch.empty(p * q * n, c, device=gpu)
     idx = torch.empty(p * q * n, c, dtype=torch.uint8, device=gpu)
-    L.check(lib.tspm_maxpool_fwd(n, h, w, c, 3, 2, 1, p, q, xd.data_ptr(), y.data_ptr(), idx.data_ptr(), sh()), "mp fwd")
+    L.check(lib.tspm_maxpool_fwd(n, h, w, c, 3, 2, 1, p, q, xd.data_ptr(), y.data_ptr(), idx.data_ptr(), None, 0, sh()),
+            "mp fwd")
+    if (p * q * n) % 4 == 0:  # tiled variant with the transposed copy: same y / idx bitwise, y_t = y^T
+        ld_t = p * q * n + 4
+        y2, idx2 = torch.empty_like(y), torch.empty_like(idx)
+        yt = torch.full((c, ld_t), 7.0, device=gpu)
+        L.check(lib.tspm_maxpool_fwd(n, h, w, c, 3, 2, 1, p, q, xd.data_ptr(), y2.data_ptr(), idx2.data_ptr(),
+                                     yt.data_ptr(), ld_t, sh()), "mp fwd_t")
+        torch.cuda.synchronize()
+        assert torch.equal(y2, y) and torch.equal(idx2, idx)
+        assert torch.equal(yt[:, :p * q * n], y.view(p * q * n, c).t())
+        assert bool((yt[:, p * q * n:] == 7.0).all())
     dx = torch.empty(h * w * n, c, device=gpu)
     gd = to_hwnc(gout.to(gpu))
     L.check(lib.tspm_maxpool_bwd(n, h, w, c, 3, 2, 1, p, q, gd.data_ptr(), idx.data_ptr(), dx.data_ptr(), sh()), "mp bwd")
@@ -462,3 +475,150 @@ def test_linear_strided_rows(gpu):
     assert torch.allclose(y[:, :o].double().cpu(), x @ w.double().T, rtol=1e-5, atol=1e-4)
     assert torch.equal(y[:, o:].cpu(), torch.full((n, ldy - o), 7.0))
     assert torch.allclose(dw.double().cpu(), gy[:, :o].double().T @ x, rtol=1e-5, atol=1e-4)
+
+
+def test_fused_bn_counters_rearm_and_running_stats(gpu):
+    """The in-launch merge leaves its counters zero (so one buffer serves every launch), repeated
+    launches give identical statistics, and the running statistics follow nn.BatchNorm2d."""
+    from abi_helpers import conv_fwd_with_stats, zeroed_counters
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(128, 64, 7, 7, generator=g).to(gpu)
+    wt = (torch.randn(128, 64, 3, 3, generator=g) * 0.05).to(gpu)
+    cnt = zeroed_counters(128, gpu)
+    rm = torch.zeros(128, device=gpu)
+    rv = torch.ones(128, device=gpu)
+    outs = []
+    for algo in [(1, 2, 1, 4, 1), (1, 2, 1, 4, 1), (2, 2, 2, 2, 1), (1, 1, 4, 1, 1)]:
+        outs.append(conv_fwd_with_stats(x, wt, 2, 1, algo, fused=True, counters=cnt, running=(rm, rv)))
+        torch.cuda.synchronize()
+        assert int(cnt.abs().sum()) == 0
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+    y = outs[0][0].double().cpu()
+    mean_ref = y.mean((0, 2, 3))
+    var_unb = y.var((0, 2, 3), unbiased=True)
+    rm_ref, rv_ref = torch.zeros(128, dtype=torch.float64), torch.ones(128, dtype=torch.float64)
+    for _ in range(4):
+        rm_ref = 0.9 * rm_ref + 0.1 * mean_ref
+        rv_ref = 0.9 * rv_ref + 0.1 * var_unb
+    assert torch.allclose(rm.double().cpu(), rm_ref, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(rv.double().cpu(), rv_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_wgrad_split_counters_rearm(gpu):
+    """Split-K weight gradient with the in-launch slab reduction: repeated calls of different split
+    counts through ONE zeroed workspace stay within the fp32 bound of the fp64 result (the last
+    arriver of each tile re-arms its counter), and the counter header is zero afterwards."""
+    import ctypes
+    from abi_helpers import shape, sh, to_hwnc
+    from tspm_amd import _lib as L
+    lib = L.lib()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(128, 64, 7, 7, generator=g)
+    dy = torch.randn(128, 64, 7, 7, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (64, 64, 3, 3), dy.double(), 1, 1)
+    bound = torch.nn.grad.conv2d_weight(x.double().abs(), (64, 64, 3, 3), dy.double().abs(), 1, 1)
+    shp = shape(128, 7, 7, 64, 64, 3, 3, 1, 1)
+    xd, dyd = to_hwnc(x.to(gpu)), to_hwnc(dy.to(gpu))
+    st = L.hwnc_strides(128, 7, 7, 64)
+    need = max(lib.tspm_conv_wgrad_workspace(ctypes.byref(shp), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, sp)))
+               for sp in (2, 5, 16))
+    ws = torch.zeros(need, dtype=torch.uint8, device=gpu)
+    for sp in (2, 5, 16, 5, 2):
+        dw = torch.empty(64, 64, 3, 3, device=gpu).contiguous(memory_format=torch.channels_last)
+        a = L.ConvAlgo(1, 1, 1, 4, sp)
+        L.check(lib.tspm_conv_wgrad(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st),
+                                    dyd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, sh()), "wgrad")
+        torch.cuda.synchronize()
+        _check(dw.contiguous(), ref, bound, f"split {sp}")
+        assert int(ws[:L.COUNTER_BYTES].int().sum()) == 0
+
+
+@pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (96, 128)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_bn_transposed_copies(gpu, m, c, mode):
+    """The tiled kernels that also write transposed copies (the tspm_conv_wgrad_t operand layout)
+    give bitwise the same HWNC outputs as the plain kernels, and the copies are exact transposes."""
+    from tspm_amd import _lib as L
+    lib = L.lib()
+    g = torch.Generator().manual_seed(8)
+    t = lambda *sh_, s=1.0: (torch.randn(*sh_, generator=g) * s).to(gpu)  # noqa: E731
+    y, y2, res, gout = t(m, c, s=3), t(m, c, s=2), t(m, c), t(m, c)
+    mean, inv, gamma, beta = t(c), t(c).abs() + 0.5, t(c), t(c)
+    mean2, inv2, gamma2, beta2 = t(c), t(c).abs() + 0.5, t(c), t(c)
+    two = mode == 2
+    r = res if mode == 1 else (y2 if two else None)
+    ld_t = m + 8
+
+    def apply(out, out_t):
+        L.check(lib.tspm_bn_apply(m, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                  mode, L.ptr(r), mean2.data_ptr() if two else None, inv2.data_ptr() if two else None,
+                                  gamma2.data_ptr() if two else None, beta2.data_ptr() if two else None, 1,
+                                  out.data_ptr(), L.ptr(out_t), ld_t if out_t is not None else 0, sh()), "apply")
+
+    o1, o2 = torch.empty(m, c, device=gpu), torch.empty(m, c, device=gpu)
+    ot = torch.zeros(c, ld_t, device=gpu)
+    apply(o1, None)
+    apply(o2, ot)
+
+    def bwd(dy, dy2, dres, dy_t, dy2_t):
+        ws, wsb = _bn_ws(lib, m, c, gpu, bwd=True)
+        gw, gb, gw2, gb2 = (torch.empty(c, device=gpu) for _ in range(4))
+        L.check(lib.tspm_bn_bwd(m, c, gout.data_ptr(), o1.data_ptr(), y.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                gamma.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
+                                y2.data_ptr() if two else None, mean2.data_ptr() if two else None,
+                                inv2.data_ptr() if two else None, gamma2.data_ptr() if two else None,
+                                gw2.data_ptr() if two else None, gb2.data_ptr() if two else None, L.ptr(dy2),
+                                L.ptr(dres), L.ptr(dy_t), L.ptr(dy2_t), ld_t if dy_t is not None else 0, ws.data_ptr(),
+                                wsb, sh()), "bn_bwd")
+
+    mk = lambda: torch.empty(m, c, device=gpu)  # noqa: E731
+    a = [mk(), mk() if two else None, mk() if mode == 1 else None]
+    b = [mk(), mk() if two else None, mk() if mode == 1 else None]
+    dyt = torch.zeros(c, ld_t, device=gpu)
+    dy2t = torch.zeros(c, ld_t, device=gpu) if two else None
+    bwd(*a, None, None)
+    bwd(*b, dyt, dy2t)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.equal(ot[:, :m], o1.t())
+    for u, v in zip(a, b):
+        if u is not None:
+            assert torch.equal(u, v)
+    assert torch.equal(dyt[:, :m], b[0].t())
+    if two:
+        assert torch.equal(dy2t[:, :m], b[1].t())
+
+
+@pytest.mark.parametrize("case", [CONV_CASES[i] for i in range(len(CONV_CASES))])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (1, 1, 1, 4, 1), (2, 2, 1, 2, 3), (1, 2, 2, 2, 1), (1, 1, 1, 16, 6),
+                                  (1, 1, 1, 8, 20)])
+def test_conv_wgrad_transposed(gpu, case, algo):
+    """tspm_conv_wgrad_t (operands in the transposed [C][rows] layout) vs fp64."""
+    import ctypes
+    from abi_helpers import shape, to_hwnc
+    from tspm_amd import _lib as L
+    n, c, h, w, k, r, s_, st, pad = case
+    if n % 8:
+        pytest.skip("wgrad_t needs n % 8 == 0")
+    lib = L.lib()
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(n, c, h, w, generator=g)
+    p = (h + 2 * pad - r) // st + 1
+    q = (w + 2 * pad - s_) // st + 1
+    dy = torch.randn(n, k, p, q, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (k, c, r, s_), dy.double(), st, pad)
+    bound = torch.nn.grad.conv2d_weight(x.double().abs(), (k, c, r, s_), dy.double().abs(), st, pad)
+    shp = shape(n, h, w, c, k, r, s_, st, pad)
+    ldx, ldy = h * w * n + 4, p * q * n + 12
+    xt = torch.zeros(c, ldx, device=gpu)
+    xt[:, :h * w * n] = to_hwnc(x.to(gpu)).t()
+    dyt = torch.zeros(k, ldy, device=gpu)
+    dyt[:, :p * q * n] = to_hwnc(dy.to(gpu)).t()
+    a = L.ConvAlgo(*algo)
+    wsb = lib.tspm_conv_wgrad_workspace(ctypes.byref(shp), ctypes.byref(a))
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
+    dw = torch.empty(k, c, r, s_, device=gpu).contiguous(memory_format=torch.channels_last)
+    L.check(lib.tspm_conv_wgrad_t(ctypes.byref(shp), ctypes.byref(a), xt.data_ptr(), ldx, dyt.data_ptr(), ldy,
+                                  dw.data_ptr(), ws.data_ptr(), wsb, sh()), "wgrad_t")
+    torch.cuda.synchronize()
+    _check(dw.contiguous(), ref, bound, f"wgrad_t {case} {algo}")
