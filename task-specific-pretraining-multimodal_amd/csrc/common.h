@@ -46,19 +46,21 @@ static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
     if (e__ != hipSuccess) return TSPM_ERR_LAUNCH;        \
   } while (0)
 
-// In-launch hand-off to the LAST arriving workgroup of a group (cdna_hip_programming.md §5,
-// "in-launch split-K reduction" recipe): every wave drains its global stores, the workgroup
-// releases at agent scope (per-XCD L2s are not coherent) and draws a ticket; the workgroup that
-// draws total-1 acquires at agent scope, re-arms the counter to 0 for the next launch and returns
-// true in every thread.  `flag` is one int of the kernel's (dynamic) LDS array.  Every thread of
-// the workgroup must call this (it contains barriers).  Counters must be zero before the first
-// launch that uses them.
+// Write-through (sc1) store: visible at agent scope once the storing wave drains vmcnt, without
+// a release fence (whose buffer_wbl2 writes back the whole XCD L2).
+TSPM_DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// In-launch hand-off to the LAST arriving workgroup of a group (cdna_hip_programming.md §5 and
+// §6 Guideline 16, the sc1 form): every wave has stored its share of the payload with st_sc1 and
+// drains vmcnt, the workgroup draws a ticket (relaxed agent-scope add); the workgroup that draws
+// total-1 acquires at agent scope (drops this CU's stale L1 lines), re-arms the counter to 0 for the
+// next launch and returns true in every thread.  `flag` is one int of the kernel's LDS.  Every
+// thread of the workgroup must call this (it contains barriers).  Counters must be zero before the
+// first launch that uses them.
 TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == total - 1;
     if (last) {

@@ -56,7 +56,9 @@ struct Acc {
         for (int b = 0; b < TN; ++b) v[a][b] = mfma32(A[a][j], B[b][j], v[a][b]);
   }
   // store rows row0 + a*32 + acc_row, cols col0 + b*32 + (lane&31) of a [rows, ld] matrix
-  TSPM_DEV void store(float* out, int row0, int col0, int rows, int cols, long long ld, int lane, bool accumulate) const {
+  // (sc1: write-through, the payload of an in-launch hand-off)
+  TSPM_DEV void store(float* out, int row0, int col0, int rows, int cols, long long ld, int lane, bool accumulate,
+                      bool sc1 = false) const {
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -68,7 +70,8 @@ struct Acc {
           const int row = row0 + a * 32 + acc_row(i, lane);
           if (row < rows) {
             float* p = out + (long long)row * ld + col;
-            *p = accumulate ? (*p + v[a][b][i]) : v[a][b][i];
+            if (sc1) st_sc1(p, v[a][b][i]);
+            else *p = accumulate ? (*p + v[a][b][i]) : v[a][b][i];
           }
         }
       }
@@ -105,7 +108,7 @@ struct Acc {
   // BatchNorm partial statistics of this tile's valid rows, per column (channel):
   //   part[0][mt][col] = K (the tile's first row), part[1][..] = mean - K, part[2][..] = M2
   TSPM_DEV void bn_partials(float* part, long long plane, int mt, int row0, int col0, int rows, int cols,
-                            int lane) const {
+                            int lane, bool sc1) const {
     const int cnt = min(TM * 32, rows - row0);
     const float inv = 1.0f / (float)cnt;
 #pragma unroll
@@ -134,9 +137,13 @@ struct Acc {
       s2 += __shfl_xor(s2, 32, 64);
       if (lane < 32 && col < cols) {
         const double n = (double)cnt;
-        part[(long long)mt * cols + col] = K;
-        part[plane + (long long)mt * cols + col] = (float)((double)off + (double)sd / n);
-        part[2 * plane + (long long)mt * cols + col] = (float)((double)s2 - (double)sd * (double)sd / n);
+        const float v0 = K, v1 = (float)((double)off + (double)sd / n), v2 = (float)((double)s2 - (double)sd * (double)sd / n);
+        float* p0 = part + (long long)mt * cols + col;
+        if (sc1) {
+          st_sc1(p0, v0); st_sc1(p0 + plane, v1); st_sc1(p0 + 2 * plane, v2);
+        } else {
+          p0[0] = v0; p0[plane] = v1; p0[2 * plane] = v2;
+        }
       }
     }
   }
@@ -293,7 +300,8 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     acc.store(y, row0, col0, g.m, g.k, g.k, lane, false);
-    if (bf.partial) acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
+    if (bf.partial)
+      acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane, bf.counters != nullptr);
   }
   fwd_bn_tail<TM, TN, WN>(g, bf, lds);
 }
@@ -362,7 +370,8 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_gather(ConvArgs g, co
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     acc.store(y, row0, col0, g.m, g.k, g.k, lane, false);
-    if (bf.partial) acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane);
+    if (bf.partial)
+      acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane, bf.counters != nullptr);
   }
   fwd_bn_tail<TM, TN, WN>(g, bf, lds);
 }
@@ -561,7 +570,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const f
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     float* out = g.splits > 1 ? dw + (long long)z * g.slab : dw;
-    acc.store(out, row0, col0, K, RSC, RSC, lane, false);
+    acc.store(out, row0, col0, K, RSC, RSC, lane, false, g.cnt != nullptr);
   }
   if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
 }
@@ -659,7 +668,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad_t(ConvArgs g, const
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
   if (wk == 0 && active) {
     float* out = g.splits > 1 ? dw + (long long)z * g.slab : dw;
-    acc.store(out, row0, col0, K, RSC, RSC, lane, false);
+    acc.store(out, row0, col0, K, RSC, RSC, lane, false, g.cnt != nullptr);
   }
   if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
 }
@@ -783,6 +792,16 @@ ConvArgs make_args(const tspm_conv_shape* s) {
 constexpr int kMaxFusedSplits = 16;   // wgrad: in-launch slab reduction up to this many slabs
 constexpr int kMaxFusedMergeIters = 16;  // fwd: in-launch BN merge when each thread reads <= this many tiles
 
+// TSPM_INLAUNCH=0 turns the in-launch hand-offs off (separate merge / reduction launches) — an A/B
+// switch for measurements; read once.
+bool inlaunch_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TSPM_INLAUNCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool is_hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
   if (!st) return true;
   return st->sc == 1 && st->sn == s->c && st->sw == (long long)s->n * s->c && st->sh == (long long)s->w * s->n * s->c;
@@ -848,7 +867,7 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   // otherwise the parallel tspm_bn_finalize pass follows
   const int tiles = (int)grid.x, groups = 2 * al.wk / al.tn;
   const tspm_bn_fuse want = bf;
-  if (bf.counters && cdiv(tiles, groups) > kMaxFusedMergeIters) bf.counters = nullptr;
+  if (bf.counters && (cdiv(tiles, groups) > kMaxFusedMergeIters || !inlaunch_enabled())) bf.counters = nullptr;
   size_t lds = lds_bytes(al);
   if (bf.counters) lds = std::max(lds, (size_t)16 + 8 * (size_t)(64 * al.wn * al.wk + 32 * al.wn * al.tn));
   const bool vec = is_hwnc(s, xs) && (s->c % 8 == 0);
@@ -911,7 +930,8 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
     if (!ws || ws_bytes < tspm_conv_wgrad_workspace(s, user)) return TSPM_ERR_WORKSPACE;
     out = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
     // in-launch reduction when the last arriver's serial read is short; else a separate pass
-    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned))
+    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned) &&
+        inlaunch_enabled())
       g.cnt = static_cast<unsigned*>(ws);
   }
   const size_t lds = std::max(lds_bytes(al), (size_t)16);
@@ -949,7 +969,8 @@ extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo*
   if (al.splits > 1) {
     if (!ws || ws_bytes < tspm_conv_wgrad_workspace(s, user)) return TSPM_ERR_WORKSPACE;
     out = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
-    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned))
+    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned) &&
+        inlaunch_enabled())
       g.cnt = static_cast<unsigned*>(ws);
   }
   const size_t lds = std::max(lds_bytes(al), (size_t)16);

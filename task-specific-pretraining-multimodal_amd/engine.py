@@ -184,7 +184,11 @@ class EncoderEngine:
         self.final_c = c
         # weight gradients from transposed operands (16-byte loads on both GEMM operands) whenever
         # an 8-row chunk shares one output position
-        self.use_t = N % 8 == 0
+        # Off by default: measured on MI355X at batch 128 (same box, interleaved runs) the transposed
+        # copies cost the BN/maxpool kernels more than tspm_conv_wgrad_t saves once the two encoder
+        # streams overlap (34.7k vs 36.1k samples/s), although each wgrad_t launch alone is faster.
+        # TSPM_WGRAD_T=1 turns it on.
+        self.use_t = N % 8 == 0 and os.environ.get("TSPM_WGRAD_T", "0") == "1"
         self.mp_t = None
         if self.use_t:
             self.mp_t = torch.empty(C0, self.mp.shape[0], **f32)
