@@ -1,6 +1,6 @@
 """Summarise one graph-replayed train step from a rocprofv3 kernel trace.
 
-    python scripts/trace_summary.py gpurun_out/prof/run_kernel_trace.csv [--step -3]
+    python scripts/trace_summary.py gpurun_out/prof/run_kernel_trace.csv|run_results.db [--step -3]
 
 A step is delimited by consecutive `k_adam<...>` launches (Adam ends every step).  Prints the step's
 wall time, summed kernel time, busy time (union of kernel intervals, i.e. with concurrency folded),
@@ -24,8 +24,13 @@ def main():
     ap.add_argument("--step", type=int, default=-3, help="which step (index into the list of Adam-delimited steps)")
     ap.add_argument("--top", type=int, default=25)
     args = ap.parse_args()
-    rows = list(csv.DictReader(open(args.trace)))
-    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows))
+    if args.trace.endswith(".db"):  # rocprofv3 rocpd SQLite output (the default format)
+        import sqlite3
+        con = sqlite3.connect(args.trace)
+        ks = sorted((int(s), int(e), n, str(q)) for s, e, n, q in con.execute("select start, end, name, queue_id from kernels"))
+    else:
+        rows = list(csv.DictReader(open(args.trace)))
+        ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows))
     adam = [i for i, k in enumerate(ks) if "k_adam<" in k[2] or "k_adam(" in k[2] or k[2].startswith("void k_adam")
             and "begin" not in k[2]]
     if len(adam) < 2:
