@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 5 */
+int tspm_abi_version(void);  /* 6 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -53,15 +53,23 @@ typedef struct tspm_conv_shape {
   int32_t p, q;        /* output height, width (= (h + 2 pad - r) / stride + 1, ...) */
 } tspm_conv_shape;
 
-/* Tile / split configuration.  tm, tn: 32x32 MFMA tiles per wave along M (rows) and N (columns);
- * a workgroup holds wn x wk waves: wn neighbouring column tiles of the same rows and wk waves that
- * split the reduction of one tile and combine through LDS in fixed order (deterministic, no
- * workspace).  splits: additional split of the wgrad reduction over workgroups (fp32 slabs, summed
- * in slab order).  Supported: (tm,tn) in {(1,1),(1,2),(2,2)}, wn in {1,2,4}, wk in {1,2,4,8,16},
- * wn*wk <= 8 when wn > 1, wk == 16 only with wn == 1, at most 160 KiB of LDS for the combine.
- * All-zero fields select the built-in heuristic. */
+/* Tile / split configuration.  tm, tn: 32x32 MFMA tiles per wave along M (rows) and N (columns).
+ * variant 0 — register-direct kernels (operands loaded straight into MFMA fragments): a workgroup
+ *   holds wn x wk waves: wn neighbouring column tiles of the same rows and wk waves that split the
+ *   reduction of one tile and combine through LDS in fixed order (deterministic, no workspace);
+ *   splits: additional split of the wgrad reduction over workgroups (fp32 slabs, summed in slab
+ *   order).  Supported: (tm,tn) in {(1,1),(1,2),(2,2)}, wn in {1,2,4}, wk in {1,2,4,8,16},
+ *   wn*wk <= 8 when wn > 1, wk == 16 only with wn == 1, at most 160 KiB of LDS for the combine.
+ *   All-zero fields select the built-in heuristic.
+ * variant 1 — LDS-staged kernels (operand stages fetched in full 128-B lines, double-buffered in
+ *   LDS): a workgroup is 4 waves = wm x wn x wk with wm = 4 / (wn*wk); tile (wm*tm*32) x (wn*tn*32);
+ *   wk waves split every 32-deep reduction stage; splits: split-K over workgroups for fwd, dgrad
+ *   and wgrad (fp32 slabs in the workspace, reduced in slab order in-launch).  tm, tn in {1,2}.
+ *   Needs HWNC operands, n % (wm*tm*32) == 0 (fwd/dgrad), c % 32 == 0 (fwd), k % 32 == 0 (dgrad),
+ *   n % 32 == 0 and c % (wn*tn*32) == 0 (wgrad); otherwise the call returns TSPM_ERR_INVALID. */
 typedef struct tspm_conv_algo {
   int32_t tm, tn, wn, wk, splits;
+  int32_t variant;
 } tspm_conv_algo;
 
 /* Element strides (n, h, w, c) of a conv input tensor.  HWNC tensors: {c, w*n*c, n*c, 1}.
@@ -88,17 +96,18 @@ typedef struct tspm_bn_fuse {
 } tspm_bn_fuse;
 
 /* y[P,Q,N,K] = conv(x, w).  y is HWNC.  bn: NULL, or the BatchNorm statistics to produce from the
- * epilogue (see tspm_bn_fuse) — the conv output is never re-read for them. */
+ * epilogue (see tspm_bn_fuse) — the conv output is never re-read for them.  Workspace
+ * (tspm_conv_fwd_workspace; nonzero only for variant-1 split-K): TSPM_COUNTER_BYTES of arrival
+ * counters, zero before first use and left zero, followed by the fp32 slabs. */
 int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
                   const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
-                  tspm_stream_t stream);
+                  void* workspace, size_t workspace_bytes, tspm_stream_t stream);
 int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
-/* Always 0 (kept for ABI symmetry: the forward needs no workspace). */
 size_t tspm_conv_fwd_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
-/* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}.  Needs no
- * workspace (the workspace arguments are accepted and ignored). */
+/* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}.  Workspace
+ * (tspm_conv_dgrad_workspace) only for variant-1 split-K, laid out as for the forward. */
 int tspm_conv_dgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy,
                     const float* w, float* dx, int32_t beta, void* workspace, size_t workspace_bytes,
                     tspm_stream_t stream);

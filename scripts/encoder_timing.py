@@ -69,6 +69,16 @@ def main():
     for name, fn in [("audio", audio), ("image", image), ("both_serial", both_serial), ("both_2streams", both_par)]:
         res[name] = timeit(fn)
         print(f"{name:14s} {res[name]:8.1f} us", flush=True)
+    # the same without a graph (eager launches from this thread)
+    for name, fn in [("eager_audio", audio), ("eager_image", image), ("eager_2streams", both_par)]:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        print(f"{name:14s} {(time.perf_counter() - t0) / 20 * 1e6:8.1f} us", flush=True)
     step.run(); step.run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

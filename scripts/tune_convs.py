@@ -3,8 +3,10 @@ workload and write the fastest per (kind, shape) as a table the engine loads at 
 
     python scripts/tune_convs.py --batch 128 --out task-specific-pretraining-multimodal_amd/tuned/mi355x.json
 
-Each candidate is checked against the default configuration's output (max |diff| <= 1e-5 x max |y|)
-before it may win; timings are HIP events around back-to-back launches on one stream.
+Candidates: the configuration currently in the table (or the heuristic) and every supported
+variant-1 (LDS-staged) configuration.  Each candidate is checked against the baseline's output
+(max |diff| <= 1e-5 x max |y|) before it may win; timings are HIP-graph replays of back-to-back
+launches on one stream (graph_time).
 """
 from __future__ import annotations
 
@@ -99,55 +101,110 @@ def launcher(kind, s, xs, b, algo):
                                            b.dy.data_ptr(), b.dw.data_ptr(), b.ws.data_ptr(), wsb, sh)
         return f, b.dw
     if kind == "dgrad":
+        need = lib.tspm_conv_dgrad_workspace(ctypes.byref(s), ctypes.byref(a))
+        if need > b.ws.numel():
+            b.ws = torch.zeros(need, dtype=torch.uint8, device=b.x.device)
+        wsb = b.ws.numel()
+
         def f():
             return lib.tspm_conv_dgrad(ctypes.byref(s), ctypes.byref(a), b.dy.data_ptr(), b.w.data_ptr(),
-                                       b.dx.data_ptr(), 0, None, 0, sh)
+                                       b.dx.data_ptr(), 0, b.ws.data_ptr(), wsb, sh)
         return f, b.dx
 
     bnf = L.BnFuse(b.part.data_ptr(), b.cnt.data_ptr(), None, None, 0.1, 1e-5, b.mean.data_ptr(), b.inv.data_ptr())
 
+    need = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a))
+    if need > b.ws.numel():
+        b.ws = torch.zeros(need, dtype=torch.uint8, device=b.x.device)
+    wsb = b.ws.numel()
+
     def f():  # the engine's launch: conv + BN statistics merged in-launch
         return lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), b.x.data_ptr(), ctypes.byref(xs), b.w.data_ptr(),
-                                 b.y.data_ptr(), ctypes.byref(bnf), sh)
+                                 b.y.data_ptr(), ctypes.byref(bnf), b.ws.data_ptr(), wsb, sh)
     return f, b.y
 
 
-def time_launch(f, reps):
-    for _ in range(2):
-        if f() != 0:
-            return None
+def graph_time(make, reps, iters=20):
+    """Per-launch time of `reps` back-to-back launches captured in one HIP graph and replayed
+    `iters` times (device time + the dependent-launch boundary; no host launch overhead).  make()
+    returns the launch closure; it is called inside the capture so the closure binds the capture
+    stream.  Returns None if the launch fails."""
+    if make()() != 0:
+        return None
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        f = make()
+        for _ in range(reps):
+            f()
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(reps):
-        f()
+    for _ in range(iters):
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1000.0 / reps
+    return e0.elapsed_time(e1) * 1000.0 / (iters * reps)
+
+
+LDS_TILES = [(1, 1), (1, 2), (2, 1), (2, 2)]
+LDS_WAVES = [(1, 1), (2, 1), (4, 1), (1, 2), (2, 2), (1, 4)]   # (wn, wk); wm = 4 / (wn * wk)
+LDS_SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32]
+
+
+def lds_candidates(kind, s):
+    """Supported variant-1 (LDS-staged) configurations of one launch, with split-K only while the
+    grid stays under ~2048 workgroups."""
+    for (tm, tn), (wn, wk) in itertools.product(LDS_TILES, LDS_WAVES):
+        wm = 4 // (wn * wk)
+        bm, bn = wm * tm * 32, wn * tn * 32
+        if kind == "fwd":
+            if s.c % 32 or s.n % bm:
+                continue
+            wgs = (s.p * s.q * s.n // bm) * -(-s.k // bn)
+        elif kind == "dgrad":
+            if s.k % 32 or s.n % bm:
+                continue
+            wgs = (s.h * s.w * s.n // bm) * -(-s.c // bn)
+        else:
+            if s.n % 32 or s.c % bn:
+                continue
+            wgs = -(-s.k // bm) * (s.r * s.s * s.c // bn)
+        for sp in LDS_SPLITS:
+            if sp > 1 and wgs * sp > 2048:
+                break
+            yield (tm, tn, wn, wk, sp, 1)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only-kind", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    ops = distinct_ops(args.batch, dev)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from conv_bench import step_ops
     table = []
     t0 = time.time()
-    tot_def, tot_best = 0.0, 0.0
-    for key, (s, xs, stem) in sorted(ops.items(), key=lambda kv: str(kv[0])):
+    tot_base, tot_best = 0.0, 0.0
+    for key, (s, xs, stem, count, base) in sorted(step_ops(args.batch, dev).items(), key=lambda kv: str(kv[0])):
         kind = key[0]
+        if args.only_kind and kind != args.only_kind:
+            continue
         b = Bufs(s, stem, dev)
-        f, out = launcher(kind, s, xs, b, (0, 0, 0, 0, 0))
-        t_def = time_launch(f, args.reps)
+        t_base = graph_time(lambda: launcher(kind, s, xs, b, base)[0], args.reps, args.iters)
+        _, out = launcher(kind, s, xs, b, base)
         ref = out.clone()
         scale = float(ref.abs().max()) + 1e-30
-        best = ((0, 0, 0, 0, 0), t_def)
+        best = (tuple(base), t_base)
         n_ok = 0
-        for algo in candidates(kind):
+        cands = [] if stem else list(lds_candidates(kind, s))
+        for algo in cands:
             f, out = launcher(kind, s, xs, b, algo)
             out.fill_(float("nan"))
             if f() != 0:
@@ -157,24 +214,23 @@ def main():
             if not err <= 1e-5 * scale:
                 print(f"  MISMATCH {kind} {tuple(key[1:])} {algo} err={err:.3e} scale={scale:.3e}", flush=True)
                 continue
-            t = time_launch(f, args.reps)
+            t = graph_time(lambda: launcher(kind, s, xs, b, algo)[0], args.reps, args.iters)
             if t is None:
                 continue
             n_ok += 1
             if t < best[1]:
                 best = (algo, t)
-        # confirm the winner with a longer run
-        f, _ = launcher(kind, s, xs, b, best[0])
-        t_best = time_launch(f, 3 * args.reps)
-        tot_def += t_def
-        tot_best += t_best
+        t_best = graph_time(lambda: launcher(kind, s, xs, b, best[0])[0], args.reps, 4 * args.iters)
+        tot_base += t_base * count
+        tot_best += t_best * count
         table.append({"kind": kind, "shape": list(key[1:]), "algo": list(best[0]), "us": round(t_best, 2),
-                      "default_us": round(t_def, 2), "candidates": n_ok})
-        print(f"{kind:5s} {str(tuple(key[1:])):42s} default {t_def:7.1f} us  best {t_best:7.1f} us  {best[0]}  "
-              f"({n_ok} ok, {time.time() - t0:.0f}s)", flush=True)
+                      "base_us": round(t_base, 2), "base_algo": list(base), "count": count, "candidates": n_ok})
+        print(f"{kind:5s} {str(tuple(key[1:])):42s} x{count:2d} base {t_base:7.2f} us  best {t_best:7.2f} us  "
+              f"{best[0]}  ({n_ok} ok, {time.time() - t0:.0f}s)", flush=True)
         del b
-    print(f"sum over distinct launches: default {tot_def:.0f} us, tuned {tot_best:.0f} us", flush=True)
-    doc = {"device": torch.cuda.get_device_name(0), "batch": args.batch, "entries": table}
+    print(f"per-step sum over launches: base {tot_base:.0f} us, tuned {tot_best:.0f} us", flush=True)
+    doc = {"device": torch.cuda.get_device_name(0), "batch": args.batch, "timing": "hip-graph replay",
+           "entries": table}
     if args.out:
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
         with open(args.out, "w") as fh:

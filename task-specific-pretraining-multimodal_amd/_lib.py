@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -34,7 +34,8 @@ class ConvShape(Structure):
 
 
 class ConvAlgo(Structure):
-    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits")]
+    """tspm_conv_algo: (tm, tn, wn, wk, splits[, variant]); variant 1 = LDS-staged kernels."""
+    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits", "variant")]
 
 
 class Strides4(Structure):
@@ -62,7 +63,7 @@ _SIGS = {
     "tspm_abi_version": (c_int32, []),
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
     "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, POINTER(BnFuse),
-                                _P]),
+                                _P, c_size_t, _P]),
     "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),

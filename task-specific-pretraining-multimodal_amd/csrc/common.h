@@ -40,6 +40,38 @@ TSPM_DEV int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Diagnostic build only (-DTSPM_STAMPS, `make stamps` → libtspm_stamps.so): lane 0 of every wave
+// records s_memrealtime (100 MHz, chip-global) at numbered points of a kernel into a per-TU device
+// buffer read back by tspm_debug_stamps().  The product build compiles these to nothing.
+#ifdef TSPM_STAMPS
+#define TSPM_STAMP_SLOTS 8
+#define TSPM_STAMP_WAVES (1 << 18)
+#define TSPM_STAMP(buf, slot)                                                                             \
+  do {                                                                                                    \
+    const unsigned long long t__ = __builtin_amdgcn_s_memrealtime();                                     \
+    const unsigned long long w__ = ((unsigned long long)blockIdx.x +                                     \
+                                    (unsigned long long)gridDim.x * (blockIdx.y + (unsigned long long)gridDim.y * blockIdx.z)) * \
+                                       (blockDim.x >> 6) + (threadIdx.x >> 6);                           \
+    if ((threadIdx.x & 63) == 0 && w__ < TSPM_STAMP_WAVES) buf[w__ * TSPM_STAMP_SLOTS + (slot)] = t__;  \
+  } while (0)
+// slot 6 / 7: s_memtime (shader clock) at entry / exit, for the in-kernel clock
+#define TSPM_STAMP_CLK(buf, slot)                                                                         \
+  do {                                                                                                    \
+    const unsigned long long t__ = __builtin_amdgcn_s_memtime();                                         \
+    const unsigned long long w__ = ((unsigned long long)blockIdx.x +                                     \
+                                    (unsigned long long)gridDim.x * (blockIdx.y + (unsigned long long)gridDim.y * blockIdx.z)) * \
+                                       (blockDim.x >> 6) + (threadIdx.x >> 6);                           \
+    if ((threadIdx.x & 63) == 0 && w__ < TSPM_STAMP_WAVES) buf[w__ * TSPM_STAMP_SLOTS + (slot)] = t__;  \
+  } while (0)
+#else
+#define TSPM_STAMP_CLK(buf, slot) \
+  do {                            \
+  } while (0)
+#define TSPM_STAMP(buf, slot) \
+  do {                        \
+  } while (0)
+#endif
+
 #define TSPM_LAUNCH_CHECK()                               \
   do {                                                    \
     hipError_t e__ = hipGetLastError();                   \

@@ -22,171 +22,22 @@
 // The forward epilogue can also emit BatchNorm partial statistics of its output tile (per column:
 // shift K = the tile's first row, mean offset and corrected sum of squared deviations), so the BN
 // statistics never re-read the conv output (tspm_bn_finalize merges them).
-#include "common.h"
+#include "conv_common.h"
+
+#ifdef TSPM_STAMPS
+__device__ unsigned long long tspm_g_stamps[TSPM_STAMP_WAVES * TSPM_STAMP_SLOTS];
+extern "C" int tspm_debug_stamps(void* host_dst, size_t bytes) {
+  if (bytes > sizeof(tspm_g_stamps)) bytes = sizeof(tspm_g_stamps);
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(tspm_g_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+extern "C" int tspm_debug_stamps_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(tspm_g_stamps)) != hipSuccess) return 2;
+  return hipMemset(p, 0, sizeof(tspm_g_stamps)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 namespace {
-
-struct ConvArgs {
-  int n, h, w, c, k, r, s, st, pad, p, q;
-  long long sn, sh, sw, sc;  // input strides (fwd / wgrad)
-  int m;                     // GEMM rows: fwd P*Q*N, dgrad H*W*N, wgrad K
-  int splits;                // wgrad global split
-  long long slab;            // elements per split slab
-  int beta;                  // dgrad accumulate
-  unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
-};
-
-template <int TM, int TN>
-struct Acc {
-  f32x16 v[TM][TN];
-  TSPM_DEV void zero() {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[a][b][i] = 0.f;
-  }
-  TSPM_DEV void mma4(const f32x4 (&A)[TM], const f32x4 (&B)[TN]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) v[a][b] = mfma32(A[a][j], B[b][j], v[a][b]);
-  }
-  // store rows row0 + a*32 + acc_row, cols col0 + b*32 + (lane&31) of a [rows, ld] matrix
-  // (sc1: write-through, the payload of an in-launch hand-off)
-  TSPM_DEV void store(float* out, int row0, int col0, int rows, int cols, long long ld, int lane, bool accumulate,
-                      bool sc1 = false) const {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = col0 + b * 32 + (lane & 31);
-        if (col >= cols) continue;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = row0 + a * 32 + acc_row(i, lane);
-          if (row < rows) {
-            float* p = out + (long long)row * ld + col;
-            if (sc1) st_sc1(p, v[a][b][i]);
-            else *p = accumulate ? (*p + v[a][b][i]) : v[a][b][i];
-          }
-        }
-      }
-  }
-  // split-K combine of the WK waves of one tile through LDS (wave wk > 0 writes, wave 0 sums in
-  // order).  Every wave of the workgroup must call this (it contains barriers).
-  template <int WN, int WK>
-  TSPM_DEV void combine(float* lds, int wn, int wk, int lane, bool active) {
-    if constexpr (WK > 1) {
-      constexpr int TILE = TM * TN * 16 * 64;
-      if (wk > 0 && active) {
-        float* dst = lds + ((wk - 1) * WN + wn) * TILE;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) dst[((a * TN + b) * 16 + i) * 64 + lane] = v[a][b][i];
-      }
-      __syncthreads();
-      if (wk == 0 && active) {
-        for (int k = 1; k < WK; ++k) {
-          const float* src = lds + ((k - 1) * WN + wn) * TILE;
-#pragma unroll
-          for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) v[a][b][i] += src[((a * TN + b) * 16 + i) * 64 + lane];
-        }
-      }
-    }
-  }
-  // BatchNorm partial statistics of this tile's valid rows, per column (channel):
-  //   part[0][mt][col] = K (the tile's first row), part[1][..] = mean - K, part[2][..] = M2
-  TSPM_DEV void bn_partials(float* part, long long plane, int mt, int row0, int col0, int rows, int cols,
-                            int lane, bool sc1) const {
-    const int cnt = min(TM * 32, rows - row0);
-    const float inv = 1.0f / (float)cnt;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int col = col0 + b * 32 + (lane & 31);
-      const float K = __shfl(v[0][b][0], lane & 31, 64);  // row 0 of the tile lives in lane (col, half 0), reg 0
-      float s = 0.f;
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (row0 + a * 32 + acc_row(i, lane) < rows) s += v[a][b][i] - K;
-      s += __shfl_xor(s, 32, 64);
-      const float off = s * inv;
-      float sd = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (row0 + a * 32 + acc_row(i, lane) < rows) {
-            const float d = (v[a][b][i] - K) - off;
-            sd += d;
-            s2 += d * d;
-          }
-      sd += __shfl_xor(sd, 32, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 32 && col < cols) {
-        const double n = (double)cnt;
-        const float v0 = K, v1 = (float)((double)off + (double)sd / n), v2 = (float)((double)s2 - (double)sd * (double)sd / n);
-        float* p0 = part + (long long)mt * cols + col;
-        if (sc1) {
-          st_sc1(p0, v0); st_sc1(p0 + plane, v1); st_sc1(p0 + 2 * plane, v2);
-        } else {
-          p0[0] = v0; p0[plane] = v1; p0[2 * plane] = v2;
-        }
-      }
-    }
-  }
-};
-
-TSPM_DEV int split_lo(int T, int z, int S) { return (int)(((long long)T * z) / S); }
-
-// wgrad tail with split-K over workgroups: the last of the `splits` workgroups of this tile sums
-// the slabs in slab order (bitwise equal to tspm_reduce_slabs) and writes dw.
-template <int TM, int TN, int WN>
-TSPM_DEV void slab_tail(const ConvArgs& g, const float* slabs, float* dw_final, int RSC, float* lds) {
-  if (!last_arriver(g.cnt + (blockIdx.y * gridDim.x + blockIdx.x), g.splits, reinterpret_cast<int*>(lds))) return;
-  const int r0 = blockIdx.x * (TM * 32), rn = min(TM * 32, g.k - r0);
-  const int cb0 = blockIdx.y * (WN * TN * 32), cn = min(WN * TN * 32, RSC - cb0);
-  for (int e = threadIdx.x; e < rn * cn; e += blockDim.x) {
-    const int rr = e / cn, cc = e - rr * cn;
-    const long long off = (long long)(r0 + rr) * RSC + cb0 + cc;
-    float sum = 0.f;
-    int zz = 0;
-    for (; zz + 8 <= g.splits; zz += 8) {  // 8 independent loads in flight, summed in slab order
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = slabs[(zz + u) * g.slab + off];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; zz < g.splits; ++zz) sum += slabs[zz * g.slab + off];
-    dw_final[off] = sum;
-  }
-}
-
-// Forward tail with in-launch BatchNorm: the last workgroup of each column block (all row tiles
-// of its WN*TN*32 channels have written their partials) merges them (no finalize launch).
-template <int TM, int TN, int WN>
-TSPM_DEV void fwd_bn_tail(const ConvArgs& g, const tspm_bn_fuse& bf, float* lds) {
-  if (!bf.counters) return;
-  if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(lds))) return;
-  constexpr int CB = WN * TN * 32;
-  double* red = reinterpret_cast<double*>(lds) + 2;
-  double* smu = red + blockDim.x;
-  bn_merge_block(g.m, g.k, gridDim.x, TM * 32, bf.partial, blockIdx.y * CB, CB, bf.running_mean, bf.running_var,
-                 bf.momentum, bf.eps, bf.save_mean, bf.save_invstd, red, smu);
-}
 
 // =============================================================================================
 // Forward, vector path: HWNC input, C % 8 == 0.
@@ -196,6 +47,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
                                                               const float* __restrict__ w, float* __restrict__ y,
                                                               tspm_bn_fuse bf) {
   extern __shared__ float lds[];
+  TSPM_STAMP(tspm_g_stamps, 0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave % WN, wk = wave / WN;
@@ -234,45 +86,21 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
       const int nr = r_hi - r_lo + 1, ns = s_hi - s_lo + 1;
       const int T = (nr > 0 && ns > 0) ? nr * ns * cch : 0;
       const int it0 = split_lo(T, wk, WK), it1 = split_lo(T, wk + 1, WK);
-      if (it0 < it1) {
-        int tap = it0 / cch, ci = (it0 - tap * cch) * 8;
-        int r = r_lo + tap / ns, s = s_lo + tap % ns;
-        const float* xa[TM];
+      const float* xa[TM];
 #pragma unroll
-        for (int a = 0; a < TM; ++a) xa[a] = x + (long long)nb[a] * C + 4 * hh;
-        auto a_off = [&](int rr, int ss, int cc) -> long long {
-          return ((long long)(h0 + rr) * g.w + (w0 + ss)) * N * C + cc;
-        };
-        auto b_off = [&](int rr, int ss, int cc) -> int { return (rr * g.s + ss) * C + cc; };
-        f32x4 A[TM], B[TN];
-        {
-          long long ao = a_off(r, s, ci);
-          int bo = b_off(r, s, ci);
+      for (int a = 0; a < TM; ++a) xa[a] = x + (long long)nb[a] * C + 4 * hh;
+      // iteration it = (valid tap, 8-channel chunk), taps row-major over the valid window
+      run_pipelined<TM, TN, prefetch_depth<TM, TN>()>(acc, it0, it1, [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
+        const int tap = it / cch, ci = (it - tap * cch) * 8;
+        const int tr = tap / ns;
+        const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
+        const long long ao = ((long long)(h0 + r) * g.w + (w0 + s)) * N * C + ci;
+        const int bo = (r * g.s + s) * C + ci;
 #pragma unroll
-          for (int a = 0; a < TM; ++a) A[a] = ld4(xa[a] + ao);
+        for (int a = 0; a < TM; ++a) A[a] = ld4(xa[a] + ao);
 #pragma unroll
-          for (int b = 0; b < TN; ++b) B[b] = ld4(wrow[b] + bo);
-        }
-        for (int it = it0; it < it1; ++it) {
-          int ci2 = ci + 8, s2 = s, r2 = r;
-          if (ci2 == C) { ci2 = 0; ++s2; if (s2 > s_hi) { s2 = s_lo; ++r2; } }
-          const bool more = it + 1 < it1;
-          const int rl = more ? r2 : r, sl = more ? s2 : s, cl = more ? ci2 : ci;
-          f32x4 An[TM], Bn[TN];
-          long long ao = a_off(rl, sl, cl);
-          int bo = b_off(rl, sl, cl);
-#pragma unroll
-          for (int a = 0; a < TM; ++a) An[a] = ld4(xa[a] + ao);
-#pragma unroll
-          for (int b = 0; b < TN; ++b) Bn[b] = ld4(wrow[b] + bo);
-          acc.mma4(A, B);
-#pragma unroll
-          for (int a = 0; a < TM; ++a) A[a] = An[a];
-#pragma unroll
-          for (int b = 0; b < TN; ++b) B[b] = Bn[b];
-          ci = ci2; s = s2; r = r2;
-        }
-      }
+        for (int b = 0; b < TN; ++b) B[b] = ld4(wrow[b] + bo);
+      });
     } else {
       // ---- mixed positions: all taps, per-lane padding masks ----
       const int T = g.r * g.s * cch;
@@ -297,13 +125,17 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_vec(ConvArgs g, const
       }
     }
   }
+  TSPM_STAMP(tspm_g_stamps, 1);
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
+  TSPM_STAMP(tspm_g_stamps, 2);
   if (wk == 0 && active) {
     acc.store(y, row0, col0, g.m, g.k, g.k, lane, false);
     if (bf.partial)
       acc.bn_partials(bf.partial, (long long)gridDim.x * g.k, blockIdx.x, row0, col0, g.m, g.k, lane, bf.counters != nullptr);
   }
+  TSPM_STAMP(tspm_g_stamps, 3);
   fwd_bn_tail<TM, TN, WN>(g, bf, lds);
+  TSPM_STAMP(tspm_g_stamps, 4);
 }
 
 // =============================================================================================
@@ -384,6 +216,7 @@ template <int TM, int TN, int WN, int WK, bool F_>
 __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const float* __restrict__ dy,
                                                             const float* __restrict__ w, float* __restrict__ dx) {
   extern __shared__ float lds[];
+  TSPM_STAMP(tspm_g_stamps, 0);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave % WN, wk = wave / WN;
@@ -433,7 +266,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const f
       const float* dya[TM];
 #pragma unroll
       for (int a = 0; a < TM; ++a) dya[a] = dy + (long long)nb[a] * K + 4 * hh;
-      for (int it = it0; it < it1; ++it) {
+      run_pipelined<TM, TN, prefetch_depth<TM, TN>()>(acc, it0, it1, [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
         const int t = it / kch, c0 = (it - t * kch) * 8;
         const int ri = t / ns, si = t - ri * ns;
         unsigned rm = rmask, sm = smask;
@@ -442,7 +275,6 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const f
         const int r = __builtin_ctz(rm), s = __builtin_ctz(sm);
         const int pp = (hi + g.pad - r) / g.st, qq = (wi + g.pad - s) / g.st;
         const long long aoff = ((long long)pp * g.q + qq) * N * K + c0;
-        f32x4 A[TM], B[TN];
 #pragma unroll
         for (int a = 0; a < TM; ++a) A[a] = ld4(dya[a] + aoff);
         const long long wbase = (long long)(c0 + 4 * hh) * RSC + (r * g.s + s) * C;
@@ -450,8 +282,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const f
         for (int b = 0; b < TN; ++b)
 #pragma unroll
           for (int j = 0; j < 4; ++j) B[b][j] = w[wbase + (long long)j * RSC + ci[b]];
-        acc.mma4(A, B);
-      }
+      });
     } else {
       const int T = g.r * g.s * kch;
       const int it0 = split_lo(T, wk, WK), it1 = split_lo(T, wk + 1, WK);
@@ -476,8 +307,11 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_dgrad(ConvArgs g, const f
       }
     }
   }
+  TSPM_STAMP(tspm_g_stamps, 1);
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
+  TSPM_STAMP(tspm_g_stamps, 2);
   if (wk == 0 && active) acc.store(dx, row0, col0, g.m, C, C, lane, g.beta != 0);
+  TSPM_STAMP(tspm_g_stamps, 3);
 }
 
 // =============================================================================================
@@ -523,8 +357,38 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const f
     }
     const int tap_first = col0 / C, tap_last = (min(col0 + TN * 32, RSC) - 1) / C;
     const bool one_tap = tap_first == tap_last;
-    const int T = cdiv_dev(Mout, 8);
     const int S = g.splits * WK, zz = z * WK + wk;
+    if (FAST && one_tap) {
+      // The tile's columns share one tap (r, s): only output positions whose input tap lies inside
+      // the image contribute — a rectangle [pp_lo, pp_hi] x [qq_lo, qq_hi].  Enumerate its 8-row
+      // chunks (rows (pp*Q + qq)*N + n, n in chunk), split evenly over the S reducers.
+      const int r = tap_first / g.s, s = tap_first - r * g.s;
+      const int pp_lo = max(0, cdiv_dev(g.pad - r, g.st)), pp_hi = min(g.p - 1, (g.h - 1 + g.pad - r) / g.st);
+      const int qq_lo = max(0, cdiv_dev(g.pad - s, g.st)), qq_hi = min(g.q - 1, (g.w - 1 + g.pad - s) / g.st);
+      const int npp = max(0, pp_hi - pp_lo + 1), nqq = max(0, qq_hi - qq_lo + 1), n8 = N >> 3;
+      const int T = npp * nqq * n8;
+      const int it0 = split_lo(T, zz, S), it1 = split_lo(T, zz + 1, S);
+      long long xoff[TN];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) xoff[b] = (long long)kc[b] * g.sc;
+      run_pipelined<TM, TN, prefetch_depth<TM, TN>()>(acc, it0, it1, [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
+        const int pc = it / n8, nch = it - pc * n8;
+        const int ip = pc / nqq, iq = pc - ip * nqq;
+        const int pp = pp_lo + ip, qq = qq_lo + iq;
+        const int n0 = nch * 8 + hh;
+        const long long mrow = ((long long)pp * g.q + qq) * N + n0;
+        const long long xb = (long long)n0 * g.sn + (long long)(pp * g.st - g.pad + r) * g.sh +
+                             (long long)(qq * g.st - g.pad + s) * g.sw;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int a = 0; a < TM; ++a) A[a][j] = dy[(mrow + 2 * j) * K + co[a]];
+#pragma unroll
+          for (int b = 0; b < TN; ++b) B[b][j] = x[xb + 2 * j * g.sn + xoff[b]];
+        }
+      });
+    } else {
+    const int T = cdiv_dev(Mout, 8);
     const int it0 = split_lo(T, zz, S), it1 = split_lo(T, zz + 1, S);
     for (int it = it0; it < it1; ++it) {
       const int mbase = it * 8;
@@ -565,6 +429,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const f
         }
       }
       acc.mma4(A, B);
+    }
     }
   }
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
@@ -827,37 +692,52 @@ Algo wgrad_algo(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   return pick(user, s->k, cols, iters, true);
 }
 
+// variant 1 (LDS-staged, conv_lds.hip): wm = 4 / (wn * wk)
+bool is_lds(const tspm_conv_algo* user) { return user && user->variant == 1; }
+tspm_detail::LdsAlgo lds_algo(const tspm_conv_algo* u) {
+  tspm_detail::LdsAlgo a{u->tm, u->tn, 0, u->wn, u->wk, u->splits > 0 ? u->splits : 1};
+  const int wnk = a.wn * a.wk;
+  a.wm = (wnk > 0 && 4 % wnk == 0) ? 4 / wnk : 0;
+  return a;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
 extern "C" size_t tspm_conv_fwd_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
-  (void)s; (void)user;
-  return 0;  // in-workgroup split-K: no workspace
+  if (!shape_ok(s) || !is_lds(user)) return 0;  // register-direct: in-workgroup split-K only
+  return tspm_detail::lds_fwd_workspace(s, lds_algo(user));
 }
 
 extern "C" int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
-  Algo al = fwd_algo(s, user);
-  return cdiv(s->p * s->q * s->n, al.tm * 32);
+  const int rows = is_lds(user) ? user->tm * 32 : fwd_algo(s, user).tm * 32;
+  return rows > 0 ? cdiv(s->p * s->q * s->n, rows) : 0;
 }
 
 extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
-  return fwd_algo(s, user).tm * 32;
+  return is_lds(user) ? user->tm * 32 : fwd_algo(s, user).tm * 32;
 }
 
 extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
-                             const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn,
-                             tspm_stream_t stream) {
+                             const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn, void* ws,
+                             size_t ws_bytes, tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !w || !y) return TSPM_ERR_INVALID;
-  Algo al = fwd_algo(s, user);
-  if (!algo_supported(al)) return TSPM_ERR_INVALID;
   tspm_bn_fuse bf{};
   if (bn) {
     bf = *bn;
     if (!bf.partial && bf.counters) return TSPM_ERR_INVALID;
     if (bf.counters && (!bf.save_mean || !bf.save_invstd)) return TSPM_ERR_INVALID;
   }
+  if (is_lds(user)) {
+    const tspm_detail::LdsAlgo la = lds_algo(user);
+    if (!tspm_detail::lds_fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
+    return tspm_detail::lds_fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  }
+  (void)ws; (void)ws_bytes;
+  Algo al = fwd_algo(s, user);
+  if (!algo_supported(al)) return TSPM_ERR_INVALID;
   ConvArgs g = make_args(s);
   if (xs) { g.sn = xs->sn; g.sh = xs->sh; g.sw = xs->sw; g.sc = xs->sc; }
   g.m = s->p * s->q * s->n;
@@ -881,15 +761,20 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
 }
 
 extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
-  (void)s; (void)user;
-  return 0;
+  if (!shape_ok(s) || !is_lds(user)) return 0;
+  return tspm_detail::lds_dgrad_workspace(s, lds_algo(user));
 }
 
 extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* dy,
                                const float* w, float* dx, int32_t beta, void* ws, size_t ws_bytes,
                                tspm_stream_t stream) {
-  (void)ws; (void)ws_bytes;
   if (!shape_ok(s) || !dy || !w || !dx) return TSPM_ERR_INVALID;
+  if (is_lds(user)) {
+    const tspm_detail::LdsAlgo la = lds_algo(user);
+    if (!tspm_detail::lds_dgrad_supported(s, la)) return TSPM_ERR_INVALID;
+    return tspm_detail::lds_dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  }
+  (void)ws; (void)ws_bytes;
   if (s->k % 8 != 0) return TSPM_ERR_INVALID;
   Algo al = dgrad_algo(s, user);
   if (!algo_supported(al)) return TSPM_ERR_INVALID;
@@ -906,6 +791,7 @@ extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
 
 extern "C" size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
+  if (is_lds(user)) return tspm_detail::lds_wgrad_workspace(s, lds_algo(user));
   Algo al = wgrad_algo(s, user);
   if (al.splits <= 1) return 0;
   return TSPM_COUNTER_BYTES + (size_t)al.splits * s->k * s->r * s->s * s->c * sizeof(float);
@@ -915,6 +801,11 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
                                const tspm_strides4* xs, const float* dy, float* dw, void* ws, size_t ws_bytes,
                                tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !dy || !dw) return TSPM_ERR_INVALID;
+  if (is_lds(user)) {
+    const tspm_detail::LdsAlgo la = lds_algo(user);
+    if (!tspm_detail::lds_wgrad_supported(s, xs, la)) return TSPM_ERR_INVALID;
+    return tspm_detail::lds_wgrad(s, la, x, dy, dw, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  }
   Algo al = wgrad_algo(s, user);
   if (!algo_supported(al)) return TSPM_ERR_INVALID;
   ConvArgs g = make_args(s);

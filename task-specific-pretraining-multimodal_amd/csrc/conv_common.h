@@ -1,0 +1,235 @@
+// Device helpers shared by the register-direct (conv.hip) and LDS-staged (conv_lds.hip)
+// implicit-GEMM convolution kernels: argument block, MFMA accumulator tile with its epilogues
+// (stores, split-K combine, BatchNorm partial statistics), split-K slab reduction and the in-launch
+// BatchNorm merge.  Replaces nn.Conv2d of MML_Suite/models/msa/networks/resnet.py:25,30,137,176.
+#pragma once
+#include "common.h"
+
+namespace {
+
+struct ConvArgs {
+  int n, h, w, c, k, r, s, st, pad, p, q;
+  long long sn, sh, sw, sc;  // input strides (fwd / wgrad)
+  int m;                     // GEMM rows: fwd P*Q*N, dgrad H*W*N, wgrad K
+  int splits;                // wgrad global split
+  long long slab;            // elements per split slab
+  int beta;                  // dgrad accumulate
+  unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
+};
+
+template <int TM, int TN>
+struct Acc {
+  f32x16 v[TM][TN];
+  TSPM_DEV void zero() {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[a][b][i] = 0.f;
+  }
+  TSPM_DEV void mma4(const f32x4 (&A)[TM], const f32x4 (&B)[TN]) {
+#ifdef TSPM_EXP_NOMFMA  // diagnostic ablation (stamped build only): consume operands without MFMA
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) v[a][b][0] += A[a][0] * B[b][0] + A[a][3] * B[b][3];
+#else
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) v[a][b] = mfma32(A[a][j], B[b][j], v[a][b]);
+#endif
+  }
+  // store rows row0 + a*32 + acc_row, cols col0 + b*32 + (lane&31) of a [rows, ld] matrix
+  // (sc1: write-through, the payload of an in-launch hand-off)
+  TSPM_DEV void store(float* out, int row0, int col0, int rows, int cols, long long ld, int lane, bool accumulate,
+                      bool sc1 = false) const {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = col0 + b * 32 + (lane & 31);
+        if (col >= cols) continue;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = row0 + a * 32 + acc_row(i, lane);
+          if (row < rows) {
+            float* p = out + (long long)row * ld + col;
+            if (sc1) st_sc1(p, v[a][b][i]);
+            else *p = accumulate ? (*p + v[a][b][i]) : v[a][b][i];
+          }
+        }
+      }
+  }
+  // split-K combine of the WK waves of one tile through LDS (wave wk > 0 writes, wave 0 sums in
+  // order).  Every wave of the workgroup must call this (it contains barriers).
+  template <int WN, int WK>
+  TSPM_DEV void combine(float* lds, int wn, int wk, int lane, bool active) {
+    if constexpr (WK > 1) {
+      constexpr int TILE = TM * TN * 16 * 64;
+      if (wk > 0 && active) {
+        float* dst = lds + ((wk - 1) * WN + wn) * TILE;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dst[((a * TN + b) * 16 + i) * 64 + lane] = v[a][b][i];
+      }
+      __syncthreads();
+      if (wk == 0 && active) {
+        for (int k = 1; k < WK; ++k) {
+          const float* src = lds + ((k - 1) * WN + wn) * TILE;
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) v[a][b][i] += src[((a * TN + b) * 16 + i) * 64 + lane];
+        }
+      }
+    }
+  }
+  // BatchNorm partial statistics of this tile's valid rows, per column (channel):
+  //   part[0][mt][col] = K (the tile's first row), part[1][..] = mean - K, part[2][..] = M2
+  TSPM_DEV void bn_partials(float* part, long long plane, int mt, int row0, int col0, int rows, int cols,
+                            int lane, bool sc1) const {
+    const int cnt = min(TM * 32, rows - row0);
+    const float inv = 1.0f / (float)cnt;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = col0 + b * 32 + (lane & 31);
+      const float K = __shfl(v[0][b][0], lane & 31, 64);  // row 0 of the tile lives in lane (col, half 0), reg 0
+      float s = 0.f;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (row0 + a * 32 + acc_row(i, lane) < rows) s += v[a][b][i] - K;
+      s += __shfl_xor(s, 32, 64);
+      const float off = s * inv;
+      float sd = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (row0 + a * 32 + acc_row(i, lane) < rows) {
+            const float d = (v[a][b][i] - K) - off;
+            sd += d;
+            s2 += d * d;
+          }
+      sd += __shfl_xor(sd, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 32 && col < cols) {
+        const double n = (double)cnt;
+        const float v0 = K, v1 = (float)((double)off + (double)sd / n), v2 = (float)((double)s2 - (double)sd * (double)sd / n);
+        float* p0 = part + (long long)mt * cols + col;
+        if (sc1) {
+          st_sc1(p0, v0); st_sc1(p0 + plane, v1); st_sc1(p0 + 2 * plane, v2);
+        } else {
+          p0[0] = v0; p0[plane] = v1; p0[2 * plane] = v2;
+        }
+      }
+    }
+  }
+};
+
+TSPM_DEV int split_lo(int T, int z, int S) { return (int)(((long long)T * z) / S); }
+
+// Register prefetch depth of the main loops: loads of PF reduction iterations are in flight while
+// one is multiplied, so a wave pays one memory round trip per PF iterations instead of one per
+// iteration (at batch 128 most layers give a wave 4-20 iterations: with a one-deep prefetch the
+// loop was a chain of dependent L2/HBM round trips, 2-5x the MFMA time).
+template <int TM, int TN>
+constexpr int prefetch_depth() {
+  return TM * TN == 1 ? 8 : (TM * TN == 2 ? 4 : 3);
+}
+
+// Runs iterations [it0, it1) through a PF-slot register ring: slot d holds iteration
+// base + d; right after slot d is multiplied it is refilled with iteration base + PF + d.  The main
+// loop has no data-dependent branches around its loads (past the end a slot reloads iteration
+// it1-1, which is never multiplied), so the compiler's counted vmcnt waits keep PF-1 loads in
+// flight.  load(it, A, B) fills the operands of reduction iteration it.
+template <int TM, int TN, int PF, class LoadFn>
+TSPM_DEV void run_pipelined(Acc<TM, TN>& acc, int it0, int it1, LoadFn&& load) {
+  const int n = it1 - it0;
+  if (n <= 0) return;
+  f32x4 A[PF][TM], B[PF][TN];
+#pragma unroll
+  for (int d = 0; d < PF; ++d) load(min(it0 + d, it1 - 1), A[d], B[d]);
+  const int nfull = n / PF;
+  for (int bt = 0; bt < nfull; ++bt) {
+    const int nb = it0 + (bt + 1) * PF;
+#pragma unroll
+    for (int d = 0; d < PF; ++d) {
+      acc.mma4(A[d], B[d]);
+      load(min(nb + d, it1 - 1), A[d], B[d]);
+    }
+  }
+  const int rem = n - nfull * PF;
+#pragma unroll
+  for (int d = 0; d < PF; ++d)
+    if (d < rem) acc.mma4(A[d], B[d]);
+}
+
+// wgrad tail with split-K over workgroups: the last of the `splits` workgroups of this tile sums
+// the slabs in slab order (bitwise equal to tspm_reduce_slabs) and writes dw.
+template <int TM, int TN, int WN>
+TSPM_DEV void slab_tail(const ConvArgs& g, const float* slabs, float* dw_final, int RSC, float* lds) {
+  if (!last_arriver(g.cnt + (blockIdx.y * gridDim.x + blockIdx.x), g.splits, reinterpret_cast<int*>(lds))) return;
+  const int r0 = blockIdx.x * (TM * 32), rn = min(TM * 32, g.k - r0);
+  const int cb0 = blockIdx.y * (WN * TN * 32), cn = min(WN * TN * 32, RSC - cb0);
+  for (int e = threadIdx.x; e < rn * cn; e += blockDim.x) {
+    const int rr = e / cn, cc = e - rr * cn;
+    const long long off = (long long)(r0 + rr) * RSC + cb0 + cc;
+    float sum = 0.f;
+    int zz = 0;
+    for (; zz + 8 <= g.splits; zz += 8) {  // 8 independent loads in flight, summed in slab order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slabs[(zz + u) * g.slab + off];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; zz < g.splits; ++zz) sum += slabs[zz * g.slab + off];
+    dw_final[off] = sum;
+  }
+}
+
+// Forward tail with in-launch BatchNorm: the last workgroup of each column block (all row tiles
+// of its WN*TN*32 channels have written their partials) merges them (no finalize launch).
+template <int TM, int TN, int WN>
+TSPM_DEV void fwd_bn_tail(const ConvArgs& g, const tspm_bn_fuse& bf, float* lds) {
+  if (!bf.counters) return;
+  if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(lds))) return;
+  constexpr int CB = WN * TN * 32;
+  double* red = reinterpret_cast<double*>(lds) + 2;
+  double* smu = red + blockDim.x;
+  bn_merge_block(g.m, g.k, gridDim.x, TM * 32, bf.partial, blockIdx.y * CB, CB, bf.running_mean, bf.running_var,
+                 bf.momentum, bf.eps, bf.save_mean, bf.save_invstd, red, smu);
+}
+
+}  // namespace
+
+// Host-side launchers of the LDS-staged kernels (conv_lds.hip), called by the C ABI entry points
+// in conv.hip for tspm_conv_algo.variant == 1.  Return a TSPM status.
+namespace tspm_detail {
+struct LdsAlgo {
+  int tm, tn, wm, wn, wk, splits;
+};
+bool lds_fwd_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
+bool lds_dgrad_supported(const tspm_conv_shape* s, const LdsAlgo& a);
+bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
+size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
+size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
+size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
+int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st);
+int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
+              void* ws, size_t ws_bytes, hipStream_t st);
+int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
+              size_t ws_bytes, hipStream_t st);
+}  // namespace tspm_detail

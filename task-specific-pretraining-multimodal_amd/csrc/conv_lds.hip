@@ -1,0 +1,652 @@
+// LDS-staged implicit-GEMM convolution (tspm_conv_algo.variant == 1) on v_mfma_f32_32x32x2_f32.
+//
+// Replaces nn.Conv2d fwd / dgrad / wgrad of MML_Suite/models/msa/networks/resnet.py:25,30,176
+// (3x3 s1/s2 p1 and 1x1 s2 convolutions; the Cin=1 stem stays on conv.hip's gather kernels).
+//
+// Why a second family: operands fetched straight into MFMA fragments are "fragment-shaped" loads,
+// 32 rows x 32 B per wave instruction.  Measured on MI355X (scripts/membench.py) such loads stream
+// at ~9.6 TB/s chip-wide against ~34 TB/s for full 128-B lines, and the register-direct kernels
+// (conv.hip) sit under that ceiling.  Here every operand stage is fetched in full lines (8 lanes
+// per 128-B row segment), staged through LDS and read back in fragment order:
+//   * workgroup = 4 waves = WM x WN x WK; tile BM x BN = (WM*TM*32) x (WN*TN*32); the WK waves split
+//     each 32-deep stage between them (8*4/WK reduction elements each) and combine their
+//     accumulators through LDS in fixed order at the end;
+//   * an LDS ring of 2-4 stage slots filled by LDS-DMA (global_load_lds, 16 B per lane): the loads
+//     of the next D-1 stages are in flight while one stage is multiplied; one barrier per stage;
+//   * operands whose fragments run along a 128-B row (the gathered activation rows of fwd / dgrad
+//     and the fwd weights) are stored as 32-float rows with the 16-B chunk q of row r at position
+//     q ^ ((r >> 1) & 7): the ds_read_b128 of one chunk column by 32 rows is bank-conflict-free;
+//     operands whose fragments run down a column (dgrad weights, both wgrad operands) are read with
+//     ds_read_b32 from plain rows (conflict-free: 32 consecutive floats per lane half);
+//   * split-K over `splits` workgroups (grid.z): fp32 slabs written through (sc1), reduced in slab
+//     order by the last arriving workgroup of each tile, which then runs the epilogue (results do
+//     not depend on arrival order).
+// Row blocks never straddle an output position (N % BM == 0 with the HWNC row order), so the set
+// of non-padding taps is uniform per workgroup and padding taps are skipped, not multiplied.
+#include "conv_common.h"
+
+#ifdef TSPM_STAMPS
+__device__ unsigned long long tspm_g_stamps_lds[TSPM_STAMP_WAVES * TSPM_STAMP_SLOTS];
+extern "C" int tspm_debug_stamps_lds(void* host_dst, size_t bytes) {
+  if (bytes > sizeof(tspm_g_stamps_lds)) bytes = sizeof(tspm_g_stamps_lds);
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(tspm_g_stamps_lds), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+extern "C" int tspm_debug_stamps_lds_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(tspm_g_stamps_lds)) != hipSuccess) return 2;
+  return hipMemset(p, 0, sizeof(tspm_g_stamps_lds)) == hipSuccess ? 0 : 2;
+}
+#endif
+
+namespace {
+
+constexpr int kThreads = 256;
+
+TSPM_DEV int swz(int row) { return (row >> 1) & 7; }
+
+// 4 consecutive k (chunk q) of `row` in a swizzled 32-float-row image
+TSPM_DEV f32x4 frag_row(const float* img, int row, int q) {
+  return *reinterpret_cast<const f32x4*>(img + row * 32 + ((q ^ swz(row)) << 2));
+}
+// img[k0 + j][col], j < 4, of a plain image with row length ld
+TSPM_DEV f32x4 frag_col(const float* img, int ld, int k0, int col) {
+  f32x4 v;
+  v[0] = img[k0 * ld + col];
+  v[1] = img[(k0 + 1) * ld + col];
+  v[2] = img[(k0 + 2) * ld + col];
+  v[3] = img[(k0 + 3) * ld + col];
+  return v;
+}
+
+// wave -> (wm, wn, wk); wk slowest so that the WM*WN waves of one k-slice are contiguous
+template <class C>
+struct WaveId {
+  int wm, wn, wk;
+  TSPM_DEV WaveId() {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    wm = w % C::WM;
+    wn = (w / C::WM) % C::WN;
+    wk = w / (C::WM * C::WN);
+  }
+};
+
+// one 16-B-per-lane LDS-DMA: lane l's bytes land at dst + 16*l (dst wave-uniform)
+TSPM_DEV void glds16(const float* src, float* dst) {
+#ifndef TSPM_EXP_NOGLDS  // diagnostic ablation (stamped build only): skip the operand DMA
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+#endif
+}
+
+// ring depth for a stage image of `stage_floats`: as deep as fits 64 KiB (two workgroups per CU
+// keep 128 KiB of rings), at least double-buffered
+#ifndef TSPM_RING_MAX
+#define TSPM_RING_MAX 4
+#endif
+#ifndef TSPM_RING_BYTES
+#define TSPM_RING_BYTES (64 * 1024)
+#endif
+template <int STAGE>
+constexpr int ring_depth() {
+  int d = TSPM_RING_MAX;
+  while (d > 2 && STAGE * 4 * d > TSPM_RING_BYTES) --d;
+  return d;
+}
+
+template <int TM_, int TN_, int WM_, int WN_, int WK_>
+struct Cfg {
+  static constexpr int TM = TM_, TN = TN_, WM = WM_, WN = WN_, WK = WK_;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  static constexpr int KGW = 4 / WK;                     // 8-k groups per wave per stage
+  static constexpr int STAGE = (BM + BN) * 32;           // floats per stage image (A then B)
+  static constexpr int D = ring_depth<STAGE>();          // LDS ring slots
+  static constexpr int NI = (BM + BN) / 32;              // LDS-DMA instructions per thread per stage
+  static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+};
+
+// Per-stage operand offsets returned by a kernel's prep(stage) (A and B operand base offsets).
+struct Off {
+  long long a, b;
+};
+
+// One stage's MFMAs with the next stage's LDS-DMA issues interleaved between them.  Measured
+// (scripts/stamp_conv.py ablations): a global_load_lds blocks its wave ~170 cycles at issue, and
+// with one wave per SIMD issuing them all before the MFMAs serialised DMA issue and matrix work
+// (per stage: DMA path 0.56 us + MFMA path 0.65 us = 1.13 us).  Issued between MFMAs (64-cycle
+// f32 MFMAs keep the matrix pipe busy meanwhile) the issue cost hides under the matrix work.
+// MFMA order (kk, j, a, b) equals Acc::mma4's, so results are bitwise unchanged.
+template <class C, int NI, class IssueI>
+TSPM_DEV void mma_interleaved(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM],
+                              const f32x4 (&B)[C::KGW][C::TN], IssueI&& issue_i) {
+  constexpr int NF = C::KGW * 4 * C::TM * C::TN;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int b = f % C::TN, a = (f / C::TN) % C::TM, j = (f / (C::TN * C::TM)) % 4, kk = f / (C::TN * C::TM * 4);
+    acc.v[a][b] = mfma32(A[kk][a][j], B[kk][b][j], acc.v[a][b]);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if ((i * NF) / NI == f) issue_i(i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// LDS-DMA ring over stages [st0, st1): C::D stage slots of C::STAGE floats.  prep(st) returns the
+// operand offsets of stage st, issue_i(off, slot, i) issues this thread's i-th of C::NI
+// global_load_lds (16 B per lane, lane-linear destination) of that stage into the slot,
+// frags(slot, A, B) reads one stage's MFMA fragments from LDS.  Loads run D-1 stages ahead of the
+// multiply.  Ordering: a slot is read only after the issuing threads' counted `s_waitcnt vmcnt`
+// and a barrier; a slot is refilled only after the barrier that follows every wave's multiply of
+// its previous stage (the MFMAs consumed the ds_reads).  Past the end the ring re-loads stage
+// st1-1 into slots that are never read again, so the vmcnt count is the same in every iteration.
+// Raw s_barrier, not __syncthreads(): the latter waits vmcnt(0) and would drain the ring.  Every
+// thread of the workgroup must call this with the same st0/st1; the ring is drained on return.
+template <class C, class Prep, class IssueI, class Frags>
+TSPM_DEV void ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, IssueI&& issue_i,
+                        Frags&& frags) {
+  constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
+  const int n = st1 - st0;
+  if (n <= 0) return;
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) {
+    const Off off = prep(min(st0 + d, st1 - 1));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) issue_i(off, lds + d * SF, i);
+  }
+  f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
+  for (int it = 0; it < n; ++it) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * NI) : "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
+    const Off off = prep(min(st0 + it + D - 1, st1 - 1));
+    float* nslot = lds + ((it + D - 1) % D) * SF;
+    frags(lds + (it % D) * SF, A, B);
+    mma_interleaved<C, NI>(acc, A, B, [&](int i) { issue_i(off, nslot, i); });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Combine the WK k-slices of each (wm, wn) tile through LDS, in k-slice order (deterministic).
+// Afterwards waves with wk == 0 hold the tile.  All waves must call (barriers).
+template <class C>
+TSPM_DEV void combine_k(Acc<C::TM, C::TN>& acc, float* lds, const WaveId<C>& id, int lane) {
+  if constexpr (C::WK > 1) {
+    constexpr int TILE = C::TM * C::TN * 16 * 64;
+    const int mn = id.wm * C::WN + id.wn;
+    __syncthreads();  // the stage images may still be read by slower waves
+    if (id.wk > 0) {
+      float* dst = lds + ((id.wk - 1) * C::WM * C::WN + mn) * TILE;
+#pragma unroll
+      for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::TN; ++b)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dst[((a * C::TN + b) * 16 + i) * 64 + lane] = acc.v[a][b][i];
+    }
+    __syncthreads();
+    if (id.wk == 0) {
+      for (int k = 1; k < C::WK; ++k) {
+        const float* src = lds + ((k - 1) * C::WM * C::WN + mn) * TILE;
+#pragma unroll
+        for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+          for (int b = 0; b < C::TN; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc.v[a][b][i] += src[((a * C::TN + b) * 16 + i) * 64 + lane];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Split-K over workgroups: every workgroup writes its (combined) tile to slab z; the last arriver
+// of the tile re-reads all slabs in slab order into the waves that hold the tile.  Returns false in
+// the workgroups that are done.  slab = rows*ld floats; tile origin (row0, col0) per wave.
+template <class C>
+TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lane, float* slabs, long long slab,
+                            int splits, unsigned* cnt, int row0, int col0, int rows, int cols, long long ld,
+                            float* lds) {
+  if (splits <= 1) return true;
+  if (id.wk == 0) acc.store(slabs + (long long)blockIdx.z * slab, row0, col0, rows, cols, ld, lane, false, true);
+  if (!last_arriver(cnt + (blockIdx.y * gridDim.x + blockIdx.x), (unsigned)splits, reinterpret_cast<int*>(lds)))
+    return false;
+  if (id.wk == 0) {
+    acc.zero();
+    for (int z = 0; z < splits; ++z) {
+      const float* src = slabs + (long long)z * slab;
+#pragma unroll
+      for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::TN; ++b) {
+          const int col = min(col0 + b * 32 + (lane & 31), cols - 1);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int row = min(row0 + a * 32 + acc_row(i, lane), rows - 1);
+            acc.v[a][b][i] += src[(long long)row * ld + col];
+          }
+        }
+    }
+  }
+  return true;
+}
+
+// =============================================================================================
+// Forward: y[(p,q,n), k] = sum_{valid (r,s), c} x[(p*st-pad+r, q*st-pad+s, n), c] w[k, r, s, c]
+// A image: BM rows (n) x 32 channels (swizzled); B image: BN rows (output channel) x 32 channels.
+// =============================================================================================
+template <class C>
+__global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
+                                                     const float* __restrict__ w, float* __restrict__ y,
+                                                     tspm_bn_fuse bf, float* __restrict__ slabs) {
+  extern __shared__ float lds[];
+  TSPM_STAMP(tspm_g_stamps_lds, 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const WaveId<C> id;
+  const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
+  const int m0 = blockIdx.x * C::BM, n0col = blockIdx.y * C::BN;
+  const int pos = m0 / N, nb0 = m0 - pos * N;
+  const int pp = pos / g.q, qq = pos - pp * g.q;
+  const int h0 = pp * g.st - g.pad, w0 = qq * g.st - g.pad;
+  const int r_lo = max(0, -h0), r_hi = min(g.r - 1, g.h - 1 - h0);
+  const int s_lo = max(0, -w0), s_hi = min(g.s - 1, g.w - 1 - w0);
+  const int nr = r_hi - r_lo + 1, ns = s_hi - s_lo + 1;
+  const int cb = Cc >> 5;
+  const int T = (nr > 0 && ns > 0) ? nr * ns * cb : 0;
+  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+
+  constexpr int NA = C::BM / 32, NB = C::BN / 32;
+  const int wv = tid >> 6;
+  const float* xa[NA];
+  const float* wb[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = (i * 4 + wv) * 8 + (lane >> 3);
+    xa[i] = x + (long long)(nb0 + row) * Cc + (((lane & 7) ^ swz(row)) << 2);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = (i * 4 + wv) * 8 + (lane >> 3);
+    wb[i] = w + (long long)min(n0col + row, K - 1) * RSC + (((lane & 7) ^ swz(row)) << 2);
+  }
+  Acc<C::TM, C::TN> acc;
+  acc.zero();
+  ring_loop<C>(
+      acc, lds, st0, st1,
+      [&](int st) -> Off {
+        const int tap = st / cb, cc = (st - tap * cb) << 5;
+        const int tr = tap / ns;
+        const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
+        return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
+      },
+      [&](const Off& off, float* slot, int i) {
+        if (i < NA) glds16(xa[i] + off.a, slot + (i * 4 + wv) * 256);
+        else glds16(wb[i - NA] + off.b, slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256);
+      },
+      [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
+#pragma unroll
+        for (int kk = 0; kk < C::KGW; ++kk) {
+          const int q = (id.wk * C::KGW + kk) * 2 + (lane >> 5);
+#pragma unroll
+          for (int a = 0; a < C::TM; ++a) A[kk][a] = frag_row(img, (id.wm * C::TM + a) * 32 + (lane & 31), q);
+#pragma unroll
+          for (int b = 0; b < C::TN; ++b)
+            B[kk][b] = frag_row(img + C::BM * 32, (id.wn * C::TN + b) * 32 + (lane & 31), q);
+        }
+      });
+  TSPM_STAMP(tspm_g_stamps_lds, 2);
+  combine_k<C>(acc, lds, id, lane);
+  TSPM_STAMP(tspm_g_stamps_lds, 3);
+  const int row0 = m0 + id.wm * C::TM * 32, col0 = n0col + id.wn * C::TN * 32;
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds))
+    return;
+  TSPM_STAMP(tspm_g_stamps_lds, 4);
+  const bool active = id.wk == 0 && col0 < K;
+  if (active) {
+    acc.store(y, row0, col0, g.m, K, K, lane, false);
+    if (bf.partial)
+      acc.bn_partials(bf.partial, (long long)gridDim.x * C::WM * K, blockIdx.x * C::WM + id.wm, row0, col0, g.m, K,
+                      lane, bf.counters != nullptr);
+  }
+  TSPM_STAMP(tspm_g_stamps_lds, 5);
+  if (bf.counters) {
+    if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(lds))) return;
+    double* red = reinterpret_cast<double*>(lds) + 2;
+    double* smu = red + kThreads;
+    bn_merge_block(g.m, K, gridDim.x * C::WM, C::TM * 32, bf.partial, n0col, C::BN, bf.running_mean,
+                   bf.running_var, bf.momentum, bf.eps, bf.save_mean, bf.save_invstd, red, smu);
+  }
+}
+
+// =============================================================================================
+// Data gradient: dx[(h,w,n), ci] = sum_{valid (r,s), co} dy[((h+pad-r)/st, (w+pad-s)/st, n), co] w[co,r,s,ci]
+// A image: BM rows (n) x 32 output channels (swizzled); B image: 32 rows (co) x BN input channels.
+// =============================================================================================
+template <class C>
+__global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
+                                                       const float* __restrict__ w, float* __restrict__ dx,
+                                                       float* __restrict__ slabs) {
+  extern __shared__ float lds[];
+  TSPM_STAMP(tspm_g_stamps_lds, 0);
+  TSPM_STAMP_CLK(tspm_g_stamps_lds, 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const WaveId<C> id;
+  const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
+  const int m0 = blockIdx.x * C::BM, c0col = blockIdx.y * C::BN;
+  const int pos = m0 / N, nb0 = m0 - pos * N;
+  const int hi = pos / g.w, wi = pos - hi * g.w;
+  unsigned rmask = 0, smask = 0;
+  for (int r = 0; r < g.r; ++r) {
+    const int t = hi + g.pad - r;
+    if (t >= 0 && t % g.st == 0 && t / g.st < g.p) rmask |= 1u << r;
+  }
+  for (int s = 0; s < g.s; ++s) {
+    const int t = wi + g.pad - s;
+    if (t >= 0 && t % g.st == 0 && t / g.st < g.q) smask |= 1u << s;
+  }
+  const int nr = __builtin_popcount(rmask), ns = __builtin_popcount(smask);
+  const int kb = K >> 5;
+  const int T = nr * ns * kb;
+  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+
+  constexpr int NA = C::BM / 32;
+  constexpr int BCH = C::BN / 4;            // 16-B chunks per B row
+  constexpr int NB = C::BN / 32;            // = 32 rows * BCH chunks / 256 threads
+  const int wv = tid >> 6;
+  const float* da[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = (i * 4 + wv) * 8 + (lane >> 3);
+    da[i] = dy + (long long)(nb0 + row) * K + (((lane & 7) ^ swz(row)) << 2);
+  }
+  const float* wb[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int e = (i * 4 + wv) * 64 + lane;
+    const int brow = e / BCH, bcol = (e - brow * BCH) * 4;
+    wb[i] = w + (long long)brow * RSC + min(c0col + bcol, Cc - 4);
+  }
+  Acc<C::TM, C::TN> acc;
+  acc.zero();
+  ring_loop<C>(
+      acc, lds, st0, st1,
+      [&](int st) -> Off {
+        const int t = st / kb, k0 = (st - t * kb) << 5;
+        const int ri = t / ns, si = t - ri * ns;
+        unsigned rm = rmask, sm = smask;
+        for (int i = 0; i < ri; ++i) rm &= rm - 1;
+        for (int i = 0; i < si; ++i) sm &= sm - 1;
+        const int r = __builtin_ctz(rm), s = __builtin_ctz(sm);
+        const int pp = (hi + g.pad - r) / g.st, qq = (wi + g.pad - s) / g.st;
+        return Off{((long long)pp * g.q + qq) * N * K + k0, (long long)k0 * RSC + (r * g.s + s) * Cc};
+      },
+      [&](const Off& off, float* slot, int i) {
+        if (i < NA) glds16(da[i] + off.a, slot + (i * 4 + wv) * 256);
+        else glds16(wb[i - NA] + off.b, slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256);
+      },
+      [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
+#pragma unroll
+        for (int kk = 0; kk < C::KGW; ++kk) {
+          const int q = (id.wk * C::KGW + kk) * 2 + (lane >> 5);
+#pragma unroll
+          for (int a = 0; a < C::TM; ++a) A[kk][a] = frag_row(img, (id.wm * C::TM + a) * 32 + (lane & 31), q);
+#pragma unroll
+          for (int b = 0; b < C::TN; ++b)
+            B[kk][b] = frag_col(img + C::BM * 32, C::BN, q * 4, (id.wn * C::TN + b) * 32 + (lane & 31));
+        }
+      });
+  TSPM_STAMP(tspm_g_stamps_lds, 2);
+  combine_k<C>(acc, lds, id, lane);
+  TSPM_STAMP(tspm_g_stamps_lds, 3);
+  const int row0 = m0 + id.wm * C::TM * 32, col0 = c0col + id.wn * C::TN * 32;
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds))
+    return;
+  TSPM_STAMP(tspm_g_stamps_lds, 4);
+  if (id.wk == 0 && col0 < Cc) acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
+  TSPM_STAMP(tspm_g_stamps_lds, 5);
+  TSPM_STAMP_CLK(tspm_g_stamps_lds, 7);
+}
+
+// =============================================================================================
+// Weight gradient: dw[co, (r,s,ci)] = sum_m dy[m, co] x[in(m, r, s), ci], one tap per workgroup
+// column block (C % BN == 0).  Stage = 32 rows m (32 samples of one output position inside the
+// tap's valid rectangle).  A image: 32 rows (m) x BM output channels; B image: 32 rows x BN inputs.
+// =============================================================================================
+template <class C>
+__global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float* __restrict__ x,
+                                                       const float* __restrict__ dy, float* __restrict__ dw,
+                                                       float* __restrict__ slabs) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const WaveId<C> id;
+  const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
+  const int co0 = blockIdx.x * C::BM, col0b = blockIdx.y * C::BN;
+  const int tap = col0b / Cc, ci0 = col0b - tap * Cc;
+  const int r = tap / g.s, s = tap - r * g.s;
+  const int pp_lo = max(0, cdiv_dev(g.pad - r, g.st)), pp_hi = min(g.p - 1, (g.h - 1 + g.pad - r) / g.st);
+  const int qq_lo = max(0, cdiv_dev(g.pad - s, g.st)), qq_hi = min(g.q - 1, (g.w - 1 + g.pad - s) / g.st);
+  const int npp = max(0, pp_hi - pp_lo + 1), nqq = max(0, qq_hi - qq_lo + 1), n32 = N >> 5;
+  const int T = npp * nqq * n32;
+  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+
+  constexpr int ACH = C::BM / 4, BCH = C::BN / 4;
+  constexpr int NA = C::BM / 32, NB = C::BN / 32;
+  const int wv = tid >> 6;
+  const float* ap[NA];
+  const float* bp[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int e = (i * 4 + wv) * 64 + lane;
+    const int arow = e / ACH, acol = (e - arow * ACH) * 4;
+    ap[i] = dy + (long long)arow * K + min(co0 + acol, K - 4);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int e = (i * 4 + wv) * 64 + lane;
+    const int brow = e / BCH, bcol = (e - brow * BCH) * 4;
+    bp[i] = x + (long long)brow * Cc + ci0 + bcol;
+  }
+  Acc<C::TM, C::TN> acc;
+  acc.zero();
+  ring_loop<C>(
+      acc, lds, st0, st1,
+      [&](int st) -> Off {
+        const int pc = st / n32, nc = st - pc * n32;
+        const int ip = pc / nqq, iq = pc - ip * nqq;
+        const int pp = pp_lo + ip, qq = qq_lo + iq;
+        const long long mrow = ((long long)pp * g.q + qq) * N + nc * 32;
+        const long long xrow = ((long long)(pp * g.st - g.pad + r) * g.w + (qq * g.st - g.pad + s)) * N + nc * 32;
+        return Off{mrow * K, xrow * Cc};
+      },
+      [&](const Off& off, float* slot, int i) {
+        if (i < NA) glds16(ap[i] + off.a, slot + (i * 4 + wv) * 256);
+        else glds16(bp[i - NA] + off.b, slot + 32 * C::BM + ((i - NA) * 4 + wv) * 256);
+      },
+      [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
+#pragma unroll
+        for (int kk = 0; kk < C::KGW; ++kk) {
+          const int k0 = (id.wk * C::KGW + kk) * 8 + 4 * (lane >> 5);
+#pragma unroll
+          for (int a = 0; a < C::TM; ++a) A[kk][a] = frag_col(img, C::BM, k0, (id.wm * C::TM + a) * 32 + (lane & 31));
+#pragma unroll
+          for (int b = 0; b < C::TN; ++b)
+            B[kk][b] = frag_col(img + 32 * C::BM, C::BN, k0, (id.wn * C::TN + b) * 32 + (lane & 31));
+        }
+      });
+  combine_k<C>(acc, lds, id, lane);
+  const int row0 = co0 + id.wm * C::TM * 32, col0 = col0b + id.wn * C::TN * 32;
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds))
+    return;
+  if (id.wk == 0 && row0 < K) acc.store(dw, row0, col0, K, RSC, RSC, lane, false);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+using tspm_detail::LdsAlgo;
+
+bool algo_ok(const LdsAlgo& a) {
+  if (!((a.tm == 1 || a.tm == 2) && (a.tn == 1 || a.tn == 2))) return false;
+  if (!(a.wm >= 1 && a.wn >= 1 && a.wk >= 1 && a.wm * a.wn * a.wk == 4)) return false;
+  return a.splits >= 1 && a.splits <= 256;
+}
+int bm_of(const LdsAlgo& a) { return a.wm * a.tm * 32; }
+int bn_of(const LdsAlgo& a) { return a.wn * a.tn * 32; }
+
+size_t lds_bytes(const LdsAlgo& a, bool bn_tail) {
+  const size_t st1 = (size_t)(bm_of(a) + bn_of(a)) * 32 * sizeof(float);
+  int depth = TSPM_RING_MAX;  // = ring_depth<>
+  while (depth > 2 && st1 * depth > TSPM_RING_BYTES) --depth;
+  const size_t stage = depth * st1;
+  const size_t comb = (size_t)(a.wk - 1) * a.wm * a.wn * a.tm * a.tn * 16 * 64 * sizeof(float);
+  const size_t tail = bn_tail ? 16 + 8 * (size_t)(kThreads + bn_of(a)) : 16;
+  return std::max(std::max(stage, comb), tail);
+}
+
+bool hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
+  if (!st) return true;
+  return st->sc == 1 && st->sn == s->c && st->sw == (long long)s->n * s->c && st->sh == (long long)s->w * s->n * s->c;
+}
+
+ConvArgs args_of(const tspm_conv_shape* s) {
+  ConvArgs g;
+  g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
+  g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
+  g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
+  g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
+  return g;
+}
+
+size_t splitk_ws(int splits, long long rows, long long cols) {
+  return splits > 1 ? TSPM_COUNTER_BYTES + (size_t)splits * rows * cols * sizeof(float) : 0;
+}
+
+// dispatch over the supported (tm, tn, wm, wn, wk) combinations
+#define TSPM_LDS_CASE(TM_, TN_, WM_, WN_, WK_, FN)                                      \
+  if (a.tm == TM_ && a.tn == TN_ && a.wm == WM_ && a.wn == WN_ && a.wk == WK_) {      \
+    using CF = Cfg<TM_, TN_, WM_, WN_, WK_>;                                          \
+    FN(CF);                                                                           \
+    return TSPM_OK;                                                                   \
+  }
+#define TSPM_LDS_WAVES(TM_, TN_, FN)      \
+  TSPM_LDS_CASE(TM_, TN_, 4, 1, 1, FN)    \
+  TSPM_LDS_CASE(TM_, TN_, 2, 2, 1, FN)    \
+  TSPM_LDS_CASE(TM_, TN_, 1, 4, 1, FN)    \
+  TSPM_LDS_CASE(TM_, TN_, 2, 1, 2, FN)    \
+  TSPM_LDS_CASE(TM_, TN_, 1, 2, 2, FN)    \
+  TSPM_LDS_CASE(TM_, TN_, 1, 1, 4, FN)
+#define TSPM_LDS_DISPATCH(FN)   \
+  TSPM_LDS_WAVES(1, 1, FN)      \
+  TSPM_LDS_WAVES(1, 2, FN)      \
+  TSPM_LDS_WAVES(2, 1, FN)      \
+  TSPM_LDS_WAVES(2, 2, FN)      \
+  return TSPM_ERR_INVALID;
+
+}  // namespace
+
+namespace tspm_detail {
+
+bool lds_fwd_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a) {
+  if (!algo_ok(a) || !hwnc(s, xs)) return false;
+  if (s->c % 32 != 0 || s->r > 31 || s->s > 31) return false;
+  const int bm = bm_of(a);
+  return s->n % bm == 0 && lds_bytes(a, true) <= 160 * 1024;
+}
+bool lds_dgrad_supported(const tspm_conv_shape* s, const LdsAlgo& a) {
+  if (!algo_ok(a)) return false;
+  if (s->k % 32 != 0 || s->c % 4 != 0 || s->r > 31 || s->s > 31) return false;
+  return s->n % bm_of(a) == 0 && lds_bytes(a, false) <= 160 * 1024;
+}
+bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a) {
+  if (!algo_ok(a) || !hwnc(s, xs)) return false;
+  if (s->n % 32 != 0 || s->k % 4 != 0 || s->c % bn_of(a) != 0) return false;
+  return lds_bytes(a, false) <= 160 * 1024;
+}
+size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
+  return splitk_ws(a.splits, (long long)s->p * s->q * s->n, s->k);
+}
+size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
+  return splitk_ws(a.splits, (long long)s->h * s->w * s->n, s->c);
+}
+size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
+  return splitk_ws(a.splits, s->k, (long long)s->r * s->s * s->c);
+}
+
+int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
+  ConvArgs g = args_of(s);
+  g.m = s->p * s->q * s->n;
+  g.splits = a.splits;
+  float* slabs = nullptr;
+  if (a.splits > 1) {
+    if (!ws || ws_bytes < lds_fwd_workspace(s, a)) return TSPM_ERR_WORKSPACE;
+    g.cnt = static_cast<unsigned*>(ws);
+    slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+  }
+  tspm_bn_fuse bf{};
+  if (bn) bf = *bn;
+  const int bm = bm_of(a), bnn = bn_of(a);
+  const dim3 grid(g.m / bm, cdiv(s->k, bnn), a.splits);
+  if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
+  // in-launch BN merge only when each merging thread reads few tiles (else tspm_bn_finalize)
+  const int tiles = (int)grid.x * a.wm, groups = kThreads / bnn;
+  const tspm_bn_fuse want = bf;
+  if (bf.counters && cdiv(tiles, groups) > 16) bf.counters = nullptr;
+  const size_t lds = lds_bytes(a, bf.counters != nullptr);
+#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, w, y, bf, slabs)
+  const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
+#undef TSPM_FWD
+  if (rc != TSPM_OK) return rc;
+  TSPM_LAUNCH_CHECK();
+  if (want.counters && !bf.counters)
+    return tspm_bn_finalize(g.m, s->k, tiles, a.tm * 32, want.partial, want.running_mean, want.running_var,
+                            want.momentum, want.eps, want.save_mean, want.save_invstd, st);
+  return TSPM_OK;
+}
+
+int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
+              void* ws, size_t ws_bytes, hipStream_t st) {
+  ConvArgs g = args_of(s);
+  g.m = s->h * s->w * s->n;
+  g.splits = a.splits;
+  g.beta = beta ? 1 : 0;
+  float* slabs = nullptr;
+  if (a.splits > 1) {
+    if (!ws || ws_bytes < lds_dgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
+    g.cnt = static_cast<unsigned*>(ws);
+    slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+  }
+  const dim3 grid(g.m / bm_of(a), cdiv(s->c, bn_of(a)), a.splits);
+  if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
+  const size_t lds = lds_bytes(a, false);
+#define TSPM_DG(CFG) hipLaunchKernelGGL(k_dgrad_lds<CFG>, grid, dim3(kThreads), lds, st, g, dy, w, dx, slabs)
+  const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_DG) }();
+#undef TSPM_DG
+  if (rc != TSPM_OK) return rc;
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
+              size_t ws_bytes, hipStream_t st) {
+  ConvArgs g = args_of(s);
+  g.m = s->k;
+  g.splits = a.splits;
+  float* slabs = nullptr;
+  if (a.splits > 1) {
+    if (!ws || ws_bytes < lds_wgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
+    g.cnt = static_cast<unsigned*>(ws);
+    slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+  }
+  const int RSC = s->r * s->s * s->c;
+  const dim3 grid(cdiv(s->k, bm_of(a)), RSC / bn_of(a), a.splits);
+  if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
+  const size_t lds = lds_bytes(a, false);
+#define TSPM_WG(CFG) hipLaunchKernelGGL(k_wgrad_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, dy, dw, slabs)
+  const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_WG) }();
+#undef TSPM_WG
+  if (rc != TSPM_OK) return rc;
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+}  // namespace tspm_detail

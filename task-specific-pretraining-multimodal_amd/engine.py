@@ -68,6 +68,7 @@ class ConvOp:
     def ws_bytes(self, need_dgrad: bool) -> int:
         lib = L.lib()
         b = lib.tspm_conv_wgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_wgrad))
+        b = max(b, lib.tspm_conv_fwd_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd)))
         if need_dgrad:
             b = max(b, lib.tspm_conv_dgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_dgrad)))
         return b
@@ -243,8 +244,10 @@ class EncoderEngine:
                         lib.tspm_bn_bwd_workspace(bn.rows, bn.channels))
         self.ws_conv_bytes = max(conv_ws, 256)
         self.ws_bn_bytes = max(bn_ws, 256)
-        # zero-filled once: both workspaces start with arrival counters that every call leaves zero
+        # zero-filled once: both workspaces start with arrival counters that every call leaves zero;
+        # launches on the auxiliary stream (downsample branch, weight grads) get their own
         self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        self.ws_conv_aux = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
         ncnt = max(op.shape.k for op in self.all_convs()) // 32 + 1
         self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
@@ -276,13 +279,15 @@ class EncoderEngine:
         return w
 
     def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                  bnf: Optional[L.BnFuse] = None) -> None:
+                  bnf: Optional[L.BnFuse] = None, aux: bool = False) -> None:
         lib = L.lib()
         s, a = op.shape, op.algo_fwd
+        ws = self.ws_conv_aux if aux else self.ws_conv
         if self.conv_timer:
             self.conv_timer.begin(op, "fwd")
         L.check(lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x_ptr, ctypes.byref(strides), self._w(op).data_ptr(),
-                                  y.data_ptr(), None if bnf is None else ctypes.byref(bnf), sh), "conv_fwd")
+                                  y.data_ptr(), None if bnf is None else ctypes.byref(bnf), ws.data_ptr(),
+                                  self.ws_conv_bytes, sh), "conv_fwd")
         if self.conv_timer:
             self.conv_timer.end()
 
@@ -295,7 +300,7 @@ class EncoderEngine:
         bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
                        BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
                        bn.invstd.data_ptr())
-        self._conv_fwd(op, x_ptr, strides, y, sh, bnf)
+        self._conv_fwd(op, x_ptr, strides, y, sh, bnf, aux)
 
     def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
                out_t: Optional[torch.Tensor] = None):
@@ -376,7 +381,7 @@ class EncoderEngine:
                     if train:
                         self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, ash, aux=True)
                     else:
-                        self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, ash)
+                        self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, ash, aux=True)
             if train:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
@@ -408,8 +413,9 @@ class EncoderEngine:
                                     fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb, sh),
                 "linear_fwd(fc)")
 
-    def _conv_fwd_eval(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
-        self._conv_fwd(op, x_ptr, strides, y, sh, None)
+    def _conv_fwd_eval(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
+                       aux: bool = False) -> None:
+        self._conv_fwd(op, x_ptr, strides, y, sh, None, aux)
 
     # ---------------------------------------------------------------------------------------
     def _grad(self, p: torch.Tensor) -> torch.Tensor:
@@ -440,22 +446,22 @@ class EncoderEngine:
         if self.aux is not None:  # off the critical path: only Adam consumes weight gradients
             self.aux.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.aux):
-                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream, x_t, dy_t)
+                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream, x_t, dy_t, self.ws_conv_aux)
         else:
-            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh, x_t, dy_t)
+            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh, x_t, dy_t, self.ws_conv)
 
     def _wgrad_launch(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, gw: torch.Tensor,
-                      sh: int, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor]) -> None:
+                      sh: int, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor], ws: torch.Tensor) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "wgrad")
         lib = L.lib()
         if x_t is not None and dy_t is not None:
             L.check(lib.tspm_conv_wgrad_t(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_t.data_ptr(),
                                           x_t.shape[1], dy_t.data_ptr(), dy_t.shape[1], gw.data_ptr(),
-                                          self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_wgrad_t")
+                                          ws.data_ptr(), self.ws_conv_bytes, sh), "conv_wgrad_t")
         else:
             L.check(lib.tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr,
-                                        ctypes.byref(strides), dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(),
+                                        ctypes.byref(strides), dy.data_ptr(), gw.data_ptr(), ws.data_ptr(),
                                         self.ws_conv_bytes, sh), "conv_wgrad")
         if self.conv_timer:
             self.conv_timer.end()

@@ -45,8 +45,10 @@ def conv_fwd(x_nchw: torch.Tensor, w_oihw: torch.Tensor, stride: int, pad: int, 
     wd = w_oihw.contiguous(memory_format=torch.channels_last)
     y = torch.empty(shp.p * shp.q * n, k, device=dev)
     lib = L.lib()
+    wsb = lib.tspm_conv_fwd_workspace(ctypes.byref(shp), ctypes.byref(a))
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=dev)  # counter header starts zero
     L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
-                              y.data_ptr(), None, sh()), "conv_fwd")
+                              y.data_ptr(), None, ws.data_ptr(), wsb, sh()), "conv_fwd")
     return from_hwnc(y, n, shp.p, shp.q, k)
 
 
@@ -81,8 +83,10 @@ def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0), fused
                        inv.data_ptr())
     else:
         bnf = L.BnFuse(part.data_ptr(), None, None, None, 0.1, 1e-5, None, None)
+    wsb = lib.tspm_conv_fwd_workspace(ctypes.byref(shp), ctypes.byref(a))
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=dev)
     L.check(lib.tspm_conv_fwd(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), wd.data_ptr(),
-                              y.data_ptr(), ctypes.byref(bnf), sh()), "conv_fwd")
+                              y.data_ptr(), ctypes.byref(bnf), ws.data_ptr(), wsb, sh()), "conv_fwd")
     if not fused:
         L.check(lib.tspm_bn_finalize(m, k, tiles, rows, part.data_ptr(), L.ptr(rm), L.ptr(rv), 0.1, 1e-5,
                                      mean.data_ptr(), inv.data_ptr(), sh()), "bn_finalize")
@@ -106,7 +110,7 @@ def conv_dgrad(dy_nchw: torch.Tensor, w_oihw: torch.Tensor, in_hw, stride: int, 
         dx = torch.empty(h * w * n, c, device=dev)
     lib = L.lib()
     wsb = lib.tspm_conv_dgrad_workspace(ctypes.byref(shp), ctypes.byref(a))
-    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=dev)  # counter header starts zero
     L.check(lib.tspm_conv_dgrad(ctypes.byref(shp), ctypes.byref(a), dyd.data_ptr(), wd.data_ptr(), dx.data_ptr(),
                                 1 if beta_init is not None else 0, ws.data_ptr(), wsb, sh()), "conv_dgrad")
     return from_hwnc(dx, n, h, w, c)
@@ -134,6 +138,23 @@ def conv_wgrad(x_nchw: torch.Tensor, dy_nchw: torch.Tensor, rs, stride: int, pad
     L.check(lib.tspm_conv_wgrad(ctypes.byref(shp), ctypes.byref(a), xd.data_ptr(), ctypes.byref(st), dyd.data_ptr(),
                                 dw.data_ptr(), ws.data_ptr(), wsb, sh()), "conv_wgrad")
     return dw.contiguous()
+
+
+def lds_supported(kind: str, case, algo) -> bool:
+    """Mirror of the variant-1 (LDS-staged) support rules in include/tspm.h."""
+    n, c, h, w, k, r, s, st, pad = case
+    tm, tn, wn, wk, sp = algo[:5]
+    if len(algo) < 6 or algo[5] != 1:
+        return True
+    if wn * wk == 0 or 4 % (wn * wk):
+        return False
+    wm = 4 // (wn * wk)
+    bm, bn = wm * tm * 32, wn * tn * 32
+    if kind == "fwd":
+        return c % 32 == 0 and n % bm == 0
+    if kind == "dgrad":
+        return k % 32 == 0 and c % 4 == 0 and n % bm == 0
+    return n % 32 == 0 and k % 4 == 0 and c % bn == 0
 
 
 def conv_bound(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:

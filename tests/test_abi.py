@@ -49,13 +49,13 @@ def test_invalid_arguments_are_rejected_before_launch():
     lib = L.load()
     s = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 7, 8)  # wrong p
     a = L.ConvAlgo()
-    assert lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), 1, None, 1, 1, None, None) == 1
+    assert lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), 1, None, 1, 1, None, None, 0, None) == 1
     assert lib.tspm_conv_fwd_tiles(ctypes.byref(s), ctypes.byref(a)) == 0
     good = L.ConvShape(2, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
-    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, None) == 1
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(a), None, None, 1, 1, None, None, 0, None) == 1
     for bad in [(3, 1, 1, 1, 1), (2, 1, 1, 1, 1), (1, 1, 3, 1, 1), (1, 1, 2, 8, 1), (1, 1, 2, 16, 1), (2, 2, 1, 16, 1)]:
         bad_algo = L.ConvAlgo(*bad)
-        assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, None) == 1, bad
+        assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(bad_algo), 16, None, 16, 16, None, None, 0, None) == 1, bad
     assert lib.tspm_bn_finalize(128, 64, 2, 32, 16, None, None, 0.1, 1e-5, 16, 16, None) == 1  # tiles*rows < m
     # dgrad needs K % 8 == 0
     odd = L.ConvShape(2, 8, 8, 64, 12, 3, 3, 1, 1, 8, 8)
@@ -68,6 +68,16 @@ def test_invalid_arguments_are_rejected_before_launch():
     s6 = L.ConvShape(6, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
     assert lib.tspm_conv_wgrad_t(ctypes.byref(s6), ctypes.byref(a), 16, 384, 16, 384, 16, None, 0, None) == 1
     assert lib.tspm_conv_wgrad_t(ctypes.byref(good), ctypes.byref(a), 16, 130, 16, 128, 16, None, 0, None) == 1
+    # variant 1 (LDS-staged): n % BM != 0 and wm*wn*wk != 4 are rejected, split-K needs its workspace
+    s64 = L.ConvShape(64, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
+    v1 = L.ConvAlgo(1, 1, 1, 1, 1, 1)  # wm = 4: BM = 128 > n
+    assert lib.tspm_conv_fwd(ctypes.byref(s64), ctypes.byref(v1), 16, None, 16, 16, None, None, 0, None) == 1
+    assert lib.tspm_conv_dgrad(ctypes.byref(s64), ctypes.byref(v1), 16, 16, 16, 0, None, 0, None) == 1
+    v3 = L.ConvAlgo(1, 1, 3, 1, 1, 1)
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(v3), 16, None, 16, 16, None, None, 0, None) == 1
+    vs = L.ConvAlgo(1, 1, 1, 4, 2, 1)  # BM = 32, split-K 2 without workspace
+    s32 = L.ConvShape(32, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
+    assert lib.tspm_conv_fwd(ctypes.byref(s32), ctypes.byref(vs), 16, None, 16, 16, None, None, 0, None) == 3
     assert lib.tspm_adam_step(10, 17, 16, 16, 16, 16, None) == 1   # misaligned
     assert lib.tspm_dropout_mask(10, 1.0, 0, None, 16, None) == 1   # p must be < 1
 
@@ -80,5 +90,10 @@ def test_workspace_queries():
     assert lib.tspm_conv_fwd_tile_rows(ctypes.byref(s), ctypes.byref(L.ConvAlgo(2, 2, 1, 1, 1))) == 64
     w3 = lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(L.ConvAlgo(1, 1, 1, 4, 3)))
     assert w3 == L.COUNTER_BYTES + 3 * 64 * 9 * 64 * 4
+    v = L.ConvAlgo(1, 1, 1, 1, 4, 1)  # variant 1, split-K 4
+    assert lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(v)) == L.COUNTER_BYTES + 4 * 7 * 7 * 128 * 64 * 4
+    assert lib.tspm_conv_dgrad_workspace(ctypes.byref(s), ctypes.byref(v)) == L.COUNTER_BYTES + 4 * 7 * 7 * 128 * 64 * 4
+    assert lib.tspm_conv_wgrad_workspace(ctypes.byref(s), ctypes.byref(v)) == L.COUNTER_BYTES + 4 * 64 * 9 * 64 * 4
+    assert lib.tspm_conv_fwd_tile_rows(ctypes.byref(s), ctypes.byref(L.ConvAlgo(2, 1, 1, 1, 1, 1))) == 64
     assert lib.tspm_bn_stats_workspace(6272, 64) > 0
     assert lib.tspm_bn_bwd_workspace(6272, 64) >= lib.tspm_bn_stats_workspace(6272, 64)

@@ -10,7 +10,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from abi_helpers import conv_bound, conv_dgrad, conv_fwd, conv_wgrad, from_hwnc, sh, to_hwnc
+from abi_helpers import conv_bound, conv_dgrad, conv_fwd, conv_wgrad, from_hwnc, lds_supported, sh, to_hwnc
 
 pytestmark = pytest.mark.gpu
 EPS32 = 2.0 ** -23
@@ -37,6 +37,10 @@ CONV_CASES = [
 # (tm, tn, wn, wk, splits): tile shape, waves along N per workgroup, in-workgroup split-K, wgrad split
 ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1, 1, 4, 2, 1), (1, 2, 2, 4, 1),
          (1, 1, 1, 16, 1), (1, 2, 1, 16, 1)]
+# variant 1 (LDS-staged): (tm, tn, wn, wk, splits, 1) with wm = 4 / (wn*wk); every (wm, wn, wk) wave
+# arrangement, both tile sizes and split-K over workgroups
+LDS_ALGOS = [(1, 1, 1, 1, 1, 1), (1, 1, 2, 1, 1, 1), (1, 1, 4, 1, 1, 1), (2, 2, 2, 1, 1, 1), (1, 1, 1, 4, 1, 1),
+             (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 2, 1, 1, 2, 1)]
 
 
 def _check(out, ref, bound, what):
@@ -49,8 +53,10 @@ def _check(out, ref, bound, what):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("algo", ALGOS + LDS_ALGOS)
 def test_conv_fwd(gpu, case, algo):
+    if not lds_supported("fwd", case, algo):
+        pytest.skip("variant-1 tile does not fit this shape")
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(hash((case, algo)) % (2 ** 31))
     x = torch.randn(n, c, h, w, generator=g)
@@ -74,9 +80,11 @@ def test_stem_fwd_nchw_input(gpu, case, algo):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("algo", ALGOS[:4] + ALGOS[6:])
+@pytest.mark.parametrize("algo", ALGOS[:4] + ALGOS[6:] + LDS_ALGOS)
 @pytest.mark.parametrize("beta", [0, 1])
 def test_conv_dgrad(gpu, case, algo, beta):
+    if not lds_supported("dgrad", case, algo):
+        pytest.skip("variant-1 tile does not fit this shape")
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(11)
     wt = torch.randn(k, c, r, s, generator=g) * 0.05
@@ -95,8 +103,10 @@ def test_conv_dgrad(gpu, case, algo, beta):
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("algo", ALGOS[:3] + [(1, 1, 1, 4, 7), (2, 2, 2, 2, 3), (1, 2, 4, 1, 16),
-                                             (1, 1, 1, 16, 5), (1, 2, 1, 16, 2)])
+                                             (1, 1, 1, 16, 5), (1, 2, 1, 16, 2)] + LDS_ALGOS + [(1, 1, 1, 1, 16, 1)])
 def test_conv_wgrad(gpu, case, algo):
+    if not lds_supported("wgrad", case, algo):
+        pytest.skip("variant-1 tile does not fit this shape")
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(13)
     x = torch.randn(n, c, h, w, generator=g)
@@ -123,13 +133,16 @@ def test_stem_wgrad_nchw_input(gpu, case):
 
 
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 5, 6, 8, 12)])
-@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 2, 2, 1), (1, 1, 1, 8, 1)])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 2, 2, 1), (1, 1, 1, 8, 1), (1, 1, 1, 1, 1, 1),
+                                  (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1)])
 @pytest.mark.parametrize("offset", [0.0, 3e4])
 @pytest.mark.parametrize("fused", [True, False])
 def test_conv_fwd_epilogue_bn_statistics(gpu, case, algo, offset, fused):
     """BatchNorm batch statistics of the conv output from the conv epilogue's per-tile partials,
     merged in-launch (fused) or by tspm_bn_finalize."""
     from abi_helpers import conv_fwd_with_stats
+    if not lds_supported("fwd", case, algo):
+        pytest.skip("variant-1 tile does not fit this shape")
     n, c, h, w, k, r, s, st, pad = case
     g = torch.Generator().manual_seed(31)
     x = torch.randn(n, c, h, w, generator=g) + offset / 100
