@@ -105,6 +105,8 @@ def main() -> None:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--phased", action="store_true",
+                    help="at N=1, run the DP step path anyway (1-rank RCCL group, all-reduce = identity)")
     args = ap.parse_args()
 
     import tspm_amd
@@ -119,12 +121,17 @@ def main() -> None:
     torch.manual_seed(0)
     model = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
     opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4, grad_scale=1.0 / world)
-    allreduce = None
+    step = tspm_amd.FusedTrainStep(model, opt, None, B, use_graph=not args.no_graph)
     if world > 1:
         for fg in opt.flat_groups():
             dist.broadcast(fg.param, src=0)
-        allreduce = ddp.GradAllReduce([fg.grad for fg in opt.flat_groups()])
-    step = tspm_amd.FusedTrainStep(model, opt, None, B, use_graph=not args.no_graph, allreduce=allreduce)
+        # RCCL gradient all-reduce overlapped with the second backward phase (ddp.PhasedGradAllReduce)
+        step.allreduce = step.phased_allreduce()
+    elif args.phased:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        step.allreduce = step.phased_allreduce(force=os.environ.get("TSPM_PHASED_FORCE", "1") == "1")
     batches = synthetic_device_batches(4, B, 1234 + rank, dev)
 
     def one(i):
@@ -160,12 +167,15 @@ def main() -> None:
     saved = step.use_graph
     step.use_graph = False
     saved_serial = step.serial
+    saved_ar = step.allreduce
     step.serial = True  # one stream: each conv's event pair brackets that kernel alone
+    step.allreduce = None  # (the instrumented step is not part of the timed region)
     a, im, lab = batches[0]
     step.load_batch(a, im, lab)
     step.run()
     step.use_graph = saved
     step.serial = saved_serial
+    step.allreduce = saved_ar
     torch.cuda.synchronize()
     for eng in (step.eng_a, step.eng_i):
         eng.conv_timer = None
@@ -200,7 +210,7 @@ def main() -> None:
         result["cpu_baseline"] = cpu_baseline(B, args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -183,6 +183,9 @@ class EncoderEngine:
                 h, w, c = ho, wo, planes
         self.final_hw = (h, w)
         self.final_c = c
+        # backward phase split: the first block of layer3 (ResNet18 [2,2,2,2] -> 4, ResNet34 [3,4,6,3] -> 7)
+        self.split_block = len(encoder.layer1) + len(encoder.layer2)
+        self._bw_state = None
         # weight gradients from transposed operands (16-byte loads on both GEMM operands) whenever
         # an 8-row chunk shares one output position
         # Off by default: measured on MI355X at batch 128 (same box, interleaved runs) the transposed
@@ -475,24 +478,54 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
-    def backward(self, g_emb: torch.Tensor, ld_g: int) -> None:
+    def phase_params(self, phase: int) -> List[torch.nn.Parameter]:
+        """Parameters whose gradients backward phase `phase` (1 or 2) writes: phase 1 = fc and the
+        blocks from layer3 on, phase 2 = layer1, layer2 and the stem."""
+        split = self.split_block
+        mods = []
+        if phase == 1:
+            mods = [self.enc.fc] + [bp for bp in self.blocks[split:]]
+        else:
+            mods = [self.enc.conv1, self.enc.bn1] + [bp for bp in self.blocks[:split]]
+        out = []
+        for m in mods:
+            if isinstance(m, BlockPlan):
+                ms = [m.conv1.module, m.bn1.module, m.conv2.module, m.bn2.module]
+                if m.ds_conv is not None:
+                    ms += [m.ds_conv.module, m.ds_bn.module]
+            else:
+                ms = [m]
+            for mm in ms:
+                out += [p for p in mm.parameters(recurse=False)]
+        return out
+
+    def backward(self, g_emb: Optional[torch.Tensor], ld_g: int, phase: int = 0) -> None:
         """g_emb: [N, hidden] gradient of the fc output (row stride ld_g).  Writes every parameter
-        gradient of the encoder (overwrite semantics) through ``grad_of``."""
+        gradient of the encoder (overwrite semantics) through ``grad_of``.  phase 0 runs the whole
+        backward; phase 1 the fc and the blocks from ``split_block`` (first block of layer3) on,
+        phase 2 (g_emb unused) the remaining blocks and the stem — the DP exchange of phase 1's
+        gradients overlaps phase 2."""
         sh = L.stream_handle()
         lib = L.lib()
         N = self.N
-        fc = self.enc.fc
-        L.check(lib.tspm_linear_bwd_weight(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
-                                           g_emb.data_ptr(), ld_g, self._grad(fc.weight).data_ptr(),
-                                           self._grad(fc.bias).data_ptr() if fc.bias is not None else None, sh),
-                "linear_bwd_weight(fc)")
-        L.check(lib.tspm_linear_bwd_data(N, self.final_c, self.hidden, g_emb.data_ptr(), ld_g, fc.weight.data_ptr(),
-                                         self.g_pooled.data_ptr(), self.final_c, sh), "linear_bwd_data(fc)")
-        h, w = self.final_hw
-        G, Gn = self.gA, self.gB
-        L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(), sh),
-                "avgpool_bwd")
-        for i in range(len(self.blocks) - 1, -1, -1):
+        if phase in (0, 1):
+            fc = self.enc.fc
+            L.check(lib.tspm_linear_bwd_weight(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
+                                               g_emb.data_ptr(), ld_g, self._grad(fc.weight).data_ptr(),
+                                               self._grad(fc.bias).data_ptr() if fc.bias is not None else None, sh),
+                    "linear_bwd_weight(fc)")
+            L.check(lib.tspm_linear_bwd_data(N, self.final_c, self.hidden, g_emb.data_ptr(), ld_g,
+                                             fc.weight.data_ptr(), self.g_pooled.data_ptr(), self.final_c, sh),
+                    "linear_bwd_data(fc)")
+            h, w = self.final_hw
+            G, Gn = self.gA, self.gB
+            L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(),
+                                         sh), "avgpool_bwd")
+            lo, hi = (self.split_block if phase == 1 else 0), len(self.blocks)
+        else:
+            G, Gn = self._bw_state
+            lo, hi = 0, self.split_block
+        for i in range(hi - 1, lo - 1, -1):
             bp = self.blocks[i]
             xin = self.blocks[i - 1].out if i > 0 else self.mp
             s1 = bp.conv1.shape
@@ -527,6 +560,11 @@ class EncoderEngine:
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             self._dgrad(bp.conv1, d1, Gnv, 1, sh)
             G, Gn = Gn, G
+        if phase == 1:
+            self._bw_state = (G, Gn)
+            if self.aux is not None and self.join_aux:
+                torch.cuda.current_stream().wait_stream(self.aux)
+            return
         # stem: maxpool -> relu/bn -> conv1 (weight grad only)
         p1, q1, p2, q2 = self.mp_shape
         C0 = self.stem.shape.k

@@ -23,6 +23,7 @@ import torch
 
 from . import _lib as L
 from .engine import EncoderEngine, prepare_encoder_layout
+from .ddp import PhasedGradAllReduce
 from .optim import FusedAdam
 
 NUM_CLASSES = 10
@@ -176,8 +177,11 @@ class FusedTrainStep:
         L.check(lib.tspm_linear_bwd_data(n, F, hd, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
                                          self.dfused.data_ptr(), F, sh), "head fc0 dgrad")
 
-    def _fwd_bwd(self) -> None:
-        """Enqueue forward + loss + backward on the current stream (+ the side stream)."""
+    def _fwd_bwd(self, phase: int = 0) -> None:
+        """Enqueue forward + loss + backward on the current stream (+ the side stream).  phase 0:
+        everything; 1: forward, loss, head backward and the encoders' backward phase 1 (fc,
+        layer4, layer3); 2: the encoders' backward phase 2 (layer2, layer1, stem) — see
+        EncoderEngine.backward and ddp.PhasedGradAllReduce."""
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
@@ -187,26 +191,125 @@ class FusedTrainStep:
         # stream may only join the origin (main) stream
         self.eng_i.fork_ds = False
         self.eng_i.join_aux = False
+        if phase in (0, 1):
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
+            self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
+            main.wait_stream(side)
+            sh = main.cuda_stream
+            self._head_fwd(sh)
+            L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
+                                               self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
+                                               self.stats.data_ptr(), sh), "cross_entropy")
+            self._head_bwd(sh)
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            self.eng_i.backward(self.dfused[:, ea:], self.F, phase=phase)
+        self.eng_a.backward(self.dfused, self.F, phase=phase)
+        main.wait_stream(side)
+        if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
+            main.wait_stream(self.aux_a)
+            main.wait_stream(self.aux_i)
+        if phase in (0, 2):
+            self.nbt.add_(1)
+
+    def phased_allreduce(self, force: bool = False, bucket_mb: float = 64.0, group=None):
+        """The overlapped DP exchange for this step: gradient ranges of FusedAdam's flat buffers in
+        three phases — (0) head + audio fc/layer4/layer3, (1) image fc/layer4/layer3, (2) both
+        encoders' layer2/layer1/stem — each launched as soon as the backward part that writes it
+        has run (see _run_phased)."""
+        from .ddp import PhasedGradAllReduce, flat_ranges
+        sets = [{id(p) for p in self.eng_a.phase_params(1)} | {id(p) for p in self.model.net.parameters()},
+                {id(p) for p in self.eng_i.phase_params(1)},
+                {id(p) for p in self.eng_a.phase_params(2) + self.eng_i.phase_params(2)}]
+        views = [[], [], []]
+        for fg in self.opt.flat_groups():
+            for p in fg.params:
+                if sum(id(p) in st for st in sets) != 1:
+                    raise L.TspmError("phased all-reduce: parameter not owned by exactly one backward phase")
+            numels = [p.numel() for p in fg.params]
+            for k, st in enumerate(sets):
+                views[k] += [fg.grad[a:b] for a, b in flat_ranges(fg.offsets, numels, fg.numel,
+                                                                  [id(p) in st for p in fg.params])]
+        return PhasedGradAllReduce(views, bucket_mb=bucket_mb, group=group, force=force)
+
+    def _fwd_head(self) -> None:
+        """Forward of both encoders (two streams), fusion head, cross-entropy, head backward."""
+        main = torch.cuda.current_stream()
+        ea = self.model.embd_size_A
+        self.eng_a.aux = self.eng_i.aux = None
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
         self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-        main.wait_stream(side)
+        main.wait_stream(self.side)
         sh = main.cuda_stream
         self._head_fwd(sh)
         L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
                                            self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
                                            self.stats.data_ptr(), sh), "cross_entropy")
         self._head_bwd(sh)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self.eng_i.backward(self.dfused[:, ea:], self.F)
-        self.eng_a.backward(self.dfused, self.F)
-        main.wait_stream(side)
-        if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
-            main.wait_stream(self.aux_a)
-            main.wait_stream(self.aux_i)
         self.nbt.add_(1)
+
+    def _run_phased(self) -> None:
+        """DP step with the RCCL exchange overlapped with backward:
+             main:   [fwd both + head + head bwd] ──────────────────────────── wait ─ [Adam]
+             s_a:        └ [audio bwd late] ─ [audio bwd early] ─┤
+             s_i:        └ [image bwd late] ─ [image bwd early] ─┤
+             RCCL:          all-reduce(head+audio late) · (image late) · (both early)
+        Each bracket is a HIP graph (captured on the second call); the collectives stay outside the
+        graphs on RCCL's stream, ordered against the compute streams by events."""
+        ar = self.allreduce
+        main = torch.cuda.current_stream()
+        sa, si = self.aux_a, self.aux_i
+        ea, F = self.model.embd_size_A, self.F
+        parts = [
+            (main, lambda: self._fwd_head()),
+            (sa, lambda: self.eng_a.backward(self.dfused, F, phase=1)),
+            (si, lambda: self.eng_i.backward(self.dfused[:, ea:], F, phase=1)),
+            (sa, lambda: self.eng_a.backward(None, F, phase=2)),
+            (si, lambda: self.eng_i.backward(None, F, phase=2)),
+            (main, self._opt),
+        ]
+        eager = not self.use_graph or self.calls == 0
+        if not eager and self.graph is None:
+            torch.cuda.synchronize(self.device)
+            gs = []
+            for stream, fn in parts:
+                g = torch.cuda.CUDAGraph()
+                # main-stream parts are captured on torch's own capture stream (the current stream
+                # may be the legacy default stream, which cannot capture) and replayed on main
+                with torch.cuda.graph(g, stream=None if stream is main else stream):
+                    fn()
+                gs.append(g)
+            self.graph = gs
+
+        def run(k):
+            stream, fn = parts[k]
+            with torch.cuda.stream(stream):
+                if eager:
+                    fn()
+                else:
+                    self.graph[k].replay()
+
+        self.eng_i.fork_ds = self.eng_a.fork_ds = False
+        run(0)
+        sa.wait_stream(main)
+        si.wait_stream(main)
+        run(1)
+        with torch.cuda.stream(sa):
+            w_a = ar.launch(0)
+        run(2)
+        with torch.cuda.stream(si):
+            w_i = ar.launch(1)
+        run(3)
+        run(4)
+        main.wait_stream(sa)
+        main.wait_stream(si)
+        w_e = ar.launch(2)
+        ar.wait(w_a + w_i + w_e)
+        run(5)
 
     def _opt(self) -> None:
         self.opt.launch(torch.cuda.current_stream().cuda_stream)
@@ -236,6 +339,11 @@ class FusedTrainStep:
         self.opt.sync_hyper()
         if self.keep_override is not None:
             self.keep.copy_(self.keep_override.reshape(self.keep.shape).to(torch.uint8), non_blocking=True)
+        if isinstance(self.allreduce, PhasedGradAllReduce):
+            self._run_phased()
+            self.opt.note_steps(1)
+            self.calls += 1
+            return
         if not self.use_graph or self.calls == 0:
             self._enqueue_all()
         else:

@@ -65,6 +65,50 @@ def test_gloo_world2_bucketed_allreduce_and_broadcast():
         assert ok_bcast is True, (rank, ok_bcast)
 
 
+def _phased_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        ddp.init_from_env("gloo")
+        # a flat buffer of 5 "parameters" (slots padded to 4 floats), phases interleaved
+        numels = [10, 3, 7, 1, 12]
+        offsets, off = [], 0
+        for n in numels:
+            offsets.append(off)
+            off += -(-n // 4) * 4
+        flat = torch.arange(off, dtype=torch.float32) * (rank + 1)
+        sel1 = [False, True, True, False, True]
+        r1 = ddp.flat_ranges(offsets, numels, off, sel1)
+        r2 = ddp.flat_ranges(offsets, numels, off, [not s for s in sel1])
+        ok_ranges = r1 == [(12, 24), (28, 40)] and r2 == [(0, 12), (24, 28)]
+        ar = ddp.PhasedGradAllReduce([[flat[a:b] for a, b in r1], [flat[a:b] for a, b in r2]], bucket_mb=1e-5)
+        w1 = ar.launch(0)
+        w2 = ar.launch(1)
+        ar.wait(w1 + w2)
+        ok_sum = bool(torch.equal(flat, torch.arange(off, dtype=torch.float32) * sum(range(1, world + 1))))
+        q.put((rank, ok_ranges, ok_sum))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, repr(e), None))
+
+
+def test_gloo_world2_phased_allreduce_ranges():
+    """flat_ranges merges adjacent selected slots (padding included) and the two phases together
+    cover the buffer; PhasedGradAllReduce sums every range across ranks (small buckets)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_phased_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok_ranges, ok_sum in res:
+        assert ok_ranges is True, (rank, ok_ranges)
+        assert ok_sum is True, (rank, ok_sum)
+
+
 def test_single_process_allreduce_is_noop():
     g = torch.ones(10)
     ddp.GradAllReduce([g])()

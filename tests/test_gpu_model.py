@@ -215,6 +215,47 @@ def test_graph_replay_equals_eager(gpu):
     assert torch.equal(results[0], results[1])
 
 
+def test_phased_allreduce_step_equals_plain_step(gpu):
+    """The DP step path — backward split in two phases, graph 1 | RCCL all-reduce of phase-1
+    gradients overlapping graph 2 | RCCL of the rest | Adam graph — under a 1-rank RCCL group
+    (all-reduce = identity) gives bitwise the parameters of the plain fused step, eager and
+    graph-replayed, and covers every parameter exactly once."""
+    import os
+    import socket
+    import torch.distributed as dist
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+        created = True
+    try:
+        results = []
+        for phased in (False, True):
+            torch.manual_seed(9)
+            ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+            opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
+            st = tspm_amd.FusedTrainStep(ours, opt, None, 32, use_graph=True)
+            if phased:
+                st.allreduce = st.phased_allreduce(force=True)
+                covered = sum(v.numel() for ph in st.allreduce.phases for v in ph)
+                assert covered == sum(fg.numel for fg in opt.flat_groups())
+                assert len(st.allreduce.phases[0]) >= 1 and len(st.allreduce.phases[1]) >= 1
+            for i in range(4):
+                audio, image, labels, _ = orc.synthetic_batch(32, seed=50 + i)
+                st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+            torch.cuda.synchronize()
+            bufs = [m.running_var.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+            results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs).cpu())
+        assert torch.equal(results[0], results[1])
+    finally:
+        if created:
+            dist.destroy_process_group()
+
+
 def test_train_step_api_autograd_path(gpu):
     """AVMNIST.train_step with the reference's own torch.optim.Adam: autograd through the HIP
     encoder / head Functions (dropout off for a deterministic comparison)."""
