@@ -353,33 +353,138 @@ __global__ __launch_bounds__(256) void k_bn_bwd_final(long long M, int C, int G,
   }
 }
 
+// Backward apply with the per-channel merge folded in (no separate final launch): workgroup =
+// [rows x 64 channels] (16 float4 lanes x 16 row groups).  Prologue: merge the G partial tiles of
+// its 64 channels in double, in a fixed order (thread (lane, rg) sums tiles rg, rg+16, ... then a
+// fixed 16-way LDS reduction), so every workgroup derives bitwise the same coefficients; the
+// workgroups of row block 0 also write dgamma / dbeta.  Body: dy = ca*g' - cm - cb*(y - mean).
+// G is kept <= 64 by the host (kMergeTiles), so the merge is <= 12 float4 loads per thread, all in
+// flight together.
+constexpr int kMergeTiles = 64;
 template <bool HAS_OUT, bool TWO, bool DRES>
-__global__ __launch_bounds__(256) void k_bn_bwd_apply(long long n4, int C, const float* __restrict__ g,
-                                                      const float* __restrict__ out, const float* __restrict__ y,
-                                                      const float* __restrict__ mean, const float* __restrict__ y2,
-                                                      const float* __restrict__ mean2, const float* __restrict__ coef,
-                                                      float* __restrict__ dy, float* __restrict__ dy2,
-                                                      float* __restrict__ dres) {
-  const int L = C >> 2;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    const int c4 = (int)(i % L);
-    f32x4 gv = ld4(g + 4 * i);
-    if (HAS_OUT) {
-      const f32x4 ov = ld4(out + 4 * i);
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int G, const float* __restrict__ part,
+                                                        const float* __restrict__ inv, const float* __restrict__ gamma,
+                                                        const float* __restrict__ inv2, const float* __restrict__ gamma2,
+                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                        float* __restrict__ dgamma2, float* __restrict__ dbeta2,
+                                                        const float* __restrict__ g, const float* __restrict__ out,
+                                                        const float* __restrict__ y, const float* __restrict__ mean,
+                                                        const float* __restrict__ y2, const float* __restrict__ mean2,
+                                                        long long rows_per_block, float* __restrict__ dy,
+                                                        float* __restrict__ dy2, float* __restrict__ dres) {
+  __shared__ double red[3][4][256];
+  __shared__ f32x4 scoef[6][16];
+  const int t = threadIdx.x;
+  const int lane = t & 15, rg = t >> 4;
+  const int c4 = blockIdx.y * 16 + lane;
+  const bool cok = 4 * c4 < C;
+  const long long plane = (long long)G * C;
+  {
+    double a[3][4] = {};
+    if (cok) {
+      f32x4 v[4][3];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) gv[j] = ov[j] > 0.f ? gv[j] : 0.f;
+      for (int u = 0; u < kMergeTiles / 16; ++u) {
+        const int gt = rg + 16 * u;
+        const bool ok = gt < G;
+        const long long off = (long long)(ok ? gt : 0) * C + 4 * c4;
+        v[u][0] = ok ? ld4(part + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[u][1] = ok ? ld4(part + plane + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[u][2] = (ok && TWO) ? ld4(part + 2 * plane + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < kMergeTiles / 16; ++u)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[k][j] += (double)v[u][k][j];
     }
-    {
-      const f32x4 ca = ld4(coef + 4 * c4), cb = ld4(coef + C + 4 * c4), cm = ld4(coef + 2 * C + 4 * c4);
-      const f32x4 d = ld4(y + 4 * i) - ld4(mean + 4 * c4);
-      st4(dy + 4 * i, ca * gv - cm - cb * d);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[k][j][t] = a[k][j];
+  }
+  __syncthreads();
+  if (rg == 0 && cok) {
+    double sg[4], sx[4], sx2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sg[j] = red[0][j][lane];
+      sx[j] = red[1][j][lane];
+      sx2[j] = red[2][j][lane];
     }
-    if (TWO) {
-      const f32x4 ca = ld4(coef + 3 * C + 4 * c4), cb = ld4(coef + 4 * C + 4 * c4), cm = ld4(coef + 5 * C + 4 * c4);
-      const f32x4 d = ld4(y2 + 4 * i) - ld4(mean2 + 4 * c4);
-      st4(dy2 + 4 * i, ca * gv - cm - cb * d);
+    for (int k = 1; k < 16; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sg[j] += red[0][j][k * 16 + lane];
+        sx[j] += red[1][j][k * 16 + lane];
+        sx2[j] += red[2][j][k * 16 + lane];
+      }
+    const double n = (double)M;
+    f32x4 ca, cb, cm, ca2 = {0.f, 0.f, 0.f, 0.f}, cb2 = ca2, cm2 = ca2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 4 * c4 + j;
+      const double iv = inv[c], ga = gamma[c];
+      const double dg = sx[j] * iv;
+      const double a_ = ga * iv;
+      ca[j] = (float)a_;
+      cb[j] = (float)(a_ * iv * dg / n);
+      cm[j] = (float)(a_ * sg[j] / n);
+      if (blockIdx.x == 0) {
+        if (dgamma) dgamma[c] = (float)dg;
+        if (dbeta) dbeta[c] = (float)sg[j];
+      }
+      if (TWO) {
+        const double iv2 = inv2[c], ga2 = gamma2[c];
+        const double dg2 = sx2[j] * iv2;
+        const double a2 = ga2 * iv2;
+        ca2[j] = (float)a2;
+        cb2[j] = (float)(a2 * iv2 * dg2 / n);
+        cm2[j] = (float)(a2 * sg[j] / n);
+        if (blockIdx.x == 0) {
+          if (dgamma2) dgamma2[c] = (float)dg2;
+          if (dbeta2) dbeta2[c] = (float)sg[j];
+        }
+      }
     }
-    if (DRES) st4(dres + 4 * i, gv);
+    scoef[0][lane] = ca; scoef[1][lane] = cb; scoef[2][lane] = cm;
+    scoef[3][lane] = ca2; scoef[4][lane] = cb2; scoef[5][lane] = cm2;
+  }
+  __syncthreads();
+  if (!cok) return;
+  const f32x4 ca = scoef[0][lane], cb = scoef[1][lane], cm = scoef[2][lane];
+  const f32x4 ca2 = scoef[3][lane], cb2 = scoef[4][lane], cm2 = scoef[5][lane];
+  const f32x4 mu = ld4(mean + 4 * c4);
+  const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const long long r_begin = blockIdx.x * rows_per_block;
+  const long long r_end = min(M, r_begin + rows_per_block);
+  constexpr int U = 4;
+  for (long long rb = r_begin + rg; rb < r_end; rb += U * kRowGroups) {
+    f32x4 gv[U], yv[U], y2v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = min(rb + u * kRowGroups, r_end - 1);
+      const long long off = row * C + 4 * c4;
+      gv[u] = ld4(g + off);
+      if (HAS_OUT) {
+        const f32x4 ov = ld4(out + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gv[u][j] = ov[j] > 0.f ? gv[u][j] : 0.f;
+      }
+      yv[u] = ld4(y + off);
+      if (TWO) y2v[u] = ld4(y2 + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = rb + u * kRowGroups;
+      if (row < r_end) {
+        const long long off = row * C + 4 * c4;
+        st4(dy + off, ca * gv[u] - cm - cb * (yv[u] - mu));
+        if (TWO) st4(dy2 + off, ca2 * gv[u] - cm2 - cb2 * (y2v[u] - mu2));
+        if (DRES) st4(dres + off, gv[u]);
+      }
+    }
   }
 }
 
@@ -565,7 +670,9 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
   if (!ws || ws_bytes < tspm_bn_bwd_workspace(m, c)) return TSPM_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int G = row_blocks(m, c);
+  // the merged path (no dy_t) keeps the partial tiles few enough for every apply workgroup to
+  // merge them in its prologue; the transposed-copy path keeps the separate final pass
+  const int G = dy_t ? row_blocks(m, c) : std::min(row_blocks(m, c), kMergeTiles);
   const long long rpb = cdiv64(m, G);
   const int Greal = (int)cdiv64(m, rpb);
   float* part = static_cast<float*>(ws);
@@ -579,11 +686,31 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   else { if (two) BNB_P(false, true); else BNB_P(false, false); }
 #undef BNB_P
   TSPM_LAUNCH_CHECK();
+  const bool dr = dres != nullptr;
+  if (!dy_t) {
+    if (dy2_t) return TSPM_ERR_INVALID;
+    const int cblk = cdiv(c, kChanPerBlock);
+    long long rb = cdiv64(m, std::max(1, 512 / cblk));  // ~512 workgroups, >= 64 rows each
+    if (rb < 64) rb = 64;
+    const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
+#define BNB_M(HO, TW, DR)                                                                                       \
+  hipLaunchKernelGGL((k_bn_bwd_apply_m<HO, TW, DR>), agrid, dim3(256), 0, st, (long long)m, c, Greal, part, invstd, \
+                     gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, g, out, y, mean, y2, mean2, rb, dy, dy2, dres)
+    if (ho) {
+      if (two) { if (dr) BNB_M(true, true, true); else BNB_M(true, true, false); }
+      else { if (dr) BNB_M(true, false, true); else BNB_M(true, false, false); }
+    } else {
+      if (two) { if (dr) BNB_M(false, true, true); else BNB_M(false, true, false); }
+      else { if (dr) BNB_M(false, false, true); else BNB_M(false, false, false); }
+    }
+#undef BNB_M
+    TSPM_LAUNCH_CHECK();
+    return TSPM_OK;
+  }
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 8)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
                      invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, coef);
   TSPM_LAUNCH_CHECK();
-  const bool dr = dres != nullptr;
-  if (dy_t) {
+  {
     if (!t_ok(m, dy_t, ld_t) || (two && dy2_t && !t_ok(m, dy2_t, ld_t)) || (!two && dy2_t)) return TSPM_ERR_INVALID;
     const dim3 tgrid((unsigned)cdiv64(m, 64), cdiv(c, 64));
 #define BNB_AT(HO, TW, DR)                                                                                  \
@@ -600,20 +727,5 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
     TSPM_LAUNCH_CHECK();
     return TSPM_OK;
   }
-  if (dy2_t) return TSPM_ERR_INVALID;
-  const long long n4 = (long long)m * c / 4;
-  const int nb = ew_blocks(n4);
-#define BNB_A(HO, TW, DR)                                                                                          \
-  hipLaunchKernelGGL((k_bn_bwd_apply<HO, TW, DR>), dim3(nb), dim3(256), 0, st, n4, c, g, out, y, mean, y2, mean2, \
-                     coef, dy, dy2, dres)
-  if (ho) {
-    if (two) { if (dr) BNB_A(true, true, true); else BNB_A(true, true, false); }
-    else { if (dr) BNB_A(true, false, true); else BNB_A(true, false, false); }
-  } else {
-    if (two) { if (dr) BNB_A(false, true, true); else BNB_A(false, true, false); }
-    else { if (dr) BNB_A(false, false, true); else BNB_A(false, false, false); }
-  }
-#undef BNB_A
-  TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

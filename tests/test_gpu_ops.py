@@ -550,7 +550,10 @@ def test_wgrad_split_counters_rearm(gpu):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_bn_transposed_copies(gpu, m, c, mode):
     """The tiled kernels that also write transposed copies (the tspm_conv_wgrad_t operand layout)
-    give bitwise the same HWNC outputs as the plain kernels, and the copies are exact transposes."""
+    give the same HWNC outputs as the plain kernels (forward bitwise; backward within 1e-6: the
+    plain path merges its <= 64 partial tiles inside the apply kernel, the transposed path keeps the
+    separate final pass over more tiles, so the per-channel sums are added in a different fixed
+    order), and the copies are exact transposes."""
     from tspm_amd import _lib as L
     lib = L.lib()
     g = torch.Generator().manual_seed(8)
@@ -596,7 +599,7 @@ def test_bn_transposed_copies(gpu, m, c, mode):
     assert torch.equal(ot[:, :m], o1.t())
     for u, v in zip(a, b):
         if u is not None:
-            assert torch.equal(u, v)
+            assert torch.allclose(u, v, rtol=1e-6, atol=1e-6 * float(v.abs().max()))
     assert torch.equal(dyt[:, :m], b[0].t())
     if two:
         assert torch.equal(dy2t[:, :m], b[1].t())
