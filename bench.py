@@ -1,8 +1,9 @@
 """Benchmark: samples/sec (node) of the AVMNIST late-fusion train step on 1..8 MI355X.
 
 One rank per GPU (torchrun env).  Per rank: batch 128 (BASELINE.json configs[2]: global 1024 on 8
-GPUs), synthetic AVMNIST-shaped inputs already resident in HBM, random-init weights (seed 0).  A
-"step" = one fused train step: H2D-free batch copy into the static buffers → ResNet18(audio) ‖
+GPUs), a synthetic AVMNIST-shaped corpus resident in HBM, random-init weights (seed 0).  A
+"step" = batch assembly on device (tspm_avmnist_gather from the corpus into the step's static
+buffers: the reference's __getitem__/collate_fn/H2D) → ResNet18(audio) ‖
 ResNet34(image) forward → fusion head → cross-entropy → backward → [RCCL all-reduce] → Adam,
 all in fp32 on the libtspm HIP kernels (graph-replayed).
 
@@ -32,18 +33,25 @@ METRIC = "samples/sec (node) AVMNIST late-fusion train step at 1/2/4/8 MI355X"
 PER_RANK_BATCH = 128
 
 
-def synthetic_device_batches(k: int, batch: int, seed: int, dev):
-    """k distinct synthetic batches (BASELINE.md 'Synthetic inputs'), resident in HBM."""
-    sys.path.insert(0, REPO)
-    from oracle.avmnist_ref import synthetic_batch  # same generator the parity tests use (data only)
-    import numpy as np
-    lut = torch.from_numpy(np.frombuffer(open(os.path.join(REPO, "tests/golden/lut_gist_earth_L.bin"), "rb").read(),
-                                         dtype=np.uint8).copy())
-    out = []
-    for i in range(k):
-        a, im, lab, _ = synthetic_batch(batch, seed=seed + 7919 * i, lut=lut)
-        out.append((a.to(dev), im.to(dev), lab.to(dev)))
-    return out
+def corpus_loader(step, batch: int, seed: int, dev, n_corpus: int):
+    """The input stage: a synthetic AVMNIST corpus (SURVEY.md §8(d) distributions; no dataset download
+    here) resident in HBM, read in shuffled epochs by data.DeviceLoader — one tspm_avmnist_gather
+    launch per step (index gather + colormap LUT + 1/255 + pattern masks + labels) writing straight
+    into the fused step's static input buffers."""
+    from tspm_amd.data import AVMNIST, synthetic_corpus
+    ds = AVMNIST(None, "train", "multimodal", selected_patterns=["ai"], corpus=synthetic_corpus(n_corpus, seed),
+                 device=dev)
+    ds.device_corpus  # upload once, outside the timed region
+    loader = ds.device_loader(batch, shuffle=True, drop_last=True, generator=torch.Generator().manual_seed(seed),
+                              out=(step.A, step.I, step.labels))
+
+    def batches():
+        epoch = 0
+        while True:
+            loader.set_epoch(epoch)
+            yield from loader
+            epoch += 1
+    return batches()
 
 
 class ConvTimer:
@@ -96,6 +104,107 @@ def cpu_baseline(batch: int, budget_s: float = 15.0):
                       f"{el:.1f}s, torch.set_num_threads({threads})"}
 
 
+INPUT_BYTES_PER_SAMPLE = (12032 + 784 + 8 + 8 + 8) + (12032 + 3136 + 8)  # reads (audio, image u8, label,
+# index, 2 masks) + writes (audio, image f32, label) of tspm_avmnist_gather, per sample
+
+
+def input_stage_bench(args) -> None:
+    """--input-stage: the AVMNIST input stage alone.  Reports samples/s of
+    (a) the drop-in path (torch DataLoader → AVMNIST.__getitems__ → collate_fn: one pinned ≈2 KB H2D
+    + one gather launch per batch, Python included), (b) DeviceLoader epochs, with the gather kernel's
+    HBM roofline at batch 128 and 1024, and a CPU baseline: the reference's per-sample host path
+    (torch.load + cm.gist_earth + PIL + stack + .to(device)) restated in oracle/avmnist_data_ref.py."""
+    import tempfile
+    from tspm_amd.data import AVMNIST, synthetic_corpus
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n = args.corpus_input
+    t0 = time.perf_counter()
+    corpus = synthetic_corpus(n, 1234)
+    ds = AVMNIST(None, "valid", "multimodal", selected_patterns=["ai", "a", "i"], corpus=corpus, device=dev)
+    dc = ds.device_corpus
+    torch.cuda.synchronize()
+    upload_s = time.perf_counter() - t0
+    res = {"metric": "samples/sec AVMNIST input stage (batch assembly into HBM)", "unit": "samples/sec",
+           "corpus_samples": n, "corpus_bytes_hbm": n * (12032 + 784 + 8),
+           "corpus_build_and_upload_s": round(upload_s, 2)}
+    kern = {}
+    for B in (128, 1024):
+        idx = torch.randint(0, n, (B,), device=dev)
+        am = torch.ones(B, device=dev)
+        im = torch.ones(B, device=dev)
+        out = (torch.empty(B, 32, 94, device=dev), torch.empty(B, 1, 28, 28, device=dev),
+               torch.empty(B, dtype=torch.int64, device=dev))
+        for _ in range(20):
+            dc.gather(idx, am, im, out=out)
+        # device time per launch: R launches captured in one HIP graph, replayed (the host-side
+        # ctypes launch path, ~9 us per call, would otherwise be what is measured)
+        R = 100
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(R):
+                dc.gather(idx, am, im, out=out)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(5):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (5 * R)
+        gbs = INPUT_BYTES_PER_SAMPLE * B / (us * 1e-6) / 1e9
+        kern[B] = {"us_per_launch": round(us, 3), "achieved_GBps": round(gbs, 1), "samples_per_s": round(B / us * 1e6)}
+    res["gather_kernel"] = kern
+    # (a) drop-in DataLoader path
+    B = 128
+    dl = torch.utils.data.DataLoader(ds, batch_size=B, shuffle=True, collate_fn=ds.collate_fn)
+    it = iter(dl)
+    for _ in range(5):
+        next(it)
+    torch.cuda.synchronize()
+    K = 200
+    t0 = time.perf_counter()
+    for _ in range(K):
+        next(it)
+    torch.cuda.synchronize()
+    res["dataloader_dropin_samples_per_s"] = round(K * B / (time.perf_counter() - t0))
+    # (b) DeviceLoader: one epoch over the 3-pattern valid split (3n items), epoch setup included
+    dv = ds.device_loader(B, shuffle=True)
+    t0 = time.perf_counter()
+    cnt = 0
+    for b in dv:
+        cnt += b["labels"].numel()
+    torch.cuda.synchronize()
+    res["device_loader_epoch_samples_per_s"] = round(cnt / (time.perf_counter() - t0))
+    res["value"] = res["dataloader_dropin_samples_per_s"]
+    k = kern[128]
+    res["roofline"] = {"bound": "hbm", "kernel": "k_avmnist_gather", "achieved": k["achieved_GBps"], "peak": 8000.0,
+                       "unit": "GB/s", "frac": round(k["achieved_GBps"] / 8000.0, 4), "traffic": None,
+                       "bytes_per_sample": INPUT_BYTES_PER_SAMPLE, "batch": 128}
+    # CPU baseline: the reference's host path on a bounded sample of files
+    from oracle import avmnist_data_ref as dref
+    torch.set_num_threads(1)
+    root = tempfile.mkdtemp(prefix="tspm_ref_corpus_")
+    m = args.cpu_input_samples
+    small = corpus.subset(range(m))
+    csv = dref.write_reference_files(root, small.audio, small.image, small.labels)
+    for _ in dref.reference_host_batches(csv, B, dev):  # warm-up: matplotlib / PIL / file cache
+        break
+    t0 = time.perf_counter()
+    cnt = 0
+    for b in dref.reference_host_batches(csv, B, dev):
+        cnt += b["labels"].numel()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": round(cnt / el, 1), "unit": "samples/sec", "cores": 1, "kind": "port",
+                           "sample": f"{cnt} samples in the reference file layout through the reference's "
+                                     f"per-sample host path (torch.load x2, cm.gist_earth, PIL convert L, "
+                                     f"ToDtype scale, mask, stack, .to(cuda)), batch {B}, 1 thread, {el:.1f}s"}
+    print(json.dumps(res), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,9 +214,16 @@ def main() -> None:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--corpus", type=int, default=16384, help="samples in the HBM-resident synthetic corpus")
     ap.add_argument("--phased", action="store_true",
                     help="at N=1, run the DP step path anyway (1-rank RCCL group, all-reduce = identity)")
+    ap.add_argument("--input-stage", action="store_true", help="benchmark the input stage alone (one JSON line)")
+    ap.add_argument("--corpus-input", type=int, default=60000, help="--input-stage corpus size (AVMNIST train: 60k)")
+    ap.add_argument("--cpu-input-samples", type=int, default=16384)
     args = ap.parse_args()
+    if args.input_stage:
+        input_stage_bench(args)
+        return
 
     import tspm_amd
     from tspm_amd import ddp
@@ -132,11 +248,10 @@ def main() -> None:
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
         step.allreduce = step.phased_allreduce(force=os.environ.get("TSPM_PHASED_FORCE", "1") == "1")
-    batches = synthetic_device_batches(4, B, 1234 + rank, dev)
+    feed = corpus_loader(step, B, 1234 + rank, dev, args.corpus)
 
     def one(i):
-        a, im, lab = batches[i % len(batches)]
-        step.load_batch(a, im, lab)
+        next(feed)  # gathers the next shuffled batch into step.A / step.I / step.labels
         step.run()
 
     for i in range(args.warmup):
@@ -170,9 +285,7 @@ def main() -> None:
     saved_ar = step.allreduce
     step.serial = True  # one stream: each conv's event pair brackets that kernel alone
     step.allreduce = None  # (the instrumented step is not part of the timed region)
-    a, im, lab = batches[0]
-    step.load_batch(a, im, lab)
-    step.run()
+    step.run()  # on the last gathered batch
     step.use_graph = saved
     step.serial = saved_serial
     step.allreduce = saved_ar
@@ -191,8 +304,9 @@ def main() -> None:
             "metric": METRIC, "value": round(value, 2), "unit": "samples/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic AVMNIST-shaped batches resident in HBM (audio [B,32,94] log-uniform-ish, "
-                    "image uint8->LUT [B,1,28,28]), random-init weights (seed 0)",
+            "data": f"synthetic AVMNIST-shaped corpus of {args.corpus} samples resident in HBM (audio f32 [32,94] "
+                    "log-normal-ish, image uint8 [28,28]); each step gathers a shuffled batch on device "
+                    "(colormap LUT, 1/255, masks) into the step's inputs; random-init weights (seed 0)",
             "config": {"workload": "avmnist_late_fusion_train_step(resnet18_audio+resnet34_image+mlp_head, CE, Adam)",
                        "per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},

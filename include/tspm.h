@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 6 */
+int tspm_abi_version(void);  /* 7 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -261,6 +261,21 @@ int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_av
  * ----------------------------------------------------------------------------------------------*/
 /* image_f32[i] = lut[u8[i]] * (1/255)  (gist_earth→L colormap LUT, torchvision ToDtype(scale)). */
 int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* lut, float* out, tspm_stream_t stream);
+/* Batch assembly from an HBM-resident AVMNIST corpus (replaces, per batch, AVMNIST.__getitem__ +
+ * _load_audio/_load_image + get_samples + collate_fn: MML_Suite/data/avmnist.py:164-224,248-277,
+ * data/base_dataset.py:61-74).  For r < count, s = index[r]:
+ *   audio_out[r,:]  = audio[s,:] * audio_mask[r]                       (audio_elems floats/row)
+ *   image_out[r,:]  = (float)lut[image[s,:]] * fp32(1/255) * image_mask[r]  (image_elems bytes/row)
+ *   labels_out[r]   = labels[s]
+ * A null mask means "no multiply"; a null lut means the identity map; a null output skips that
+ * modality (target_modality audio / image only).  An index outside [0, n_samples) writes NaN rows
+ * and label -1 (tspm_cross_entropy then yields NaN) instead of reading out of bounds.
+ * Fast path (16-byte audio, 4-byte image accesses) when both element counts are multiples of 4 and
+ * audio/audio_out/image_out are 16-byte and image/lut 4-byte aligned; otherwise per element. */
+int tspm_avmnist_gather(int64_t count, const int64_t* index, int64_t n_samples, const float* audio,
+                        int32_t audio_elems, const uint8_t* image, int32_t image_elems, const int64_t* labels,
+                        const uint8_t* lut, const float* audio_mask, const float* image_mask, float* audio_out,
+                        float* image_out, int64_t* labels_out, tspm_stream_t stream);
 /* Sum `nslab` slabs of `count` floats (slab_stride apart) into out (deterministic slab order). */
 int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs, float* out,
                       tspm_stream_t stream);

@@ -17,9 +17,9 @@ from .engine import EncoderEngine, prepare_encoder_layout
 from .modules import AVMNIST, BasicBlock, ResNet18, ResNet34, ResNetEncoder, modality_key
 from .optim import FusedAdam
 from .step import FusedTrainStep
-from . import plugin, ddp
+from . import plugin, ddp, data
 
 __all__ = ["AVMNIST", "BasicBlock", "ResNet18", "ResNet34", "ResNetEncoder", "FusedAdam", "FusedTrainStep",
-           "EncoderEngine", "prepare_encoder_layout", "TspmError", "TspmLibraryError", "plugin", "ddp",
+           "EncoderEngine", "prepare_encoder_layout", "TspmError", "TspmLibraryError", "plugin", "ddp", "data",
            "modality_key"]
 __version__ = "0.1.0"

@@ -157,14 +157,16 @@ __global__ __launch_bounds__(256) void k_cross_entropy(int N, int K, const float
     float se = 0.f;
     for (int k = 0; k < K; ++k) se += expf(z[k] - mx);
     const float lse = logf(se);
-    const int lab = (int)labels[n];
-    lsum += (double)(lse - (z[lab] - mx));
+    const long long lab64 = labels[n];
+    const bool lok = lab64 >= 0 && lab64 < K;  // out-of-range label: NaN loss/grad, no OOB read
+    const int lab = lok ? (int)lab64 : 0;
+    lsum += lok ? (double)(lse - (z[lab] - mx)) : (double)__builtin_nanf("");
     correct += (am == lab) ? 1 : 0;
     if (dlogits) {
       float* d = dlogits + (long long)n * K;
       for (int k = 0; k < K; ++k) {
         const float pk = expf(z[k] - mx) / se;
-        d[k] = (pk - (k == lab ? 1.f : 0.f)) * invn * gscale;
+        d[k] = lok ? (pk - (k == lab ? 1.f : 0.f)) * invn * gscale : __builtin_nanf("");
       }
     }
   }
@@ -330,7 +332,7 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
-extern "C" int tspm_abi_version(void) { return 6; }
+extern "C" int tspm_abi_version(void) { return 7; }
 
 extern "C" const char* tspm_status_string(int status) {
   switch (status) {

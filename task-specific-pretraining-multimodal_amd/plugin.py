@@ -5,7 +5,8 @@ The reference builds models through two seams:
      ``cls(**mapping)`` while the config is parsed (MML_Suite/config/yaml_constructors.py:37-43,
      159-178: ``!ResNet18``, ``!ResNet34``, ``!ResNetEncoder``).
   2. Name resolvers — ``resolve_model_name("AVMNIST")`` (config/resolvers.py:18-23),
-     ``resolve_encoder`` (:93-122) and ``resolve_optimizer("Adam")`` (:125-156).
+     ``resolve_encoder`` (:93-122), ``resolve_optimizer("Adam")`` (:125-156) and
+     ``resolve_dataset_name("AVMNIST")`` (:192-220, called by config/data_config.py:134).
 
 ``register()`` overrides the tags on the given loader (default ``yaml.SafeLoader``) and, when the
 reference's ``config.resolvers`` module is importable in the process, wraps the resolvers so the
@@ -17,6 +18,7 @@ from __future__ import annotations
 import sys
 from typing import Dict, Optional
 
+from . import data
 from .modules import AVMNIST, ResNet18, ResNet34, ResNetEncoder
 from .optim import FusedAdam
 
@@ -24,6 +26,7 @@ TAGS = {"!ResNet18": ResNet18, "!ResNet34": ResNet34, "!ResNetEncoder": ResNetEn
 MODELS = {"avmnist": AVMNIST}
 ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder}
 OPTIMIZERS = {"adam": FusedAdam}
+DATASETS = {"avmnist": data.AVMNIST}
 
 
 def _ctor(cls):
@@ -55,12 +58,13 @@ def _wrap(orig, table: Dict[str, object]):
 
 
 def register_resolvers(resolvers_module: Optional[object] = None, rebind_everywhere: bool = True) -> bool:
-    """Wrap resolve_model_name / resolve_encoder / resolve_optimizer of the reference's
+    """Wrap resolve_model_name / resolve_encoder / resolve_optimizer / resolve_dataset_name of the reference's
     ``config.resolvers`` (if loaded) and every module that imported them by name."""
     mod = resolvers_module or sys.modules.get("config.resolvers")
     if mod is None:
         return False
-    pairs = [("resolve_model_name", MODELS), ("resolve_encoder", ENCODERS), ("resolve_optimizer", OPTIMIZERS)]
+    pairs = [("resolve_model_name", MODELS), ("resolve_encoder", ENCODERS), ("resolve_optimizer", OPTIMIZERS),
+             ("resolve_dataset_name", DATASETS)]
     for name, table in pairs:
         orig = getattr(mod, name, None)
         if orig is None:

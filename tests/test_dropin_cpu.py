@@ -87,6 +87,7 @@ def test_resolver_rebinding_falls_through():
     mod.resolve_model_name = lambda name: ("orig", name)
     mod.resolve_encoder = lambda name: ("orig", name)
     mod.resolve_optimizer = lambda name: ("orig", name)
+    mod.resolve_dataset_name = lambda name: ("orig", name)
     user = types.ModuleType("fake_user")
     user.resolve_optimizer = mod.resolve_optimizer
     sys.modules["fake_user"] = user
@@ -96,6 +97,8 @@ def test_resolver_rebinding_falls_through():
         assert mod.resolve_encoder("ResNet34") is tspm_amd.ResNet34
         assert mod.resolve_optimizer("Adam") is tspm_amd.FusedAdam
         assert mod.resolve_optimizer("sgd") == ("orig", "sgd")
+        assert mod.resolve_dataset_name("AVMNIST") is tspm_amd.data.AVMNIST
+        assert mod.resolve_dataset_name("mosi") == ("orig", "mosi")
         assert user.resolve_optimizer is mod.resolve_optimizer  # imported-by-name copies rebound too
         tspm_amd.plugin.register_resolvers(mod)  # idempotent
         assert mod.resolve_model_name("mosi") == ("orig", "mosi")
