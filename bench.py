@@ -82,6 +82,22 @@ class ConvTimer:
         return len(self.events), flops, tot_ms
 
 
+def pmc_traffic(family: str = "conv"):
+    """HBM bytes per step of one kernel family from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.sh + pmc_traffic.py: FETCH_SIZE and
+    WRITE_SIZE passes over this same bench command, gfx950 read correction applied).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
+    if not files:
+        return None, None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    fam = d.get("per_step_bytes", {}).get(family)
+    if not fam:
+        return None, None, None
+    return fam["total"], fam.get("launches"), os.path.relpath(files[-1], REPO)
+
+
 def cpu_baseline(batch: int, budget_s: float = 15.0):
     """Time the oracle's CPU train step (reference-equivalent) on this host's cores."""
     from oracle import avmnist_ref as orc
@@ -297,6 +313,7 @@ def main() -> None:
     nominal, valid = step_flops_per_sample()
     step_tflops = valid * B * world / (elapsed / args.steps) / 1e12 / world
 
+    traffic, traffic_launches, traffic_src = pmc_traffic("conv")
     loss = step.loss.item()
     result = None
     if rank == 0:
@@ -313,7 +330,10 @@ def main() -> None:
             "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_conv_fwd_vec/gather, k_conv_dgrad, "
                                                     "k_conv_wgrad), fp32 MFMA 32x32x2",
                          "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per step of the conv family (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_per_launch": round(traffic / traffic_launches) if traffic else None,
+                         "traffic_source": traffic_src,
                          "launches_per_step": n_launch, "conv_ms_per_step": round(conv_ms, 4),
                          "valid_tap_flop_per_step": conv_flops,
                          "step_valid_tflops_per_gpu": round(step_tflops, 3),
