@@ -197,7 +197,8 @@ def input_stage_bench(args) -> None:
     res["value"] = res["dataloader_dropin_samples_per_s"]
     k = kern[128]
     res["roofline"] = {"bound": "hbm", "kernel": "k_avmnist_gather", "achieved": k["achieved_GBps"], "peak": 8000.0,
-                       "unit": "GB/s", "frac": round(k["achieved_GBps"] / 8000.0, 4), "traffic": None,
+                       "unit": "GB/s", "frac": round(k["achieved_GBps"] / 8000.0, 4),
+                       "traffic": pmc_traffic("gather")[0], "traffic_unit": "HBM bytes per 128-sample launch (PMC)",
                        "bytes_per_sample": INPUT_BYTES_PER_SAMPLE, "batch": 128}
     # CPU baseline: the reference's host path on a bounded sample of files
     from oracle import avmnist_data_ref as dref
@@ -221,6 +222,97 @@ def input_stage_bench(args) -> None:
     print(json.dumps(res), flush=True)
 
 
+def eval_bench(args) -> None:
+    """--eval: the evaluation path on one GPU — validation_step as one
+    FusedEvalStep graph per batch (eval forward of both encoders, head, CE, on-device prediction /
+    confusion / loss bookkeeping) fed by the device gather, over an AVMNIST-validation-sized corpus
+    with the 3 missing-data patterns; plus whole epochs through harness.EpochRunner (validation with
+    the YAML's 12 metrics, and a training epoch) and a CPU baseline: the oracle's validation_step."""
+    import tspm_amd
+    from tspm_amd.data import AVMNIST, synthetic_corpus
+    from tspm_amd.harness import EpochRunner
+    from tspm_amd.metrics import ClassificationLog
+    from tspm_amd.roofline import FP32_MFMA_PEAK_TFLOPS, eval_flops_per_sample
+    from tspm_amd.step import FusedEvalStep
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B = args.batch_per_rank
+    torch.manual_seed(0)
+    model = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
+    ds = AVMNIST(None, "valid", "multimodal", selected_patterns=["ai", "a", "i"],
+                 corpus=synthetic_corpus(args.eval_corpus, 4321), device=dev)
+    log = ClassificationLog(dev)
+    st = FusedEvalStep(model, None, B, log)
+    loader = ds.device_loader(B, shuffle=True, drop_last=True, generator=torch.Generator().manual_seed(0),
+                              out=(st.A, st.I, st.labels))
+
+    def feed():
+        while True:
+            for b in loader:
+                st.groups.copy_(b["pattern_ids"], non_blocking=True)
+                yield b
+    f = feed()
+    for _ in range(args.warmup):
+        next(f)
+        st.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        next(f)
+        st.run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    value = args.steps * B / el
+    nom, valid = eval_flops_per_sample()
+    tflops = valid * value / 1e12
+    res = {"metric": "samples/sec AVMNIST validation step (eval fwd + CE + on-device metrics), 1 MI355X",
+           "value": round(value, 1), "unit": "samples/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "dtype": "fp32",
+           "data": f"synthetic AVMNIST-shaped validation corpus of {args.eval_corpus} samples x 3 patterns in HBM",
+           "config": {"workload": "avmnist_validation_step(resnet18_audio+resnet34_image+mlp_head, CE, metrics)",
+                      "batch": B},
+           "roofline": {"bound": "mfma", "kernel": "whole eval step (conv family dominant)",
+                        "achieved": round(tflops, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(tflops / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                        "valid_tap_flop_per_sample": valid}}
+    # whole epochs through the harness (metrics computed at the end of each)
+    opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
+    runner = EpochRunner(model, opt, None)
+    vl = ds.device_loader(B)
+    runner.validate_epoch(vl)  # capture
+    t0 = time.perf_counter()
+    _, _, metrics, nb = runner.validate_epoch(vl)
+    el = time.perf_counter() - t0
+    res["validate_epoch"] = {"samples": len(ds), "batches": nb, "seconds": round(el, 4),
+                             "samples_per_s": round(len(ds) / el, 1), "accuracy_AI": float(metrics["accuracy_AI"])}
+    tr = AVMNIST(None, "train", "multimodal", selected_patterns=["ai"], corpus=synthetic_corpus(args.eval_corpus, 99),
+                 device=dev)
+    tl = tr.device_loader(B, shuffle=True, drop_last=True)
+    runner.train_epoch(tl)
+    t0 = time.perf_counter()
+    _, _, _, nb = runner.train_epoch(tl)
+    el = time.perf_counter() - t0
+    res["train_epoch"] = {"samples": nb * B, "batches": nb, "seconds": round(el, 4),
+                          "samples_per_s": round(nb * B / el, 1)}
+    if not args.no_cpu_baseline:
+        from oracle import avmnist_eval_ref as eref
+        from oracle import avmnist_ref as orc
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        ref = orc.build_oracle_avmnist(0)
+        audio, image, labels, _ = orc.synthetic_batch(B, seed=1234)
+        eref.validation_step(ref, audio, image, labels)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_budget and n < 400:
+            eref.validation_step(ref, audio, image, labels)
+            n += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n * B / el, 1), "unit": "samples/sec", "cores": threads, "kind": "port",
+                               "sample": f"{n} oracle validation steps (eval fwd + CE + softmax argmax) at batch {B}, "
+                                         f"{el:.1f}s, torch.set_num_threads({threads})"}
+    print(json.dumps(res), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -236,9 +328,14 @@ def main() -> None:
     ap.add_argument("--input-stage", action="store_true", help="benchmark the input stage alone (one JSON line)")
     ap.add_argument("--corpus-input", type=int, default=60000, help="--input-stage corpus size (AVMNIST train: 60k)")
     ap.add_argument("--cpu-input-samples", type=int, default=16384)
+    ap.add_argument("--eval", action="store_true", help="benchmark the evaluation path / epoch harness (one JSON line)")
+    ap.add_argument("--eval-corpus", type=int, default=10000, help="--eval validation corpus (x3 patterns)")
     args = ap.parse_args()
     if args.input_stage:
         input_stage_bench(args)
+        return
+    if args.eval:
+        eval_bench(args)
         return
 
     import tspm_amd

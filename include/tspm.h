@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 7 */
+int tspm_abi_version(void);  /* 8 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -234,7 +234,8 @@ int tspm_dropout_mask(int64_t count, float p, uint64_t seed, const uint64_t* cou
  * Loss — LossFunctionGroup{cross_entropy: 1.0} (experiment_utils/loss.py:123-148,
  * models/avmnist.py:301) + on-device accuracy counters (avmnist.py:305-309)
  * ----------------------------------------------------------------------------------------------*/
-/* loss[0] = mean_i CE(logits_i, labels_i); dlogits = (softmax - onehot)/n * grad_scale;
+/* loss[0] = grad_scale * mean_i CE(logits_i, labels_i) (the group's total: weight × CE, grad_scale =
+ * the term's weight); dlogits = (softmax - onehot)/n * grad_scale;
  * if stats != NULL: stats[0] += loss*n, stats[1] += #correct (argmax == label), stats[2] += n. */
 int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const int64_t* labels, float* loss,
                        float* dlogits, float grad_scale, float* stats, tspm_stream_t stream);
@@ -276,6 +277,19 @@ int tspm_avmnist_gather(int64_t count, const int64_t* index, int64_t n_samples, 
                         int32_t audio_elems, const uint8_t* image, int32_t image_elems, const int64_t* labels,
                         const uint8_t* lut, const float* audio_mask, const float* image_mask, float* audio_out,
                         float* image_out, int64_t* labels_out, tspm_stream_t stream);
+/* Classification bookkeeping for one batch, on device (replaces the per-batch softmax → argmax →
+ * .cpu() → MetricRecorder.update_group_all of models/avmnist.py:305-309,345-350 and
+ * experiment_utils/metric_recorder.py:96-145, and the epoch loops' per-batch loss lists,
+ * train_multimodal.py:478-491,525-541).  For r < n:
+ *   pred = first argmax of softmax(logits[r,:classes]);  pred_out[r] = pred  (if pred_out)
+ *   confusion[g][labels[r]][pred] += 1  with g = groups ? groups[r] : 0  (int64 counts,
+ *   [n_groups][classes][classes]; rows whose label or group is out of range are not counted)
+ * and once per call, when counters is given: loss_log[counters[0]] = *loss (if loss_log and
+ * counters[0] < log_capacity), counters[0] += 1, counters[1] += n.  Graph-capturable. */
+int tspm_classify_update(int32_t n, int32_t classes, const float* logits, const int64_t* labels,
+                         const int32_t* groups, int32_t n_groups, int64_t* confusion, int64_t* pred_out,
+                         const float* loss, float* loss_log, int64_t* counters, int64_t log_capacity,
+                         tspm_stream_t stream);
 /* Sum `nslab` slabs of `count` floats (slab_stride apart) into out (deterministic slab order). */
 int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs, float* out,
                       tspm_stream_t stream);

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void k_cross_entropy(int N, int K, const float
   }
   if (threadIdx.x == 0) {
     const float l = (float)(sl[0] / (double)N);
-    if (loss) loss[0] = l;
+    if (loss) loss[0] = l * gscale;  // LossFunctionGroup total = weight * CE (weight 1.0: exact)
     if (stats) {
       stats[0] += (float)sl[0];
       stats[1] += (float)sc[0];
@@ -332,7 +332,7 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
-extern "C" int tspm_abi_version(void) { return 7; }
+extern "C" int tspm_abi_version(void) { return 8; }
 
 extern "C" const char* tspm_status_string(int status) {
   switch (status) {

@@ -306,12 +306,12 @@ class _Staging:
         self.device, self.slots, self.k = device, slots, 0
         self.bufs: Dict[int, List[Tuple[torch.Tensor, torch.Tensor, torch.cuda.Event]]] = {}
 
-    def upload(self, index: np.ndarray, am: np.ndarray, im: np.ndarray):
+    def upload(self, index: np.ndarray, am: np.ndarray, im: np.ndarray, pid: np.ndarray):
         b = index.shape[0]
         ring = self.bufs.get(b)
         if ring is None:
-            ring = [(torch.empty(16 * b, dtype=torch.uint8).pin_memory(),
-                     torch.empty(16 * b, dtype=torch.uint8, device=self.device), torch.cuda.Event())
+            ring = [(torch.empty(20 * b, dtype=torch.uint8).pin_memory(),
+                     torch.empty(20 * b, dtype=torch.uint8, device=self.device), torch.cuda.Event())
                     for _ in range(self.slots)]
             self.bufs[b] = ring
         host, dev, ev = ring[self.k % self.slots]
@@ -319,10 +319,12 @@ class _Staging:
         ev.synchronize()  # the previous upload from this slot has left the host buffer
         host[:8 * b].view(torch.int64).numpy()[:] = index
         host[8 * b:12 * b].view(torch.float32).numpy()[:] = am
-        host[12 * b:].view(torch.float32).numpy()[:] = im
+        host[12 * b:16 * b].view(torch.float32).numpy()[:] = im
+        host[16 * b:].view(torch.int32).numpy()[:] = pid
         dev.copy_(host, non_blocking=True)
         ev.record()
-        return dev[:8 * b].view(torch.int64), dev[8 * b:12 * b].view(torch.float32), dev[12 * b:].view(torch.float32)
+        return (dev[:8 * b].view(torch.int64), dev[8 * b:12 * b].view(torch.float32),
+                dev[12 * b:16 * b].view(torch.float32), dev[16 * b:].view(torch.int32))
 
 
 class AVMNIST(torch.utils.data.Dataset):
@@ -425,6 +427,12 @@ class AVMNIST(torch.utils.data.Dataset):
         """data/avmnist.py:152-162."""
         return self.num_samples if self.split == "train" else self.num_samples * len(self.selected_patterns)
 
+    def pattern_ids(self, names: Sequence[str]) -> np.ndarray:
+        """Index of each pattern name in ``get_all_possible_patterns()`` (["a", "ai", "i"]) — the
+        ``pattern_ids`` batch entry (int32, device) that keys the device-side metrics by pattern."""
+        allp = self.get_all_possible_patterns()
+        return np.fromiter((allp.index(n) for n in names), dtype=np.int32, count=len(names))
+
     def _resolve(self, items: Sequence[int]) -> Tuple[np.ndarray, List[str], np.ndarray, np.ndarray]:
         """data/base_dataset.py:76-92 + 137-150: dataset index → (pattern, sample) and its masks."""
         n, sel = self.num_samples, self.selected_patterns
@@ -462,9 +470,12 @@ class AVMNIST(torch.utils.data.Dataset):
         t = self.target_modality
         return t in ("multimodal", "audio"), t in ("multimodal", "image")
 
-    def _pack(self, a, im, lab, names) -> Dict[Any, Any]:
-        """collate_fn's output dict (data/avmnist.py:258-277)."""
+    def _pack(self, a, im, lab, names, pids=None) -> Dict[Any, Any]:
+        """collate_fn's output dict (data/avmnist.py:258-277), plus ``pattern_ids`` (int32 device
+        tensor, see :meth:`pattern_ids`) for the device-side metrics."""
         out: Dict[Any, Any] = {"labels": lab, "pattern_name": list(names), "missing_masks": {}}
+        if pids is not None:
+            out["pattern_ids"] = pids
         if a is not None:
             out[self.keys["audio"]] = a
         if im is not None:
@@ -478,12 +489,12 @@ class AVMNIST(torch.utils.data.Dataset):
             self._staging = _Staging(dc.device)
         if len(samples) == 0:
             raise ValueError("empty batch")
-        idx_d, am_d, im_d = self._staging.upload(samples, am, im)
+        idx_d, am_d, im_d, pid_d = self._staging.upload(samples, am, im, self.pattern_ids(names))
         wa, wi = self._want()
         a, imt, lab = dc.gather(idx_d, am_d, im_d, want_audio=wa, want_image=wi)
         if names:
             self.current_pattern = names[-1]
-        return self._pack(a, imt, lab, names)
+        return self._pack(a, imt, lab, names, pid_d)
 
     def __getitems__(self, items: Sequence[int]) -> _BatchRequest:
         """torch DataLoader's batched-fetch hook: defer the whole batch to :meth:`collate_fn`."""
@@ -625,9 +636,10 @@ class DeviceLoader:
         idx_d = torch.from_numpy(samples).pin_memory().to(dc.device, non_blocking=True)
         am_d = torch.from_numpy(am).pin_memory().to(dc.device, non_blocking=True)
         im_d = torch.from_numpy(im).pin_memory().to(dc.device, non_blocking=True)
+        pid_d = torch.from_numpy(self.ds.pattern_ids(names)).pin_memory().to(dc.device, non_blocking=True)
         wa, wi = self.ds._want()
         for b in range(nb):
             lo, hi = b * self.batch_size, min(len(order), (b + 1) * self.batch_size)
             out = self.out if (self.out is not None and hi - lo == self.batch_size) else None
             a, imt, lab = dc.gather(idx_d[lo:hi], am_d[lo:hi], im_d[lo:hi], want_audio=wa, want_image=wi, out=out)
-            yield self.ds._pack(a, imt, lab, names[lo:hi])
+            yield self.ds._pack(a, imt, lab, names[lo:hi], pid_d[lo:hi])

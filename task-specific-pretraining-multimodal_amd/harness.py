@@ -1,0 +1,232 @@
+"""Epoch harness: train / validate epochs and the fit loop of MML_Suite/train_multimodal.py on the
+fused HIP steps, with the epoch's bookkeeping on the device.
+
+Reference (``MML_Suite/``):
+  train_epoch            train_multimodal.py:438-491  per batch model.train_step → loss.item(); mean
+  validate_epoch         train_multimodal.py:494-541  per batch model.validation_step → loss.item(); mean
+  check_early_stopping   train_multimodal.py:329-377
+  _train_loop            train_multimodal.py:554-791  epochs: metrics reset → train → calculate_all_groups
+                         → validate → calculate_all_groups → epoch_metrics.json → early stopping →
+                         CheckpointManager.save_checkpoint(epoch_{n}.pth, best.pth) → scheduler.step(val loss)
+  test                   train_multimodal.py:866-917  load best.pth, validate_epoch on each test split
+  CheckpointManager      experiment_utils/checkpoints.py:13-120
+
+What differs is where the per-batch work happens: the reference synchronises on every batch
+(``loss.item()`` and the predictions' ``.cpu()``); here each batch is ONE gather launch
+(data.DeviceLoader writing into the step's static inputs) plus ONE graph replay that also records
+the batch loss and the confusion counts (tspm_classify_update), and the host reads the epoch's
+losses and counts once.  Epoch loss = ``np.mean`` of the per-batch fp32 losses as Python floats, as
+the reference computes it; metrics via metrics.DeviceMetricRecorder (same keys and values as the
+reference's MetricRecorder).
+"""
+from __future__ import annotations
+
+import json
+import time
+from pathlib import Path
+from typing import Any, Dict, Iterable, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .metrics import ClassificationLog, DeviceMetricRecorder
+from .modules import modality_key
+from .step import FusedEvalStep, FusedTrainStep
+
+# the AVMNIST YAML's metric block (configs/avmnist/centralised/train_avmnist_resnet.yaml:105-166)
+AVMNIST_METRICS = {
+    "metrics": {
+        "accuracy": {"function": "sklearn.metrics.accuracy_score", "kwargs": {}},
+        "balanced_accuracy": {"function": "sklearn.metrics.balanced_accuracy_score", "kwargs": {}},
+        **{f"{m}_{avg}": {"function": f"sklearn.metrics.{fn}", "kwargs": {"average": avg, "zero_division": 0}}
+           for m, fn in (("f1", "f1_score"), ("precision", "precision_score"), ("recall", "recall_score"))
+           for avg in ("macro", "micro", "weighted")},
+        "ConfusionMatrix": {"function": "sklearn.metrics.confusion_matrix", "kwargs": {"labels": list(range(10))}},
+    },
+    "groups": {"classification": ["accuracy", "balanced_accuracy", "f1_macro", "f1_micro", "f1_weighted",
+                                  "precision_macro", "precision_micro", "precision_weighted", "recall_macro",
+                                  "recall_micro", "recall_weighted", "ConfusionMatrix"]},
+}
+
+
+def check_early_stopping(val_metrics: Dict[str, Any], best_metrics: Optional[Dict[str, Any]], patience: int,
+                         min_delta: float, wait: int, mode: str = "minimize",
+                         target_metric: str = "loss") -> Tuple[bool, bool, int]:
+    """train_multimodal.py:329-377: (is_best, should_continue, wait)."""
+    if best_metrics is None:
+        return True, True, 0
+    value, best = val_metrics.get(target_metric), best_metrics.get(target_metric)
+    if value is None or best is None:
+        raise ValueError(f"Metric '{target_metric}' not found in val_metrics or best_metrics.")
+    if (mode == "minimize" and value < best - min_delta) or (mode == "maximize" and value > best + min_delta):
+        return True, True, 0
+    wait += 1
+    return False, wait < patience, wait
+
+
+class CheckpointManager:
+    """experiment_utils/checkpoints.py:13-120 — same files (``epoch_{n}.pth``, ``best.pth``) and dict
+    keys (``model_state_dict``, ``optimizer_state_dict``, ``scheduler_state_dict``); state_dict keys and
+    OIHW shapes are the reference's, so checkpoints load on either side."""
+
+    def __init__(self, model_dir, save_metric: str = "loss", mode: str = "minimize", device: str = "cuda"):
+        self.model_dir = Path(model_dir)
+        self.save_metric, self.mode, self.device = save_metric, mode, device
+        self.best_metric = float("inf") if mode == "minimize" else float("-inf")
+        self.best_epoch = -1
+        self.model_dir.mkdir(parents=True, exist_ok=True)
+
+    def is_better(self, current: float) -> bool:
+        return current < self.best_metric if self.mode == "minimize" else current > self.best_metric
+
+    def save_checkpoint(self, model, optimizer, scheduler, epoch: int, metrics: Dict[str, float],
+                        is_best: bool = False) -> None:
+        state = {"model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict()}
+        if scheduler is not None:
+            state["scheduler_state_dict"] = scheduler.state_dict()
+        torch.save(state, self.model_dir / f"epoch_{epoch}.pth")
+        if is_best:
+            torch.save(state, self.model_dir / "best.pth")
+        value = metrics[self.save_metric]
+        if self.is_better(value):
+            self.best_metric, self.best_epoch = value, epoch
+
+    def load_checkpoint(self, model, optimizer=None, scheduler=None, epoch: Optional[int] = None,
+                        load_best: bool = False) -> Dict[str, Any]:
+        name = "best.pth" if load_best else (f"epoch_{epoch}.pth" if epoch is not None else "last.pth")
+        ck = torch.load(self.model_dir / name, map_location=self.device, weights_only=True)
+        model.load_state_dict(ck["model_state_dict"])
+        if optimizer is not None and "optimizer_state_dict" in ck:
+            optimizer.load_state_dict(ck["optimizer_state_dict"])
+        if scheduler is not None and "scheduler_state_dict" in ck:
+            scheduler.load_state_dict(ck["scheduler_state_dict"])
+        return ck
+
+
+class EpochRunner:
+    """train_epoch / validate_epoch on the fused steps.  ``loader`` yields collate_fn-style batch dicts
+    on the device (data.DeviceLoader / the drop-in DataLoader); batches of the runner's size are fed
+    through the static buffers of one captured graph, a smaller last batch through a second one."""
+
+    def __init__(self, model, optimizer, loss_functions, metric_config=None, device=None, log_capacity: int = 1 << 16):
+        self.model, self.optimizer, self.loss_functions = model, optimizer, loss_functions
+        self.device = device or next(model.parameters()).device
+        self.log = ClassificationLog(self.device, capacity=log_capacity)
+        self.recorder = DeviceMetricRecorder(metric_config or AVMNIST_METRICS, self.log)
+        self.train_steps: Dict[int, FusedTrainStep] = {}
+        self.eval_steps: Dict[int, FusedEvalStep] = {}
+
+    def _train_step(self, n: int) -> FusedTrainStep:
+        st = self.train_steps.get(n)
+        if st is None:
+            st = FusedTrainStep(self.model, self.optimizer, self.loss_functions, n)
+            self.train_steps[n] = st
+        st.log = self.log
+        return st
+
+    def _eval_step(self, n: int) -> FusedEvalStep:
+        st = self.eval_steps.get(n)
+        if st is None:
+            st = FusedEvalStep(self.model, self.loss_functions, n, self.log)
+            self.eval_steps[n] = st
+        st.log = self.log
+        return st
+
+    def _unpack(self, b):
+        a, i = b[modality_key(b, "audio")], b[modality_key(b, "image")]
+        g = b.get("pattern_ids")
+        if g is None:
+            g = self.log.group_ids(b["pattern_name"])
+        return a, i, b["labels"], g
+
+    def _finish(self, t0: float, loss: Optional[float] = None):
+        conf, losses, _ = self.log.fetch()  # the epoch's only host synchronisation
+        mean = ClassificationLog.mean_loss(losses)
+        metrics = self.recorder.calculate_metrics_for_group("classification", loss=mean, conf=conf)
+        return mean, time.time() - t0, metrics, len(losses)
+
+    def train_epoch(self, loader: Iterable[Dict[str, Any]]):
+        """→ (mean batch loss, seconds, metrics dict, batches)."""
+        self.log.reset()
+        t0 = time.time()
+        for b in loader:
+            a, i, lab, g = self._unpack(b)
+            self._train_step(a.shape[0]).step(a, i, lab, g)
+        return self._finish(t0)
+
+    @torch.no_grad()
+    def validate_epoch(self, loader: Iterable[Dict[str, Any]]):
+        self.log.reset()
+        t0 = time.time()
+        self.model.eval()
+        for b in loader:
+            a, i, lab, g = self._unpack(b)
+            self._eval_step(a.shape[0]).step(a, i, lab, g)
+        return self._finish(t0)
+
+
+def _epoch_block(loss: float, timing: float, n_batches: int, metrics: Dict[str, Any]) -> Dict[str, Any]:
+    """One split's entry of epoch_metrics.json (train_multimodal.py:627-718)."""
+    out: Dict[str, Any] = {"loss": loss, "timing": {"total_time": timing,
+                                                    "avg_batch_time": timing / max(1, n_batches)}}
+    for key, value in metrics.items():
+        if key == "loss" or not isinstance(value, (int, float)):
+            continue
+        if key.startswith("f1_") and "_" in key:
+            parts = key.split("_")
+            name = parts[0] + "_" + parts[1]
+            mod = parts[2] if len(parts) >= 3 else "IT"
+            out.setdefault(mod, {})[name] = metrics[key]
+        else:
+            out.setdefault("metrics", {})[key] = value
+    return out
+
+
+def fit(model, optimizer, loss_functions, loaders: Dict[str, Any], epochs: int, *, metric_config=None,
+        early_stopping: bool = True, patience: int = 10, min_delta: float = 1e-3, scheduler=None,
+        checkpoint_dir=None, metrics_path=None, save_metric: str = "loss", mode: str = "minimize",
+        on_epoch=None) -> Dict[str, Any]:
+    """_train_loop + test (train_multimodal.py:554-917) for the AVMNIST late-fusion model.  ``loaders``:
+    "train", "validation" and optionally "test" → iterables of device batches (a DeviceLoader is
+    re-iterated each epoch; call ``set_epoch`` in ``on_epoch`` for DistributedSampler order)."""
+    runner = EpochRunner(model, optimizer, loss_functions, metric_config)
+    ckpt = CheckpointManager(checkpoint_dir, save_metric, mode) if checkpoint_dir is not None else None
+    history: Dict[str, Any] = {"train": [], "validation": [], "epoch_metrics": []}
+    best, wait = None, 0
+    mfile = Path(metrics_path) / "epoch_metrics.json" if metrics_path is not None else None
+    if mfile is not None:
+        mfile.parent.mkdir(parents=True, exist_ok=True)
+    for epoch in range(1, epochs + 1):
+        if on_epoch is not None:
+            on_epoch(epoch)
+        tr_loss, tr_time, tr_metrics, tr_n = runner.train_epoch(loaders["train"])
+        tr_metrics = dict(tr_metrics, loss=tr_loss)
+        va_loss, va_time, va_metrics, va_n = runner.validate_epoch(loaders["validation"])
+        va_metrics = dict(va_metrics, loss=va_loss)
+        history["train"].append(tr_metrics)
+        history["validation"].append(va_metrics)
+        history["epoch_metrics"].append({"epoch": epoch, "train": _epoch_block(tr_loss, tr_time, tr_n, tr_metrics),
+                                         "validation": _epoch_block(va_loss, va_time, va_n, va_metrics)})
+        if mfile is not None:
+            with open(mfile, "w") as f:
+                json.dump(history["epoch_metrics"], f, indent=4, default=lambda o: np.asarray(o).tolist())
+        is_best, cont, wait = check_early_stopping(va_metrics, best, patience, min_delta, wait, mode, save_metric)
+        if is_best:
+            best = dict(va_metrics)
+            if ckpt is not None:
+                ckpt.save_checkpoint(model, optimizer, scheduler, epoch, va_metrics, is_best=True)
+        if early_stopping and not cont:
+            break
+        if scheduler is not None:
+            if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+                scheduler.step(va_metrics["loss"])
+            else:
+                scheduler.step()
+    if "test" in loaders:
+        if ckpt is not None and (ckpt.model_dir / "best.pth").exists():
+            ckpt.load_checkpoint(model, load_best=True)
+        te_loss, te_time, te_metrics, _ = runner.validate_epoch(loaders["test"])
+        history["test"] = dict(te_metrics, loss=te_loss)
+    history["best"] = best
+    return history

@@ -206,6 +206,11 @@ def ResNet34(in_channels: int = 1, hidden_dim: int = 128) -> ResNetEncoder:
 # ------------------------------------------------------------------------------------------------
 # Fusion model
 # ------------------------------------------------------------------------------------------------
+def _ce_weight_of(loss_functions):
+    from .step import _ce_weight
+    return _ce_weight(loss_functions)
+
+
 def modality_key(batch: Dict[Any, Any], name: str):
     """Find the batch key for modality ``name`` ('audio' / 'image').  The reference keys batches by
     ``modalities.Modality`` members (un-vendored package); accept those, plain strings, or any enum
@@ -349,16 +354,34 @@ class AVMNIST(nn.Module):
         labels = batch["labels"].to(device, non_blocking=True)
         return A, I, labels, batch.get("pattern_name")
 
+    @staticmethod
+    def _device_log(metric_recorder):
+        from .metrics import DeviceMetricRecorder
+        return metric_recorder.log if isinstance(metric_recorder, DeviceMetricRecorder) else None
+
+    @staticmethod
+    def _group_ids(batch, log, miss_type, device):
+        g = batch.get("pattern_ids")
+        if g is not None:
+            return g.to(device, non_blocking=True)
+        return log.group_ids(miss_type) if (log is not None and miss_type is not None) else None
+
     def train_step(self, batch: Dict[Any, Any], optimizer, loss_functions, device, metric_recorder, **kwargs):
-        """models/avmnist.py:269-310.  Fused native step when possible (see module docstring)."""
+        """models/avmnist.py:269-310.  Fused native step when possible (see module docstring).  With a
+        metrics.DeviceMetricRecorder the batch's predictions are recorded on the device inside the step's
+        HIP graph; with the reference's MetricRecorder they are copied to the host as the reference does."""
         from .step import FusedTrainStep, fused_step_supported
         A, I, labels, miss_type = self._unpack(batch, device)
+        dlog = self._device_log(metric_recorder)
         if fused_step_supported(self, optimizer, loss_functions, A, I):
             if self._fused_step is None or not self._fused_step.matches(A, I, optimizer, loss_functions):
                 self._fused_step = FusedTrainStep(self, optimizer, loss_functions, A.shape[0])
-            out = self._fused_step.step(A, I, labels)
+            self._fused_step.log = dlog
+            out = self._fused_step.step(A, I, labels, self._group_ids(batch, dlog, miss_type, device))
             logits = out["logits"]
             loss_t = out["loss"]
+            if dlog is not None:
+                return {"loss": float(loss_t.item())}
         else:
             self.train()
             optimizer.zero_grad()
@@ -373,17 +396,40 @@ class AVMNIST(nn.Module):
                                              m_types=np.array(miss_type if miss_type is not None else []))
         return {"loss": float(loss_t.item())}
 
+    def eval_step_for(self, loss_functions, batch: int, log=None):
+        """The cached FusedEvalStep for this batch size (one HIP graph per size)."""
+        from .step import FusedEvalStep
+        cache = self.__dict__.setdefault("_fused_eval", {})
+        st = cache.get(batch)
+        if st is None or st.ce_weight != _ce_weight_of(loss_functions):
+            st = FusedEvalStep(self, loss_functions, batch, log)
+            cache[batch] = st
+        st.log = log
+        return st
+
     def validation_step(self, batch, loss_functions, device, metric_recorder, return_test_info: bool = False):
-        """models/avmnist.py:312-360 (eval-mode BN running stats, dropout off)."""
+        """models/avmnist.py:312-360 (eval-mode BN running stats, dropout off).  With a single
+        cross-entropy loss group the batch runs as one FusedEvalStep graph (predictions recorded on the
+        device when metric_recorder is a metrics.DeviceMetricRecorder)."""
         self.eval()
         with torch.no_grad():
             A, I, labels, miss_type = self._unpack(batch, device)
-            logits = self.forward(A=A, I=I)
-            loss = loss_functions(logits, labels)["total_loss"]
-            predictions = torch.softmax(logits, dim=1).argmax(dim=1).cpu().numpy()
+            dlog = self._device_log(metric_recorder)
+            if (_ce_weight_of(loss_functions) is not None and A.is_cuda and I.is_cuda and A.dim() == 3
+                    and tuple(A.shape[1:]) == (32, 94) and tuple(I.shape[-2:]) == (28, 28)):
+                st = self.eval_step_for(loss_functions, A.shape[0], dlog)
+                out = st.step(A, I, labels, self._group_ids(batch, dlog, miss_type, device))
+                if dlog is not None and not return_test_info:
+                    return {"loss": out["loss"].item()}
+                loss = out["loss"]
+                predictions = out["preds"].cpu().numpy()
+            else:
+                logits = self.forward(A=A, I=I)
+                loss = loss_functions(logits, labels)["total_loss"]
+                predictions = torch.softmax(logits, dim=1).argmax(dim=1).cpu().numpy()
             labels_np = labels.cpu().numpy()
             miss_type = np.array(miss_type if miss_type is not None else [])
-            if metric_recorder is not None:
+            if metric_recorder is not None and dlog is None:
                 metric_recorder.update_group_all(group_name="classification", predictions=predictions,
                                                  targets=labels_np, m_types=miss_type)
             if return_test_info:

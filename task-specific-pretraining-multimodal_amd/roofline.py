@@ -67,5 +67,19 @@ def step_flops_per_sample(audio_hw=(32, 94), image_hw=(28, 28), audio_hidden=64,
     return nom, val
 
 
+def eval_flops_per_sample(audio_hw=(32, 94), image_hw=(28, 28), audio_hidden=64, image_hidden=128,
+                          head_hidden=128) -> Tuple[int, int]:
+    """(nominal, valid-tap) FLOPs per sample of the evaluation forward (validation_step)."""
+    nom = val = 0
+    for layers, (h, w) in (((2, 2, 2, 2), audio_hw), ((3, 4, 6, 3), image_hw)):
+        for _, (hh, ww, c, k, r, s, st, p) in encoder_convs(layers, h, w):
+            a, b = conv_macs(1, hh, ww, c, k, r, s, st, p)
+            nom += 2 * a
+            val += 2 * b
+    lin = 512 * audio_hidden + 512 * image_hidden + (audio_hidden + image_hidden) * head_hidden \
+        + head_hidden * (head_hidden // 2) + (head_hidden // 2) * 10
+    return nom + 2 * lin, val + 2 * lin
+
+
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak

@@ -92,6 +92,11 @@ class FusedTrainStep:
         self.A = torch.empty(batch, audio_hw[0], audio_hw[1], **f32)
         self.I = torch.empty(batch, 1, image_hw[0], image_hw[1], **f32)
         self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.groups = torch.zeros(batch, dtype=torch.int32, device=dev)  # pattern id per row (metrics)
+        # metrics.ClassificationLog: when set, the step also records predictions / confusion counts /
+        # the batch loss on the device (train metrics of the epoch, train_multimodal.py:478-491,607-612)
+        self.log = None
+        self._graph_log = None
         self.fused = torch.empty(batch, self.F, **f32)
         self.h1 = torch.empty(batch, hd, **f32)
         self.hh = torch.empty(batch, self.h2, **f32)
@@ -105,11 +110,17 @@ class FusedTrainStep:
         self.stats = torch.zeros(4, **f32)  # loss*n, correct, n (accumulated on device)
         self.keep_override: Optional[torch.Tensor] = None
         # BN num_batches_tracked of both encoders in one int64 buffer (one add per step)
+        # (shared by every FusedTrainStep of the model, e.g. a second one for a partial last batch)
         bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
-        self.nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
-        for i, m in enumerate(bns):
-            self.nbt[i] = m.num_batches_tracked.to(dev)
-            m.num_batches_tracked = self.nbt[i]
+        nbt = getattr(model, "_tspm_nbt", None)
+        if not (nbt is not None and nbt.numel() == len(bns) and nbt.device == dev and all(
+                m.num_batches_tracked.data_ptr() == nbt[i].data_ptr() for i, m in enumerate(bns))):
+            nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+            for i, m in enumerate(bns):
+                nbt[i] = m.num_batches_tracked.to(dev)
+                m.num_batches_tracked = nbt[i]
+            model._tspm_nbt = nbt
+        self.nbt = nbt
         self.side = torch.cuda.Stream(device=dev)
         # per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in all,
         # matching the 4 hardware queues HIP gives a process by default
@@ -202,6 +213,7 @@ class FusedTrainStep:
             L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
                                                self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
                                                self.stats.data_ptr(), sh), "cross_entropy")
+            self._classify(sh)
             self._head_bwd(sh)
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -249,6 +261,7 @@ class FusedTrainStep:
         L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
                                            self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
                                            self.stats.data_ptr(), sh), "cross_entropy")
+        self._classify(sh)
         self._head_bwd(sh)
         self.nbt.add_(1)
 
@@ -311,6 +324,15 @@ class FusedTrainStep:
         ar.wait(w_a + w_i + w_e)
         run(5)
 
+    def _classify(self, sh: int) -> None:
+        log = self.log
+        if log is None:
+            return
+        L.check(L.lib().tspm_classify_update(
+            self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(), self.groups.data_ptr(),
+            len(log.groups), log.conf.data_ptr(), None, self.loss.data_ptr(), log.loss_log.data_ptr(),
+            log.counters.data_ptr(), log.capacity, sh), "classify_update")
+
     def _opt(self) -> None:
         self.opt.launch(torch.cuda.current_stream().cuda_stream)
 
@@ -320,7 +342,10 @@ class FusedTrainStep:
             self._opt()
 
     # ------------------------------------------------------------------------------------------
-    def load_batch(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor) -> None:
+    def load_batch(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor,
+                   groups: Optional[torch.Tensor] = None) -> None:
+        if groups is not None and groups.data_ptr() != self.groups.data_ptr():
+            self.groups.copy_(groups.reshape(-1).to(torch.int32), non_blocking=True)
         if A.data_ptr() != self.A.data_ptr():
             self.A.copy_(A.reshape(self.A.shape), non_blocking=True)
         if I.data_ptr() != self.I.data_ptr():
@@ -328,8 +353,9 @@ class FusedTrainStep:
         if labels.data_ptr() != self.labels.data_ptr():
             self.labels.copy_(labels, non_blocking=True)
 
-    def step(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor) -> Dict[str, torch.Tensor]:
-        self.load_batch(A, I, labels)
+    def step(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor,
+             groups: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        self.load_batch(A, I, labels, groups)
         self.run()
         return {"loss": self.loss, "logits": self.logits}
 
@@ -337,6 +363,9 @@ class FusedTrainStep:
         """One training step on the batch currently in the static input buffers."""
         self.model.train()
         self.opt.sync_hyper()
+        if self._graph_log is not self.log:  # the metrics log is baked into the captured graphs
+            self.graph, self.graph_opt = None, None
+            self._graph_log = self.log
         if self.keep_override is not None:
             self.keep.copy_(self.keep_override.reshape(self.keep.shape).to(torch.uint8), non_blocking=True)
         if isinstance(self.allreduce, PhasedGradAllReduce):
@@ -375,3 +404,100 @@ class FusedTrainStep:
             with torch.cuda.graph(go):
                 self._opt()
             self.graph_opt = go
+
+
+class FusedEvalStep:
+    """AVMNIST.validation_step (MML_Suite/models/avmnist.py:312-360) as one HIP graph: both encoders in
+    eval mode (BatchNorm running statistics) on two streams, the fusion head without dropout, the loss
+    (LossFunctionGroup total = weight × CE) and ``tspm_classify_update`` — predictions, per-pattern
+    confusion counts and the per-batch loss go to a :class:`metrics.ClassificationLog` on the device,
+    so an evaluation epoch has no host round trip per batch.  Shares the encoders' cached HIP plans
+    (``ResNetEncoder.engine_for``) with the module forward."""
+
+    def __init__(self, model, loss_functions, batch: int, log=None, audio_hw=(32, 94), image_hw=(28, 28),
+                 use_graph: bool = True):
+        self.model, self.N, self.log = model, batch, log
+        self.ce_weight = _ce_weight(loss_functions)
+        if self.ce_weight is None:
+            raise L.TspmError("FusedEvalStep: the loss group must be a single cross-entropy term")
+        self.use_graph = use_graph and not os.environ.get("TSPM_NO_GRAPH")
+        dev = next(model.parameters()).device
+        self.device = dev
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.A = torch.zeros(batch, audio_hw[0], audio_hw[1], **f32)
+        self.I = torch.zeros(batch, 1, image_hw[0], image_hw[1], **f32)
+        self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.groups = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.eng_a = model.audio_encoder.engine_for(self.A)
+        self.eng_i = model.image_encoder.engine_for(self.I)
+        ea, ei = model.embd_size_A, model.embd_size_I
+        self.F, self.hd = ea + ei, model.hidden_dim
+        self.fused = torch.empty(batch, self.F, **f32)
+        self.h1 = torch.empty(batch, self.hd, **f32)
+        self.hh = torch.empty(batch, self.hd // 2, **f32)
+        self.logits = torch.empty(batch, NUM_CLASSES, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.preds = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.side = torch.cuda.Stream(device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self._graph_log = None
+        self.calls = 0
+
+    def load_batch(self, A: torch.Tensor, I: torch.Tensor, labels: torch.Tensor,
+                   groups: Optional[torch.Tensor] = None) -> None:
+        for dst, src in ((self.A, A), (self.I, I), (self.labels, labels)):
+            if src.data_ptr() != dst.data_ptr():
+                dst.copy_(src.reshape(dst.shape), non_blocking=True)
+        if groups is not None and groups.data_ptr() != self.groups.data_ptr():
+            self.groups.copy_(groups.reshape(-1).to(torch.int32), non_blocking=True)
+
+    def _enqueue(self) -> None:
+        lib = L.lib()
+        main = torch.cuda.current_stream()
+        ea = self.model.embd_size_A
+        for e in (self.eng_a, self.eng_i):
+            e.aux = None
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=False)
+        self.eng_a.forward(self.A, self.fused, self.F, train=False)
+        main.wait_stream(self.side)
+        sh = main.cuda_stream
+        n, F, hd, h2 = self.N, self.F, self.hd, self.hd // 2
+        net = self.model.net
+        L.check(lib.tspm_linear_fwd(n, F, hd, self.fused.data_ptr(), F, net[0].weight.data_ptr(),
+                                    net[0].bias.data_ptr(), 1, None, 1.0, self.h1.data_ptr(), hd, sh), "eval fc0")
+        L.check(lib.tspm_linear_fwd(n, hd, h2, self.h1.data_ptr(), hd, net[3].weight.data_ptr(),
+                                    net[3].bias.data_ptr(), 1, None, 1.0, self.hh.data_ptr(), h2, sh), "eval fc3")
+        L.check(lib.tspm_linear_fwd(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, net[5].weight.data_ptr(),
+                                    net[5].bias.data_ptr(), 0, None, 1.0, self.logits.data_ptr(), NUM_CLASSES, sh),
+                "eval fc5")
+        L.check(lib.tspm_cross_entropy(n, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
+                                       self.loss.data_ptr(), None, self.ce_weight, None, sh), "eval cross_entropy")
+        log = self.log
+        L.check(lib.tspm_classify_update(
+            n, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(), self.groups.data_ptr(),
+            len(log.groups) if log is not None else 1, log.conf.data_ptr() if log is not None else None,
+            self.preds.data_ptr(), self.loss.data_ptr(), log.loss_log.data_ptr() if log is not None else None,
+            log.counters.data_ptr() if log is not None else None, log.capacity if log is not None else 0, sh),
+            "eval classify_update")
+
+    def run(self) -> None:
+        """Evaluate the batch in the static input buffers (logits, loss, preds; log updated)."""
+        self.model.eval()
+        if not self.use_graph or self.calls == 0:
+            self._enqueue()
+        else:
+            if self.graph is None or self._graph_log is not self.log:
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._enqueue()
+                self.graph, self._graph_log = g, self.log
+            self.graph.replay()
+        self.calls += 1
+
+    def step(self, A, I, labels, groups=None) -> Dict[str, torch.Tensor]:
+        self.load_batch(A, I, labels, groups)
+        self.run()
+        return {"loss": self.loss, "logits": self.logits, "preds": self.preds}
