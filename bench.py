@@ -313,6 +313,96 @@ def eval_bench(args) -> None:
     print(json.dumps(res), flush=True)
 
 
+def mono_bench(args) -> None:
+    """--mono: BASELINE.json configs[1] — the monomodal ResNet18 audio pre-training step
+    (MML_Suite/train_monomodal.py:97-260: encoder → classifier → CE → backward → Adam, argmax
+    predictions) at batch 256 on one MI355X as one FusedMonoStep graph replay per step, each batch
+    gathered on device from an HBM-resident synthetic corpus; conv roofline as for the main line; CPU
+    baseline: the oracle's monomodal step (bit-identical to the reference's on CPU)."""
+    import tspm_amd
+    from tspm_amd.data import AVMNIST, synthetic_corpus
+    from tspm_amd.monomodal import FusedMonoStep, MonomodalEncoder
+    from tspm_amd.roofline import FP32_MFMA_PEAK_TFLOPS, mono_flops_per_sample
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B = args.mono_batch
+    torch.manual_seed(0)
+    model = MonomodalEncoder(tspm_amd.ResNet18(1, 64), 64, 10).to(dev)
+    opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
+    st = FusedMonoStep(model, opt, None, (B, 32, 94))
+    ds = AVMNIST(None, "train", "audio", selected_patterns=["a"], corpus=synthetic_corpus(args.corpus, 1234),
+                 device=dev)
+    ds.device_corpus  # upload once, outside the timed region
+    loader = ds.device_loader(B, shuffle=True, drop_last=True, generator=torch.Generator().manual_seed(1234),
+                              out=(st.X, None, st.labels))
+
+    def feed():
+        epoch = 0
+        while True:
+            loader.set_epoch(epoch)
+            yield from loader
+            epoch += 1
+    f = feed()
+    for _ in range(args.warmup):
+        next(f)
+        st.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        next(f)
+        st.run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    value = args.steps * B / el
+    # roofline: one instrumented eager step, every conv launch bracketed by HIP events
+    timer = ConvTimer()
+    st.eng.conv_timer = timer
+    st.use_graph = False
+    next(f)
+    st.run()
+    st.use_graph = True
+    torch.cuda.synchronize()
+    st.eng.conv_timer = None
+    n_launch, conv_flops, conv_ms = timer.summarize()
+    achieved = conv_flops / (conv_ms * 1e-3) / 1e12
+    nominal, valid = mono_flops_per_sample()
+    step_tf = valid * value / 1e12
+    res = {"metric": "samples/sec AVMNIST monomodal ResNet18 audio pre-train step, 1 MI355X (BASELINE.json configs[1])",
+           "value": round(value, 2), "unit": "samples/sec", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32",
+           "data": f"synthetic AVMNIST-shaped audio corpus of {args.corpus} samples resident in HBM, gathered on "
+                   "device each step; random-init weights (seed 0)",
+           "config": {"workload": "avmnist_monomodal_train_step(resnet18_audio+linear(64,10), CE, Adam)", "batch": B},
+           "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM family (LDS-staged + register-direct), "
+                                                   "fp32 MFMA 32x32x2",
+                        "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                        "launches_per_step": n_launch, "conv_ms_per_step": round(conv_ms, 4),
+                        "valid_tap_flop_per_step": conv_flops, "step_valid_tflops": round(step_tf, 3),
+                        "step_frac_of_peak": round(step_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                        "valid_tap_flop_per_sample": valid, "nominal_flop_per_sample": nominal},
+           "final_loss": round(st.loss.item(), 5)}
+    if not args.no_cpu_baseline:
+        from oracle import avmnist_ref as orc
+        from oracle import monomodal_ref as mref
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        ref = mref.build_oracle_monomodal("audio", 0)
+        ropt = orc.OracleAdam(list(ref.parameters()), lr=5e-4, weight_decay=1e-4)
+        audio, _, labels, _ = orc.synthetic_batch(B, seed=1234)
+        mref.train_step(ref, ropt, audio, labels)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_budget and n < 200:
+            mref.train_step(ref, ropt, audio, labels)
+            n += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n * B / el, 1), "unit": "samples/sec", "cores": threads, "kind": "port",
+                               "sample": f"{n} oracle monomodal train steps (ResNet18 + Linear, CE, Adam, fp32) at "
+                                         f"batch {B}, {el:.1f}s, torch.set_num_threads({threads})"}
+    print(json.dumps(res), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -330,9 +420,15 @@ def main() -> None:
     ap.add_argument("--cpu-input-samples", type=int, default=16384)
     ap.add_argument("--eval", action="store_true", help="benchmark the evaluation path / epoch harness (one JSON line)")
     ap.add_argument("--eval-corpus", type=int, default=10000, help="--eval validation corpus (x3 patterns)")
+    ap.add_argument("--mono", action="store_true",
+                    help="benchmark the monomodal ResNet18 audio pre-training step (BASELINE.json configs[1])")
+    ap.add_argument("--mono-batch", type=int, default=256)
     args = ap.parse_args()
     if args.input_stage:
         input_stage_bench(args)
+        return
+    if args.mono:
+        mono_bench(args)
         return
     if args.eval:
         eval_bench(args)

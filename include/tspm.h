@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 8 */
+int tspm_abi_version(void);  /* 9 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -290,6 +290,16 @@ int tspm_classify_update(int32_t n, int32_t classes, const float* logits, const 
                          const int32_t* groups, int32_t n_groups, int64_t* confusion, int64_t* pred_out,
                          const float* loss, float* loss_log, int64_t* counters, int64_t log_capacity,
                          tspm_stream_t stream);
+/* Argmax conventions: the fusion model predicts argmax(softmax(logits)) (models/avmnist.py:305-306),
+ * the monomodal pre-training step argmax(logits) (train_monomodal.py:236,394); they differ only when
+ * two logits round to one probability. */
+#define TSPM_ARGMAX_SOFTMAX 0
+#define TSPM_ARGMAX_LOGITS 1
+/* tspm_classify_update with an explicit convention (argmax_of: TSPM_ARGMAX_*). */
+int tspm_classify_update_ex(int32_t n, int32_t classes, const float* logits, const int64_t* labels,
+                            const int32_t* groups, int32_t n_groups, int64_t* confusion, int64_t* pred_out,
+                            const float* loss, float* loss_log, int64_t* counters, int64_t log_capacity,
+                            int32_t argmax_of, tspm_stream_t stream);
 /* Sum `nslab` slabs of `count` floats (slab_stride apart) into out (deterministic slab order). */
 int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs, float* out,
                       tspm_stream_t stream);

@@ -28,10 +28,11 @@ from tspm_amd.roofline import conv_macs  # noqa: E402
 from tune_convs import Bufs, graph_time, launcher  # noqa: E402
 
 
-def step_ops(batch, dev):
+def step_ops(batch, dev, encoders=("audio", "image")):
     """(kind, key) -> [ConvShape, strides, is_stem, count per step, tuned algo]."""
     out = {}
-    encs = [(tspm_amd.ResNet18(1, 64), 32, 94, True), (tspm_amd.ResNet34(1, 128), 28, 28, False)]
+    encs = [(tspm_amd.ResNet18(1, 64), 32, 94, True)] if "audio" in encoders else []
+    encs += [(tspm_amd.ResNet34(1, 128), 28, 28, False)] if "image" in encoders else []
     for enc, h, w, three_d in encs:
         enc = enc.to(dev)
         prepare_encoder_layout(enc)

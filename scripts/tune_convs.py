@@ -184,6 +184,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only-kind", default=None)
+    ap.add_argument("--encoders", default="audio,image", help="audio (ResNet18), image (ResNet34) or both")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -192,7 +193,8 @@ def main():
     table = []
     t0 = time.time()
     tot_base, tot_best = 0.0, 0.0
-    for key, (s, xs, stem, count, base) in sorted(step_ops(args.batch, dev).items(), key=lambda kv: str(kv[0])):
+    ops = step_ops(args.batch, dev, tuple(args.encoders.split(",")))
+    for key, (s, xs, stem, count, base) in sorted(ops.items(), key=lambda kv: str(kv[0])):
         kind = key[0]
         if args.only_kind and kind != args.only_kind:
             continue

@@ -17,9 +17,10 @@ from .engine import EncoderEngine, prepare_encoder_layout
 from .modules import AVMNIST, BasicBlock, ResNet18, ResNet34, ResNetEncoder, modality_key
 from .optim import FusedAdam
 from .step import FusedTrainStep
-from . import plugin, ddp, data
+from .monomodal import FusedMonoStep, MonomodalEncoder
+from . import plugin, ddp, data, monomodal
 
 __all__ = ["AVMNIST", "BasicBlock", "ResNet18", "ResNet34", "ResNetEncoder", "FusedAdam", "FusedTrainStep",
            "EncoderEngine", "prepare_encoder_layout", "TspmError", "TspmLibraryError", "plugin", "ddp", "data",
-           "modality_key"]
+           "modality_key", "MonomodalEncoder", "FusedMonoStep", "monomodal"]
 __version__ = "0.1.0"

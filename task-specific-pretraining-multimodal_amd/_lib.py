@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -99,6 +99,8 @@ _SIGS = {
     "tspm_image_lut": (c_int32, [c_int64, _P, _P, _P, _P]),
     "tspm_avmnist_gather": (c_int32, [c_int64, _P, c_int64, _P, c_int32, _P, c_int32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tspm_classify_update": (c_int32, [c_int32, c_int32, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int64, _P]),
+    "tspm_classify_update_ex": (c_int32, [c_int32, c_int32, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int64, c_int32,
+                                          _P]),
     "tspm_reduce_slabs": (c_int32, [c_int64, c_int32, c_int64, _P, _P, _P]),
 }
 

@@ -78,7 +78,25 @@ def register_resolvers(resolvers_module: Optional[object] = None, rebind_everywh
     return True
 
 
+def register_monomodal(module: Optional[object] = None) -> bool:
+    """``train_monomodal.py`` defines ``MonomodalEncoder`` in the script itself and ``setup_experiment``
+    looks the name up when it runs (MML_Suite/train_monomodal.py:64,525-529): rebind it in the loaded
+    script module (imported as ``train_monomodal``, or ``__main__`` when the script is the program)."""
+    from .monomodal import MonomodalEncoder
+    cands = [module] if module is not None else [sys.modules.get("train_monomodal"), sys.modules.get("__main__")]
+    done = False
+    for m in cands:
+        if m is None or not hasattr(m, "MonomodalEncoder"):
+            continue
+        if m is sys.modules.get("train_monomodal") or module is not None or hasattr(m, "train_monomodal"):
+            setattr(m, "MonomodalEncoder", MonomodalEncoder)
+            done = True
+    return done
+
+
 def register(loader=None, resolvers_module=None) -> None:
-    """Install the HIP implementations behind the reference's YAML tags and resolvers."""
+    """Install the HIP implementations behind the reference's YAML tags, resolvers and the monomodal
+    script's model class."""
     register_yaml(loader)
     register_resolvers(resolvers_module)
+    register_monomodal()

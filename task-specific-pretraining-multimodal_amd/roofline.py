@@ -81,5 +81,19 @@ def eval_flops_per_sample(audio_hw=(32, 94), image_hw=(28, 28), audio_hidden=64,
     return nom + 2 * lin, val + 2 * lin
 
 
+def mono_flops_per_sample(layers=(2, 2, 2, 2), hw=(32, 94), hidden=64, classes=10) -> Tuple[int, int]:
+    """(nominal, valid-tap) FLOPs per sample of the monomodal pre-training step (train_monomodal.py:
+    97-260, default: ResNet18 audio + Linear(64, 10)): encoder fwd + dgrad + wgrad (no stem dgrad),
+    encoder fc and classifier (3 passes each)."""
+    nom = val = 0
+    for name, (hh, ww, c, k, r, s, st, p) in encoder_convs(layers, hw[0], hw[1]):
+        a, b = conv_macs(1, hh, ww, c, k, r, s, st, p)
+        passes = 2 if name == "stem" else 3
+        nom += 2 * passes * a
+        val += 2 * passes * b
+    lin = 512 * hidden + hidden * classes
+    return nom + 6 * lin, val + 6 * lin
+
+
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak

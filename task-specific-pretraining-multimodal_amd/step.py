@@ -50,6 +50,22 @@ def _ce_weight(loss_functions) -> Optional[float]:
     return float(w)
 
 
+def shared_batches_tracked(model: torch.nn.Module, dev: torch.device) -> torch.Tensor:
+    """The ``num_batches_tracked`` counters of every BatchNorm2d of ``model`` re-pointed as views of ONE
+    int64 device buffer (one add per step instead of one per BN), shared by every fused step of the
+    model (e.g. a second one for a partial last batch)."""
+    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+    nbt = getattr(model, "_tspm_nbt", None)
+    if not (nbt is not None and nbt.numel() == len(bns) and nbt.device == dev and all(
+            m.num_batches_tracked.data_ptr() == nbt[i].data_ptr() for i, m in enumerate(bns))):
+        nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+        for i, m in enumerate(bns):
+            nbt[i] = m.num_batches_tracked.to(dev)
+            m.num_batches_tracked = nbt[i]
+        model._tspm_nbt = nbt
+    return nbt
+
+
 def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: torch.Tensor) -> bool:
     if os.environ.get("TSPM_DISABLE_FUSED_STEP"):
         return False
@@ -109,18 +125,7 @@ class FusedTrainStep:
         self.loss = torch.zeros(1, **f32)
         self.stats = torch.zeros(4, **f32)  # loss*n, correct, n (accumulated on device)
         self.keep_override: Optional[torch.Tensor] = None
-        # BN num_batches_tracked of both encoders in one int64 buffer (one add per step)
-        # (shared by every FusedTrainStep of the model, e.g. a second one for a partial last batch)
-        bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
-        nbt = getattr(model, "_tspm_nbt", None)
-        if not (nbt is not None and nbt.numel() == len(bns) and nbt.device == dev and all(
-                m.num_batches_tracked.data_ptr() == nbt[i].data_ptr() for i, m in enumerate(bns))):
-            nbt = torch.zeros(len(bns), dtype=torch.int64, device=dev)
-            for i, m in enumerate(bns):
-                nbt[i] = m.num_batches_tracked.to(dev)
-                m.num_batches_tracked = nbt[i]
-            model._tspm_nbt = nbt
-        self.nbt = nbt
+        self.nbt = shared_batches_tracked(model, dev)
         self.side = torch.cuda.Stream(device=dev)
         # per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in all,
         # matching the 4 hardware queues HIP gives a process by default
