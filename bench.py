@@ -77,7 +77,7 @@ class ConvTimer:
         for op, kind, e0, e1 in self.events:
             s = op.shape
             _, valid = conv_macs(s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad)
-            flops += 2 * valid
+            flops += 2 * valid * (2 if kind == "bwd" else 1)  # "bwd": dgrad + wgrad in one launch
             tot_ms += e0.elapsed_time(e1)
         return len(self.events), flops, tot_ms
 

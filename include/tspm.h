@@ -134,6 +134,20 @@ int tspm_conv_wgrad_t(const tspm_conv_shape* shape, const tspm_conv_algo* algo, 
                       int64_t ldx, const float* dy_t, int64_t ldy, float* dw, void* workspace,
                       size_t workspace_bytes, tspm_stream_t stream);
 
+/* Input AND weight gradient of one convolution in ONE launch (both algos variant 1): the dgrad and
+ * wgrad implicit GEMMs read the same dy and are independent, and at batch 128 either alone leaves
+ * most of the 256 CUs idle, so their workgroups share one grid.  Results are bitwise those of
+ * tspm_conv_dgrad(algo_dgrad, beta) + tspm_conv_wgrad(algo_wgrad).  Workspaces as for those two
+ * calls, one each (not the same buffer when both algos split).  Only the (dgrad, wgrad) tile pairs
+ * built into the library run fused: tspm_conv_bwd_supported() returns 1 for those, 0 otherwise
+ * (then call the two entry points; tspm_conv_bwd returns TSPM_ERR_INVALID). */
+int32_t tspm_conv_bwd_supported(const tspm_conv_shape* shape, const tspm_conv_algo* algo_dgrad,
+                                const tspm_conv_algo* algo_wgrad, const tspm_strides4* x_strides);
+int tspm_conv_bwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo_dgrad,
+                  const tspm_conv_algo* algo_wgrad, const float* x, const tspm_strides4* x_strides,
+                  const float* dy, const float* w, float* dx, int32_t beta, float* dw, void* ws_dgrad,
+                  size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, tspm_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------------
  * BatchNorm2d, training mode (batch statistics over N*H*W, biased variance for normalisation,
  * unbiased for running_var, momentum 0.1, eps 1e-5) — resnet.py:26,31,138,177.

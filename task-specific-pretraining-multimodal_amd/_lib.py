@@ -73,6 +73,9 @@ _SIGS = {
     "tspm_conv_wgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_wgrad_t": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, c_int64, _P, c_int64, _P, _P, c_size_t,
                                     _P]),
+    "tspm_conv_bwd_supported": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), POINTER(Strides4)]),
+    "tspm_conv_bwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P,
+                                _P, c_int32, _P, _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_stats": (c_int32, [c_int64, c_int32, _P, c_int32, c_int64, _P, _P, _P, c_float, c_float, _P, _P, _P,
                                 c_size_t, _P]),
     "tspm_bn_stats_workspace": (c_size_t, [c_int64, c_int32]),

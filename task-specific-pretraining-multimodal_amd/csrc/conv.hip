@@ -839,6 +839,24 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   return TSPM_OK;
 }
 
+extern "C" int32_t tspm_conv_bwd_supported(const tspm_conv_shape* s, const tspm_conv_algo* dg,
+                                          const tspm_conv_algo* wg, const tspm_strides4* xs) {
+  if (!shape_ok(s) || !is_lds(dg) || !is_lds(wg)) return 0;
+  const tspm_detail::LdsAlgo ad = lds_algo(dg), aw = lds_algo(wg);
+  return (tspm_detail::lds_dgrad_supported(s, ad) && tspm_detail::lds_wgrad_supported(s, xs, aw) &&
+          tspm_detail::lds_bwd_built(ad, aw)) ? 1 : 0;
+}
+
+extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                             const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
+                             int32_t beta, float* dw, void* ws_d, size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes,
+                             tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
+  if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
+  return tspm_detail::lds_bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w,
+                              ws_w_bytes, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x_t, int64_t ldx,
                                  const float* dy_t, int64_t ldy, float* dw, void* ws, size_t ws_bytes,
                                  tspm_stream_t stream) {

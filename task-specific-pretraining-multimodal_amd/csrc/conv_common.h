@@ -232,4 +232,8 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
               void* ws, size_t ws_bytes, hipStream_t st);
 int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
               size_t ws_bytes, hipStream_t st);
+bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw);
+int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+            const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
+            hipStream_t st);
 }  // namespace tspm_detail

@@ -109,6 +109,13 @@ struct Off {
   long long a, b;
 };
 
+// Workgroup coordinates of a GEMM tile: the launch's own blockIdx / gridDim.x, or virtual ones when
+// two GEMMs share one launch (k_bwd_lds).
+struct Blk {
+  int x, y, z, gx;
+};
+TSPM_DEV Blk hw_blk() { return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x}; }
+
 // One stage's MFMAs with the next stage's LDS-DMA issues interleaved between them.  Measured
 // (scripts/stamp_conv.py ablations): a global_load_lds blocks its wave ~170 cycles at issue, and
 // with one wave per SIMD issuing them all before the MFMAs serialised DMA issue and matrix work
@@ -205,10 +212,10 @@ TSPM_DEV void combine_k(Acc<C::TM, C::TN>& acc, float* lds, const WaveId<C>& id,
 template <class C>
 TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lane, float* slabs, long long slab,
                             int splits, unsigned* cnt, int row0, int col0, int rows, int cols, long long ld,
-                            float* lds) {
+                            float* lds, const Blk& bk) {
   if (splits <= 1) return true;
-  if (id.wk == 0) acc.store(slabs + (long long)blockIdx.z * slab, row0, col0, rows, cols, ld, lane, false, true);
-  if (!last_arriver(cnt + (blockIdx.y * gridDim.x + blockIdx.x), (unsigned)splits, reinterpret_cast<int*>(lds)))
+  if (id.wk == 0) acc.store(slabs + (long long)bk.z * slab, row0, col0, rows, cols, ld, lane, false, true);
+  if (!last_arriver(cnt + (bk.y * bk.gx + bk.x), (unsigned)splits, reinterpret_cast<int*>(lds)))
     return false;
   if (id.wk == 0) {
     acc.zero();
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
   const int row0 = m0 + id.wm * C::TM * 32, col0 = n0col + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds, hw_blk()))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
   const bool active = id.wk == 0 && col0 < K;
@@ -322,16 +329,14 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
 // A image: BM rows (n) x 32 output channels (swizzled); B image: 32 rows (co) x BN input channels.
 // =============================================================================================
 template <class C>
-__global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
-                                                       const float* __restrict__ w, float* __restrict__ dx,
-                                                       float* __restrict__ slabs) {
-  extern __shared__ float lds[];
+TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const float* __restrict__ w,
+                         float* __restrict__ dx, float* __restrict__ slabs, float* lds, const Blk& bk) {
   TSPM_STAMP(tspm_g_stamps_lds, 0);
   TSPM_STAMP_CLK(tspm_g_stamps_lds, 6);
   const int tid = threadIdx.x, lane = tid & 63;
   const WaveId<C> id;
   const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
-  const int m0 = blockIdx.x * C::BM, c0col = blockIdx.y * C::BN;
+  const int m0 = bk.x * C::BM, c0col = bk.y * C::BN;
   const int pos = m0 / N, nb0 = m0 - pos * N;
   const int hi = pos / g.w, wi = pos - hi * g.w;
   unsigned rmask = 0, smask = 0;
@@ -346,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float*
   const int nr = __builtin_popcount(rmask), ns = __builtin_popcount(smask);
   const int kb = K >> 5;
   const int T = nr * ns * kb;
-  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+  const int st0 = split_lo(T, bk.z, g.splits), st1 = split_lo(T, bk.z + 1, g.splits);
 
   constexpr int NA = C::BM / 32;
   constexpr int BCH = C::BN / 4;            // 16-B chunks per B row
@@ -398,12 +403,19 @@ __global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float*
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
   const int row0 = m0 + id.wm * C::TM * 32, col0 = c0col + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
   if (id.wk == 0 && col0 < Cc) acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
   TSPM_STAMP(tspm_g_stamps_lds, 5);
   TSPM_STAMP_CLK(tspm_g_stamps_lds, 7);
+}
+template <class C>
+__global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
+                                                       const float* __restrict__ w, float* __restrict__ dx,
+                                                       float* __restrict__ slabs) {
+  extern __shared__ float lds[];
+  dgrad_body<C>(g, dy, w, dx, slabs, lds, hw_blk());
 }
 
 // =============================================================================================
@@ -412,21 +424,19 @@ __global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float*
 // tap's valid rectangle).  A image: 32 rows (m) x BM output channels; B image: 32 rows x BN inputs.
 // =============================================================================================
 template <class C>
-__global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float* __restrict__ x,
-                                                       const float* __restrict__ dy, float* __restrict__ dw,
-                                                       float* __restrict__ slabs) {
-  extern __shared__ float lds[];
+TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const float* __restrict__ dy,
+                         float* __restrict__ dw, float* __restrict__ slabs, float* lds, const Blk& bk) {
   const int tid = threadIdx.x, lane = tid & 63;
   const WaveId<C> id;
   const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
-  const int co0 = blockIdx.x * C::BM, col0b = blockIdx.y * C::BN;
+  const int co0 = bk.x * C::BM, col0b = bk.y * C::BN;
   const int tap = col0b / Cc, ci0 = col0b - tap * Cc;
   const int r = tap / g.s, s = tap - r * g.s;
   const int pp_lo = max(0, cdiv_dev(g.pad - r, g.st)), pp_hi = min(g.p - 1, (g.h - 1 + g.pad - r) / g.st);
   const int qq_lo = max(0, cdiv_dev(g.pad - s, g.st)), qq_hi = min(g.q - 1, (g.w - 1 + g.pad - s) / g.st);
   const int npp = max(0, pp_hi - pp_lo + 1), nqq = max(0, qq_hi - qq_lo + 1), n32 = N >> 5;
   const int T = npp * nqq * n32;
-  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+  const int st0 = split_lo(T, bk.z, g.splits), st1 = split_lo(T, bk.z + 1, g.splits);
 
   constexpr int ACH = C::BM / 4, BCH = C::BN / 4;
   constexpr int NA = C::BM / 32, NB = C::BN / 32;
@@ -474,9 +484,46 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float*
       });
   combine_k<C>(acc, lds, id, lane);
   const int row0 = co0 + id.wm * C::TM * 32, col0 = col0b + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds, bk))
     return;
   if (id.wk == 0 && row0 < K) acc.store(dw, row0, col0, K, RSC, RSC, lane, false);
+}
+template <class C>
+__global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float* __restrict__ x,
+                                                       const float* __restrict__ dy, float* __restrict__ dw,
+                                                       float* __restrict__ slabs) {
+  extern __shared__ float lds[];
+  wgrad_body<C>(g, x, dy, dw, slabs, lds, hw_blk());
+}
+
+// =============================================================================================
+// Input AND weight gradient of one convolution in ONE launch (tspm_conv_bwd).  Both implicit GEMMs
+// read the same dy and are independent, and at batch 128 either alone leaves most of the 256 CUs
+// idle, so they share one grid: workgroups [0, nw) run the weight-gradient tiles (virtual grid
+// wgx x wgy x splits), the rest the data-gradient tiles.  The branch is workgroup-uniform; each
+// body is the standalone kernel's, so results are bitwise those of the two separate launches.
+// =============================================================================================
+template <class CD, class CW>
+__global__ __launch_bounds__(kThreads) void k_bwd_lds(ConvArgs gd, const float* __restrict__ dy,
+                                                     const float* __restrict__ w, float* __restrict__ dx,
+                                                     float* __restrict__ slabs_d, int dgx, int dgy, ConvArgs gw,
+                                                     const float* __restrict__ x, float* __restrict__ dw,
+                                                     float* __restrict__ slabs_w, int wgx, int wgy) {
+  extern __shared__ float lds[];
+  int b = blockIdx.x;
+  const int nw = wgx * wgy * gw.splits;
+  if (b < nw) {
+    const int z = b / (wgx * wgy);
+    b -= z * wgx * wgy;
+    const int y = b / wgx;
+    wgrad_body<CW>(gw, x, dy, dw, slabs_w, lds, Blk{b - y * wgx, y, z, wgx});
+  } else {
+    b -= nw;
+    const int z = b / (dgx * dgy);
+    b -= z * dgx * dgy;
+    const int y = b / dgx;
+    dgrad_body<CD>(gd, dy, w, dx, slabs_d, lds, Blk{b - y * dgx, y, z, dgx});
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -645,6 +692,89 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_WG) }();
 #undef TSPM_WG
   if (rc != TSPM_OK) return rc;
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+// ---- fused dgrad + wgrad (k_bwd_lds): the (dgrad, wgrad) tile pairs built into the library are the
+// tm = tn = 1 wave layouts the batch-128/256 tuning picks (tuned/*.json): 3 for dgrad x 4 for wgrad
+struct BwdLaunch {
+  ConvArgs gd, gw;
+  const float *dy, *w, *x;
+  float *dx, *dw, *slabs_d, *slabs_w;
+  int dgx, dgy, wgx, wgy;
+  size_t lds;
+  hipStream_t st;
+};
+template <class CD, class CW>
+void bwd_go(const BwdLaunch& L) {
+  const int nblk = L.wgx * L.wgy * L.gw.splits + L.dgx * L.dgy * L.gd.splits;
+  hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kThreads), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
+                     L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy);
+}
+bool is_cfg(const LdsAlgo& a, int wm, int wn, int wk) {
+  return a.tm == 1 && a.tn == 1 && a.wm == wm && a.wn == wn && a.wk == wk;
+}
+template <class CD>
+bool bwd_w(const LdsAlgo& aw, const BwdLaunch* L) {  // L == nullptr: query only
+#define TSPM_BW(WM_, WN_, WK_)                                  \
+  if (is_cfg(aw, WM_, WN_, WK_)) {                              \
+    if (L) bwd_go<CD, Cfg<1, 1, WM_, WN_, WK_>>(*L);            \
+    return true;                                                \
+  }
+  TSPM_BW(2, 2, 1)
+  TSPM_BW(1, 1, 4)
+  TSPM_BW(1, 2, 2)
+  TSPM_BW(2, 1, 2)
+#undef TSPM_BW
+  return false;
+}
+bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
+#define TSPM_BD(WM_, WN_, WK_) \
+  if (is_cfg(ad, WM_, WN_, WK_)) return bwd_w<Cfg<1, 1, WM_, WN_, WK_>>(aw, L);
+  TSPM_BD(1, 2, 2)
+  TSPM_BD(1, 4, 1)
+  TSPM_BD(1, 1, 4)
+#undef TSPM_BD
+  return false;
+}
+
+bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(ad, aw, nullptr); }
+
+int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+            const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
+            hipStream_t st) {
+  if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
+  BwdLaunch L{};
+  L.gd = args_of(s);
+  L.gd.m = s->h * s->w * s->n;
+  L.gd.splits = ad.splits;
+  L.gd.beta = beta ? 1 : 0;
+  if (ad.splits > 1) {
+    if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
+    L.gd.cnt = static_cast<unsigned*>(wsd);
+    L.slabs_d = reinterpret_cast<float*>(static_cast<char*>(wsd) + TSPM_COUNTER_BYTES);
+  }
+  L.gw = args_of(s);
+  L.gw.m = s->k;
+  L.gw.splits = aw.splits;
+  if (aw.splits > 1) {
+    if (!wsw || wsw_bytes < lds_wgrad_workspace(s, aw)) return TSPM_ERR_WORKSPACE;
+    L.gw.cnt = static_cast<unsigned*>(wsw);
+    L.slabs_w = reinterpret_cast<float*>(static_cast<char*>(wsw) + TSPM_COUNTER_BYTES);
+  }
+  if (ad.splits > 1 && aw.splits > 1 && wsd == wsw) return TSPM_ERR_INVALID;  // counters / slabs would collide
+  L.dgx = L.gd.m / bm_of(ad);
+  L.dgy = cdiv(s->c, bn_of(ad));
+  L.wgx = cdiv(s->k, bm_of(aw));
+  L.wgy = s->r * s->s * s->c / bn_of(aw);
+  const size_t cmax = TSPM_COUNTER_BYTES / sizeof(unsigned);
+  if ((ad.splits > 1 && (size_t)L.dgx * L.dgy > cmax) || (aw.splits > 1 && (size_t)L.wgx * L.wgy > cmax))
+    return TSPM_ERR_INVALID;
+  L.dy = dy; L.w = w; L.x = x; L.dx = dx; L.dw = dw;
+  L.lds = std::max(lds_bytes(ad, false), lds_bytes(aw, false));
+  L.st = st;
+  bwd_dispatch(ad, aw, &L);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

@@ -54,6 +54,7 @@ class ConvOp:
     algo_fwd: L.ConvAlgo = field(default_factory=L.ConvAlgo)
     algo_dgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
     algo_wgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
+    bwd_fused: Optional[bool] = None  # tspm_conv_bwd_supported for (algo_dgrad, algo_wgrad); None = not asked
 
     @property
     def rows_out(self) -> int:
@@ -137,6 +138,9 @@ class EncoderEngine:
         self.fork_ds = True
         self.join_aux = True
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
+        # dgrad + wgrad of a conv as ONE launch (tspm_conv_bwd) when the tile pair is built in;
+        # TSPM_FUSE_BWD=0 keeps the two separate launches (A/B switch)
+        self.fuse_bwd = os.environ.get("TSPM_FUSE_BWD", "1") != "0"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -271,6 +275,7 @@ class EncoderEngine:
                 v = table.get((key,) + base)
                 if v is not None:
                     setattr(op, f"algo_{kind}", L.ConvAlgo(*v))
+            op.bwd_fused = None
         self._alloc_workspace()
 
     # ---------------------------------------------------------------------------------------
@@ -469,6 +474,33 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
+    def _bwd_pair(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, dx: torch.Tensor, beta: int,
+                  sh: int) -> bool:
+        """Input and weight gradient of ``op`` in one launch (tspm_conv_bwd: the two GEMMs read the same
+        dy and are independent, so their workgroups share the grid).  False (nothing launched) when
+        the pair is not built in, an auxiliary stream carries the weight gradients, or the transposed
+        wgrad operands are in use; the caller then launches the two separately."""
+        if not self.fuse_bwd or self.aux is not None or self.use_t:
+            return False
+        lib = L.lib()
+        if op.bwd_fused is None:
+            op.bwd_fused = bool(lib.tspm_conv_bwd_supported(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
+                                                            ctypes.byref(op.algo_wgrad), ctypes.byref(strides)))
+        if not op.bwd_fused:
+            return False
+        gw = self._grad(op.module.weight)
+        if not gw.is_contiguous(memory_format=torch.channels_last):
+            raise L.TspmError("conv weight grad must be OHWI (channels_last)")
+        if self.conv_timer:
+            self.conv_timer.begin(op, "bwd")
+        L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
+                                  x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
+                                  beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
+                                  self.ws_conv_aux.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
+        if self.conv_timer:
+            self.conv_timer.end()
+        return True
+
     def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "dgrad")
@@ -543,9 +575,11 @@ class EncoderEngine:
                 # identity residual: g' goes straight to the block-input gradient buffer
                 self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh, dy_t=bp.g_y2_t)
             s2 = bp.conv2.shape
-            self._wgrad(bp.conv2, bp.a1.data_ptr(), L.hwnc_strides(N, s2.h, s2.w, s2.c), d2, sh, bp.a1_t, bp.g_y2_t)
+            xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
-            self._dgrad(bp.conv2, d2, da1, 0, sh)
+            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh):
+                self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh, bp.a1_t, bp.g_y2_t)
+                self._dgrad(bp.conv2, d2, da1, 0, sh)
             d1 = bp.g_y1
             self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh, dy_t=bp.g_y1_t)
             if self.debug_hook is not None:
@@ -554,11 +588,13 @@ class EncoderEngine:
                 self.debug_hook(f"block{i}.d_a1", da1)
                 self.debug_hook(f"block{i}.d_y1", d1)
             xin_t = (self.blocks[i - 1].out_t if i > 0 else self.mp_t) if self.use_t else None
-            self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh, xin_t, bp.g_y1_t)
-            if bp.ds_conv is not None:
+            # the downsample's input gradient overwrites Gnv before conv1's accumulates onto it
+            if bp.ds_conv is not None and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
                 self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh, xin_t, bp.g_yd_t)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
-            self._dgrad(bp.conv1, d1, Gnv, 1, sh)
+            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh):
+                self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh, xin_t, bp.g_y1_t)
+                self._dgrad(bp.conv1, d1, Gnv, 1, sh)
             G, Gn = Gn, G
         if phase == 1:
             self._bw_state = (G, Gn)
