@@ -48,7 +48,7 @@ def step_ops(batch, dev, encoders=("audio", "image")):
                 kinds = (("fwd", op.algo_fwd), ("dgrad", op.algo_dgrad), ("wgrad", op.algo_wgrad))
             for kind, algo in kinds:
                 e = out.setdefault((kind,) + key, [s, xs, op is eng.stem, 0,
-                                                   (algo.tm, algo.tn, algo.wn, algo.wk, algo.splits)])
+                                                   (algo.tm, algo.tn, algo.wn, algo.wk, algo.splits, algo.variant)])
                 e[3] += 1
     return out
 

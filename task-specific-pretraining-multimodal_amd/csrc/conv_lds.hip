@@ -697,7 +697,7 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
 }
 
 // ---- fused dgrad + wgrad (k_bwd_lds): the (dgrad, wgrad) tile pairs built into the library are the
-// tm = tn = 1 wave layouts the batch-128/256 tuning picks (tuned/*.json): 3 for dgrad x 4 for wgrad
+// configurations the batch-128/256 tuning picks most (tuned/*.json): 5 for dgrad x 5 for wgrad
 struct BwdLaunch {
   ConvArgs gd, gw;
   const float *dy, *w, *x;
@@ -712,29 +712,32 @@ void bwd_go(const BwdLaunch& L) {
   hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kThreads), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
                      L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy);
 }
-bool is_cfg(const LdsAlgo& a, int wm, int wn, int wk) {
-  return a.tm == 1 && a.tn == 1 && a.wm == wm && a.wn == wn && a.wk == wk;
+bool is_cfg(const LdsAlgo& a, int tm, int wm, int wn, int wk) {
+  return a.tm == tm && a.tn == 1 && a.wm == wm && a.wn == wn && a.wk == wk;
 }
 template <class CD>
 bool bwd_w(const LdsAlgo& aw, const BwdLaunch* L) {  // L == nullptr: query only
-#define TSPM_BW(WM_, WN_, WK_)                                  \
-  if (is_cfg(aw, WM_, WN_, WK_)) {                              \
-    if (L) bwd_go<CD, Cfg<1, 1, WM_, WN_, WK_>>(*L);            \
+#define TSPM_BW(TM_, WM_, WN_, WK_)                             \
+  if (is_cfg(aw, TM_, WM_, WN_, WK_)) {                         \
+    if (L) bwd_go<CD, Cfg<TM_, 1, WM_, WN_, WK_>>(*L);          \
     return true;                                                \
   }
-  TSPM_BW(2, 2, 1)
-  TSPM_BW(1, 1, 4)
-  TSPM_BW(1, 2, 2)
-  TSPM_BW(2, 1, 2)
+  TSPM_BW(1, 2, 2, 1)
+  TSPM_BW(1, 1, 1, 4)
+  TSPM_BW(1, 1, 2, 2)
+  TSPM_BW(1, 2, 1, 2)
+  TSPM_BW(2, 2, 2, 1)
 #undef TSPM_BW
   return false;
 }
 bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
-#define TSPM_BD(WM_, WN_, WK_) \
-  if (is_cfg(ad, WM_, WN_, WK_)) return bwd_w<Cfg<1, 1, WM_, WN_, WK_>>(aw, L);
-  TSPM_BD(1, 2, 2)
-  TSPM_BD(1, 4, 1)
-  TSPM_BD(1, 1, 4)
+#define TSPM_BD(TM_, WM_, WN_, WK_) \
+  if (is_cfg(ad, TM_, WM_, WN_, WK_)) return bwd_w<Cfg<TM_, 1, WM_, WN_, WK_>>(aw, L);
+  TSPM_BD(1, 1, 2, 2)
+  TSPM_BD(1, 1, 4, 1)
+  TSPM_BD(1, 1, 1, 4)
+  TSPM_BD(2, 2, 2, 1)
+  TSPM_BD(2, 1, 4, 1)
 #undef TSPM_BD
   return false;
 }

@@ -271,11 +271,18 @@ class EncoderEngine:
             s = op.shape
             base = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride)
             wkind = "wgrad_t" if (self.use_t and op is not self.stem) else "wgrad"
+            tuned_bwd = False
             for kind, key in (("fwd", "fwd"), ("dgrad", "dgrad"), ("wgrad", wkind)):
                 v = table.get((key,) + base)
                 if v is not None:
                     setattr(op, f"algo_{kind}", L.ConvAlgo(*v))
+                    tuned_bwd = tuned_bwd or kind != "fwd"
+            pair = table.get(("bwd",) + base)
             op.bwd_fused = None
+            if pair is not None:  # the tuner found the fused launch faster: its (dgrad, wgrad) configs
+                op.algo_dgrad, op.algo_wgrad = L.ConvAlgo(*pair[:6]), L.ConvAlgo(*pair[6:12])
+            elif tuned_bwd:       # tuned, and the two separate launches won
+                op.bwd_fused = False
         self._alloc_workspace()
 
     # ---------------------------------------------------------------------------------------
