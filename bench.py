@@ -520,8 +520,8 @@ def main() -> None:
             "config": {"workload": "avmnist_late_fusion_train_step(resnet18_audio+resnet34_image+mlp_head, CE, Adam)",
                        "per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
-            "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_conv_fwd_vec/gather, k_conv_dgrad, "
-                                                    "k_conv_wgrad), fp32 MFMA 32x32x2",
+            "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_fwd_lds, k_bwd_lds = dgrad+wgrad, "
+                                                    "k_dgrad_lds, k_wgrad_lds, stem k_conv_*), fp32 MFMA 32x32x2",
                          "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per step of the conv family (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
