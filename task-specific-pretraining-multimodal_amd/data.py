@@ -60,6 +60,9 @@ def _np_safe_globals() -> list:
     try:
         from numpy._core.multiarray import _reconstruct
         out.append(_reconstruct)
+        # the reference's files were pickled under numpy 1.x, which names the function by its old
+        # module path; torch matches allow-list entries by that name
+        out.append((_reconstruct, "numpy.core.multiarray._reconstruct"))
     except ImportError:  # pragma: no cover - numpy 1.x
         pass
     try:

@@ -281,3 +281,20 @@ def test_reference_host_pipeline_matches_reference_batches(tmp_path, dgold, smal
         assert sha(b["audio"].numpy()) == str(dgold[f"c0_b{bi}_audio_sha256"])
         assert np.array_equal(b["image"].numpy(), dgold[f"c0_b{bi}_image"])
         assert np.array_equal(b["labels"].numpy(), dgold[f"c0_b{bi}_labels"])
+
+
+def test_reference_sample_files_load_weights_only():
+    """Two of the reference's own per-sample files (MML_Suite/AVMNIST/dataset, copied as fixtures):
+    the image is a numpy-1.x pickle, which the weights-only unpickler takes only with the allow-list
+    entry under the old module name numpy.core.multiarray._reconstruct (data._np_safe_globals)."""
+    import os
+    import numpy as np
+    import torch
+    from tspm_amd.data import _np_safe_globals, load_sample_file
+    g = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with torch.serialization.safe_globals(_np_safe_globals()):
+        img = load_sample_file(os.path.join(g, "ref_image_10000_10000_3.pt"))
+        spec = load_sample_file(os.path.join(g, "ref_spectrogram_0_01_0.pt"))
+    img = np.asarray(img)
+    assert img.shape == (28, 28) and np.issubdtype(img.dtype, np.integer) and 0 <= img.min() and img.max() <= 255
+    assert spec.shape == (32, 94) and spec.dtype == np.float32 and np.isfinite(spec).all() and spec.min() >= 0
