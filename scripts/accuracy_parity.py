@@ -196,9 +196,19 @@ def compare(out_path: str) -> None:
                      "ours_seed_spread_pp": round(100 * (max(last["ours_test_accuracy"]) -
                                                          min(last["ours_test_accuracy"])), 2)},
            "epochs": rows}
+    # less noisy summary: per run, the mean test accuracy of the last 3 epochs; then mean and standard
+    # error over the runs of each side
+    def tail3(curves):
+        v = np.array([np.mean([c[k]["test_accuracy"] for k in range(n - 3, n)]) for c in curves.values()])
+        return float(v.mean()), float(v.std(ddof=1) / np.sqrt(len(v))) if len(v) > 1 else float("nan")
+    (rm, rse), (om, ose) = tail3(ref), tail3(our)
+    doc["last3_epochs"] = {"reference_mean": round(rm, 5), "reference_stderr": round(rse, 5), "ours_mean": round(om, 5),
+                           "ours_stderr": round(ose, 5), "delta_pp": round(100 * (om - rm), 2),
+                           "delta_stderr_pp": round(100 * float(np.hypot(rse, ose)), 2)}
     with open(out_path, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc["final"], indent=1))
+    print(json.dumps(doc["last3_epochs"], indent=1))
 
 
 def main() -> None:
