@@ -124,6 +124,23 @@ class FusedAdam(torch.optim.Optimizer):
             L.check(lib.tspm_adam_step(fg.numel, fg.param.data_ptr(), fg.grad.data_ptr(), fg.exp_avg.data_ptr(),
                                        fg.exp_avg_sq.data_ptr(), fg.hyper.data_ptr(), stream_handle), "adam_step")
 
+    def launch_begin(self, stream_handle: int) -> None:
+        """Enqueue the device step-count increment of every group (before launch_ranges)."""
+        lib = L.lib()
+        for fg in self.flat_groups():
+            L.check(lib.tspm_adam_begin(fg.hyper.data_ptr(), stream_handle), "adam_begin")
+
+    def launch_ranges(self, stream_handle: int, ranges) -> None:
+        """Enqueue the fused update over element ranges [a, b) of each group's flat buffers
+        (``ranges[i]`` for group i; ranges start at parameter offsets, so they are 16-byte aligned).
+        Adam is element-wise: any partition of the buffer gives bitwise the result of ``launch``."""
+        lib = L.lib()
+        for fg, rs in zip(self.flat_groups(), ranges):
+            for a, b in rs:
+                L.check(lib.tspm_adam_step(b - a, fg.param[a:].data_ptr(), fg.grad[a:].data_ptr(),
+                                           fg.exp_avg[a:].data_ptr(), fg.exp_avg_sq[a:].data_ptr(),
+                                           fg.hyper.data_ptr(), stream_handle), "adam_step(range)")
+
     def note_steps(self, k: int = 1) -> None:
         for fg in self.flat_groups():
             fg.step += k

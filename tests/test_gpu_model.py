@@ -325,3 +325,23 @@ def test_fused_train_step_api_and_state_dict_roundtrip(gpu, tmp_path):
     m.eval(); m2.eval()
     with torch.no_grad():
         assert torch.equal(m(A=audio.to(gpu), I=image.to(gpu)), m2(A=audio.to(gpu), I=image.to(gpu)))
+
+
+def test_overlapped_adam_equals_plain_step(gpu):
+    """Single-GPU step with the late layers' Adam on a third stream, overlapping the early layers'
+    backward (FusedTrainStep.overlap_opt), is bitwise the plain step (Adam is element-wise), eager and
+    graph-replayed, parameters and optimizer state alike."""
+    results = []
+    for overlap in ("0", "stream", "main"):
+        torch.manual_seed(13)
+        ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
+        st = tspm_amd.FusedTrainStep(ours, opt, None, 32, use_graph=True)
+        st.overlap_opt = overlap
+        for i in range(4):
+            audio, image, labels, _ = orc.synthetic_batch(32, seed=70 + i)
+            st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+        torch.cuda.synchronize()
+        fg = opt.flat_groups()[0]
+        results.append(torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).cpu())
+    assert torch.equal(results[0], results[1]) and torch.equal(results[0], results[2])
