@@ -45,7 +45,30 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   const bool want_rs = g.rowsum != nullptr && tn == 0;
   f32x16 acc = {};
   float rs = 0.f;
-  for (int k0 = kb; k0 < ke; k0 += 8) {
+  // 4 reduction steps per round with all their loads issued before the MFMAs (the operands come from
+  // L2 with ~0.5-1 us latency; one step per round left every round waiting on its own loads).  Same
+  // MFMA / row-sum order as the one-step loop below, so results are bitwise unchanged.
+  constexpr int U = 4;
+  int k0 = kb;
+  for (; k0 + 8 * U <= ke; k0 += 8 * U) {
+    float a[U][4], b[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 8 * u + 2 * j + kh;
+        a[u][j] = mok ? Ap[(long long)k * g.sak] : 0.f;
+        b[u][j] = nok ? Bp[(long long)k * g.sbk] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc = mfma32(a[u][j], b[u][j], acc);
+        rs += a[u][j];
+      }
+  }
+  for (; k0 < ke; k0 += 8) {
     float a[4], b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
