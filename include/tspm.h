@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 9 */
+int tspm_abi_version(void);  /* 10 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -84,7 +84,12 @@ typedef struct tspm_strides4 {
  * last workgroup to finish each column block merges the partials in-launch (no tspm_bn_finalize
  * launch) and writes save_mean / save_invstd and the running statistics: counters = one uint32 per
  * 32 output channels, zero before first use (left zero after every launch).  With counters == NULL
- * only the partials are written (merge them with tspm_bn_finalize). */
+ * only the partials are written (merge them with tspm_bn_finalize).
+ * counters_len / partial_floats (ABI 10; 0 = the sizes above): when they reach
+ * tspm_conv_fwd_bn_counters / tspm_conv_fwd_bn_partial_floats, a layer with too many tiles for one
+ * merging workgroup is merged in two levels inside the launch (groups of tiles by their group's
+ * last workgroup into a second partial array after the first, then the groups by the last group)
+ * instead of by a tspm_bn_finalize launch. */
 typedef struct tspm_bn_fuse {
   float* partial;
   uint32_t* counters;
@@ -93,6 +98,9 @@ typedef struct tspm_bn_fuse {
   float momentum, eps;
   float* save_mean;
   float* save_invstd;
+  int32_t counters_len;
+  int32_t reserved_;
+  int64_t partial_floats;
 } tspm_bn_fuse;
 
 /* y[P,Q,N,K] = conv(x, w).  y is HWNC.  bn: NULL, or the BatchNorm statistics to produce from the
@@ -104,6 +112,10 @@ int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, cons
                   void* workspace, size_t workspace_bytes, tspm_stream_t stream);
 int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+/* Buffer sizes that enable the two-level in-launch BN merge (tspm_bn_fuse.counters_len /
+ * partial_floats) for this shape and algo. */
+int32_t tspm_conv_fwd_bn_counters(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 size_t tspm_conv_fwd_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
 /* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}.  Workspace

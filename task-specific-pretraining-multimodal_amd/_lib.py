@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -46,7 +46,8 @@ class BnFuse(Structure):
     """tspm_bn_fuse: BatchNorm statistics produced by the conv forward epilogue."""
     _fields_ = [("partial", c_void_p), ("counters", c_void_p), ("running_mean", c_void_p),
                 ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float), ("save_mean", c_void_p),
-                ("save_invstd", c_void_p)]
+                ("save_invstd", c_void_p), ("counters_len", c_int32), ("reserved_", c_int32),
+                ("partial_floats", c_int64)]
 
 
 class AdamHyper(Structure):
@@ -66,6 +67,8 @@ _SIGS = {
                                 _P, c_size_t, _P]),
     "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_fwd_bn_counters": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_fwd_bn_partial_floats": (c_int64, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_dgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, _P, _P, c_int32, _P, c_size_t, _P]),
     "tspm_conv_dgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),

@@ -113,28 +113,31 @@ TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag) {
 // ONE workgroup whose size is a power-of-two multiple of CB.  Writes save_mean / save_invstd and
 // updates the running statistics (momentum, unbiased variance) like nn.BatchNorm2d.
 // `red` must hold blockDim.x doubles, `smu` CB doubles (LDS).
-TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const float* part, int c0, int CB,
-                             float* rmean, float* rvar, float momentum, float eps, float* smean, float* sinv,
-                             double* red, double* smu) {
+//
+// bn_merge_range is the merge itself over tiles [g_lo, g_hi) of a partial array with G_all tiles:
+// returns (in the threads with t < CB) the range's mean and sum of squared deviations in double.
+TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
+                             int c0, int CB, double* red, double* smu, double& mean_out, double& m2_out) {
   const int t = threadIdx.x, T = blockDim.x;
   const int GG = T / CB, cl = t % CB, gg = t / CB;
   const int c = c0 + cl;
   const bool cok = c < C;
-  const long long plane = (long long)G * C;
-  // tiles gg, gg+GG, ... in batches of 8 independent loads (the reads follow an acquire: they
-  // miss in cache, so issue them together)
+  const long long plane = (long long)G_all * C;
+  const long long n_rows = min((long long)g_hi * rpt, M) - (long long)g_lo * rpt;
+  // tiles g_lo+gg, g_lo+gg+GG, ... in batches of 8 independent loads (the reads follow an acquire:
+  // they miss in cache, so issue them together)
   auto tile_mean = [&](int g, double& nb, double& mb) {
     nb = (double)min(rpt, M - (long long)g * rpt);
     mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
   };
   double s = 0.0;
   if (cok)
-    for (int g0 = gg; g0 < G; g0 += 8 * GG) {
+    for (int g0 = g_lo + gg; g0 < g_hi; g0 += 8 * GG) {
       double nb[8], mb[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int g = g0 + u * GG;
-        if (g < G) tile_mean(g, nb[u], mb[u]); else { nb[u] = 0.0; mb[u] = 0.0; }
+        if (g < g_hi) tile_mean(g, nb[u], mb[u]); else { nb[u] = 0.0; mb[u] = 0.0; }
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += nb[u] * mb[u];
@@ -145,17 +148,17 @@ TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const flo
     if (gg < w) red[t] += red[t + w * CB];
     __syncthreads();
   }
-  if (gg == 0) smu[cl] = red[cl] / (double)M;
+  if (gg == 0) smu[cl] = red[cl] / (double)n_rows;
   __syncthreads();
   const double mean = smu[cl];
   double q = 0.0;
   if (cok)
-    for (int g0 = gg; g0 < G; g0 += 8 * GG) {
+    for (int g0 = g_lo + gg; g0 < g_hi; g0 += 8 * GG) {
       double nb[8], mb[8], m2b[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int g = g0 + u * GG;
-        if (g < G) {
+        if (g < g_hi) {
           tile_mean(g, nb[u], mb[u]);
           m2b[u] = (double)part[2 * plane + (long long)g * C + c];
         } else {
@@ -171,16 +174,44 @@ TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const flo
     if (gg < w) red[t] += red[t + w * CB];
     __syncthreads();
   }
-  if (gg == 0 && cok) {
+  mean_out = mean;
+  m2_out = red[cl];
+  __syncthreads();  // red is reused by the caller's next merge
+}
+
+// First level of a two-level merge: tiles [g_lo, g_hi) of `part` (G_all tiles) into ONE tile
+// `g_out` of `part1` (G1 tiles) in the same {K, mean-K, M2} format (K = mean rounded to float, so
+// mean-K carries the rounding residual), written through (sc1) for the second-level merger.
+TSPM_DEV void bn_merge_level1(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
+                              int c0, int CB, float* part1, int G1, int g_out, double* red, double* smu) {
+  double mean, m2;
+  bn_merge_range(M, C, G_all, rpt, part, g_lo, g_hi, c0, CB, red, smu, mean, m2);
+  const int t = threadIdx.x, c = c0 + t;
+  if (t < CB && c < C) {
+    const long long plane1 = (long long)G1 * C, o = (long long)g_out * C + c;
+    const float K = (float)mean;
+    __hip_atomic_store(part1 + o, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part1 + plane1 + o, (float)(mean - (double)K), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part1 + 2 * plane1 + o, (float)m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const float* part, int c0, int CB,
+                             float* rmean, float* rvar, float momentum, float eps, float* smean, float* sinv,
+                             double* red, double* smu) {
+  double mean, m2;
+  bn_merge_range(M, C, G, rpt, part, 0, G, c0, CB, red, smu, mean, m2);
+  const int cl = threadIdx.x, c = c0 + cl;
+  if (cl < CB && c < C) {
     const double n = (double)M;
-    double var = red[cl] / n;
+    double var = m2 / n;
     if (var < 0.0) var = 0.0;
     const float fmean = (float)mean, fvar = (float)var;
     smean[c] = fmean;
     sinv[c] = 1.0f / sqrtf(fvar + eps);
     if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
     if (rvar) {
-      const float unb = M > 1 ? (float)(red[cl] / (n - 1.0)) : fvar;
+      const float unb = M > 1 ? (float)(m2 / (n - 1.0)) : fvar;
       rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
     }
   }

@@ -720,6 +720,18 @@ extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_
   return is_lds(user) ? user->tm * 32 : fwd_algo(s, user).tm * 32;
 }
 
+extern "C" int32_t tspm_conv_fwd_bn_counters(const tspm_conv_shape* s, const tspm_conv_algo* user) {
+  if (!shape_ok(s)) return 0;
+  const int single = cdiv(s->k, 32);
+  return is_lds(user) ? std::max(single, tspm_detail::lds_fwd_bn_counters(s, lds_algo(user))) : single;
+}
+
+extern "C" int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* s, const tspm_conv_algo* user) {
+  if (!shape_ok(s)) return 0;
+  if (is_lds(user)) return tspm_detail::lds_fwd_bn_partial_floats(s, lds_algo(user));
+  return 3LL * tspm_conv_fwd_tiles(s, user) * s->k;
+}
+
 extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
                              const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn, void* ws,
                              size_t ws_bytes, tspm_stream_t stream) {

@@ -224,6 +224,8 @@ bool lds_fwd_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const 
 bool lds_dgrad_supported(const tspm_conv_shape* s, const LdsAlgo& a);
 bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
 size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
+int lds_fwd_bn_counters(const tspm_conv_shape* s, const LdsAlgo& a);
+long long lds_fwd_bn_partial_floats(const tspm_conv_shape* s, const LdsAlgo& a);
 size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
 size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,

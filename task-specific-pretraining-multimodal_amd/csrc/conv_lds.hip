@@ -244,7 +244,7 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 template <class C>
 __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y,
-                                                     tspm_bn_fuse bf, float* __restrict__ slabs) {
+                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
   extern __shared__ float lds[];
   TSPM_STAMP(tspm_g_stamps_lds, 0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -316,11 +316,30 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
   if (bf.counters) {
-    if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, reinterpret_cast<int*>(lds))) return;
+    int* flag = reinterpret_cast<int*>(lds);
     double* red = reinterpret_cast<double*>(lds) + 2;
     double* smu = red + kThreads;
-    bn_merge_block(g.m, K, gridDim.x * C::WM, C::TM * 32, bf.partial, n0col, C::BN, bf.running_mean,
-                   bf.running_var, bf.momentum, bf.eps, bf.save_mean, bf.save_invstd, red, smu);
+    const int T = gridDim.x * C::WM;
+    const float* part = bf.partial;
+    int G = T;
+    long long rpt = C::TM * 32;
+    if (ng > 0) {
+      // two levels: the last workgroup of each group of gw row blocks merges the group's tiles into
+      // one tile of the second array; the last group merges those
+      const int grp = blockIdx.x / gw;
+      const int x0 = grp * gw, x1 = min((int)gridDim.x, x0 + gw);
+      if (!last_arriver(bf.counters + gridDim.y + blockIdx.y * ng + grp, (unsigned)(x1 - x0), flag)) return;
+      float* part1 = bf.partial + 3LL * T * K;
+      bn_merge_level1(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu);
+      if (!last_arriver(bf.counters + blockIdx.y, (unsigned)ng, flag)) return;
+      part = part1;
+      G = ng;
+      rpt = (long long)gw * C::WM * C::TM * 32;
+    } else if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, flag)) {
+      return;
+    }
+    bn_merge_block(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
+                   bf.save_mean, bf.save_invstd, red, smu);
   }
 }
 
@@ -588,6 +607,22 @@ size_t splitk_ws(int splits, long long rows, long long cols) {
   TSPM_LDS_WAVES(2, 2, FN)      \
   return TSPM_ERR_INVALID;
 
+// BN merge plan of a forward launch: ng == 0 one level (<= 16 tiles per merging thread); ng > 0
+// two levels, first-level groups of gw row blocks (<= 8 tiles per merging thread) and ng groups
+// (<= 16 per thread); ng < 0 none fits (tspm_bn_finalize).
+struct BnLevels {
+  int gw, ng;
+};
+BnLevels bn_levels(const tspm_conv_shape* s, const LdsAlgo& a) {
+  const int bnn = bn_of(a), groups = kThreads / bnn;
+  const int gx = (s->p * s->q * s->n) / bm_of(a);
+  if (cdiv(gx * a.wm, groups) <= 16) return BnLevels{0, 0};
+  const int gw = std::max(1, 8 * groups / a.wm);
+  const int ng = cdiv(gx, gw);
+  if (cdiv(ng, groups) > 16) return BnLevels{0, -1};
+  return BnLevels{gw, ng};
+}
+
 }  // namespace
 
 namespace tspm_detail {
@@ -610,6 +645,15 @@ bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, cons
 }
 size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, (long long)s->p * s->q * s->n, s->k);
+}
+int lds_fwd_bn_counters(const tspm_conv_shape* s, const LdsAlgo& a) {
+  const BnLevels lv = bn_levels(s, a);
+  return cdiv(s->k, bn_of(a)) * (1 + std::max(lv.ng, 0));
+}
+long long lds_fwd_bn_partial_floats(const tspm_conv_shape* s, const LdsAlgo& a) {
+  const BnLevels lv = bn_levels(s, a);
+  const long long tiles = (long long)(s->p * s->q * s->n) / (a.tm * 32);
+  return 3LL * (tiles + std::max(lv.ng, 0)) * s->k;
 }
 size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, (long long)s->h * s->w * s->n, s->c);
@@ -634,12 +678,19 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
   const int bm = bm_of(a), bnn = bn_of(a);
   const dim3 grid(g.m / bm, cdiv(s->k, bnn), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
-  // in-launch BN merge only when each merging thread reads few tiles (else tspm_bn_finalize)
-  const int tiles = (int)grid.x * a.wm, groups = kThreads / bnn;
+  // in-launch BN merge: one level when each merging thread reads few tiles, two levels when the
+  // caller's buffers allow it (tspm_bn_fuse.counters_len / partial_floats), else tspm_bn_finalize
+  const int tiles = (int)grid.x * a.wm;
+  const BnLevels lv = bn_levels(s, a);
   const tspm_bn_fuse want = bf;
-  if (bf.counters && cdiv(tiles, groups) > 16) bf.counters = nullptr;
+  if (bf.counters && lv.ng != 0) {
+    const bool room = lv.ng > 0 && bf.counters_len >= (long long)grid.y * (1 + lv.ng) &&
+                      bf.partial_floats >= 3LL * (tiles + lv.ng) * s->k;
+    if (!room) bf.counters = nullptr;
+  }
+  const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
   const size_t lds = lds_bytes(a, bf.counters != nullptr);
-#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, w, y, bf, slabs)
+#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, w, y, bf, slabs, gw, ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;

@@ -74,6 +74,12 @@ class ConvOp:
             b = max(b, lib.tspm_conv_dgrad_workspace(ctypes.byref(self.shape), ctypes.byref(self.algo_dgrad)))
         return b
 
+    def bn_counters(self) -> int:
+        return L.lib().tspm_conv_fwd_bn_counters(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd))
+
+    def bn_partial_floats(self) -> int:
+        return L.lib().tspm_conv_fwd_bn_partial_floats(ctypes.byref(self.shape), ctypes.byref(self.algo_fwd))
+
     def stat_tiles(self) -> Tuple[int, int]:
         """(tiles, rows per tile) of the BN partial statistics the forward epilogue emits."""
         lib = L.lib()
@@ -141,6 +147,11 @@ class EncoderEngine:
         # dgrad + wgrad of a conv as ONE launch (tspm_conv_bwd) when the tile pair is built in;
         # TSPM_FUSE_BWD=0 keeps the two separate launches (A/B switch)
         self.fuse_bwd = os.environ.get("TSPM_FUSE_BWD", "1") != "0"
+        # BN statistics of layers with many row tiles merged in two levels inside the conv launch
+        # instead of by a tspm_bn_finalize launch (TSPM_BN_TWO_LEVEL=1).  Off by default: measured at
+        # batch 128 the merge tail on the conv's critical path costs more than the finalize launch
+        # (2.88 vs 2.83 ms per step)
+        self.bn_two_level = os.environ.get("TSPM_BN_TWO_LEVEL", "0") == "1"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -256,13 +267,15 @@ class EncoderEngine:
         self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_conv_aux = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
-        ncnt = max(op.shape.k for op in self.all_convs()) // 32 + 1
-        self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
-        self.bn_cnt_aux = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
-        part = max(3 * op.stat_tiles()[0] * op.shape.k for op in self.all_convs())
-        self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
+        # BN statistics merged in-launch (one or two levels, tspm_conv_fwd_bn_counters / _partial_floats)
         ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
-        part_ds = max([3 * op.stat_tiles()[0] * op.shape.k for op in ds] + [1])
+        ncnt = max(op.bn_counters() for op in self.all_convs())
+        ncnt_ds = max([op.bn_counters() for op in ds] + [1])
+        self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
+        self.bn_cnt_aux = torch.zeros(ncnt_ds, device=self.device, dtype=torch.int32)
+        part = max(op.bn_partial_floats() for op in self.all_convs())
+        self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
+        part_ds = max([op.bn_partial_floats() for op in ds] + [1])
         self.bn_part_aux = torch.empty(part_ds, device=self.device, dtype=torch.float32)
 
     def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
@@ -314,7 +327,8 @@ class EncoderEngine:
         part, cnt = (self.bn_part_aux, self.bn_cnt_aux) if aux else (self.bn_part, self.bn_cnt)
         bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
                        BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                       bn.invstd.data_ptr())
+                       bn.invstd.data_ptr(), cnt.numel() if self.bn_two_level else 0, 0,
+                       part.numel() if self.bn_two_level else 0)
         self._conv_fwd(op, x_ptr, strides, y, sh, bnf, aux)
 
     def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,

@@ -57,9 +57,10 @@ def zeroed_counters(k: int, dev) -> torch.Tensor:
 
 
 def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0), fused=True, counters=None,
-                        running=None):
+                        running=None, two_level=False):
     """conv forward whose epilogue emits BN partials — merged in-launch by the last workgroup of
-    each channel block (fused) or by tspm_bn_finalize — returns (y NCHW, mean, invstd)."""
+    each channel block (fused; with two_level, the buffers sized for the two-level merge) or by
+    tspm_bn_finalize — returns (y NCHW, mean, invstd)."""
     n, c, h, w = x_nchw.shape
     k, _, r, s = w_oihw.shape
     shp = shape(n, h, w, c, k, r, s, stride, pad)
@@ -73,14 +74,21 @@ def conv_fwd_with_stats(x_nchw, w_oihw, stride, pad, algo=(0, 0, 0, 0, 0), fused
     lib = L.lib()
     tiles = lib.tspm_conv_fwd_tiles(ctypes.byref(shp), ctypes.byref(a))
     rows = lib.tspm_conv_fwd_tile_rows(ctypes.byref(shp), ctypes.byref(a))
-    part = torch.empty(3 * tiles * k, device=dev)
+    nfl = lib.tspm_conv_fwd_bn_partial_floats(ctypes.byref(shp), ctypes.byref(a)) if two_level else 3 * tiles * k
+    part = torch.empty(nfl, device=dev)
     mean = torch.empty(k, device=dev)
     inv = torch.empty(k, device=dev)
     rm, rv = running if running is not None else (None, None)
     if fused:
-        cnt = counters if counters is not None else zeroed_counters(k, dev)
+        if counters is not None:
+            cnt = counters
+        elif two_level:
+            cnt = torch.zeros(lib.tspm_conv_fwd_bn_counters(ctypes.byref(shp), ctypes.byref(a)), dtype=torch.int32,
+                              device=dev)
+        else:
+            cnt = zeroed_counters(k, dev)
         bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(rm), L.ptr(rv), 0.1, 1e-5, mean.data_ptr(),
-                       inv.data_ptr())
+                       inv.data_ptr(), cnt.numel() if two_level else 0, 0, nfl if two_level else 0)
     else:
         bnf = L.BnFuse(part.data_ptr(), None, None, None, 0.1, 1e-5, None, None)
     wsb = lib.tspm_conv_fwd_workspace(ctypes.byref(shp), ctypes.byref(a))

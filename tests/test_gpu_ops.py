@@ -517,6 +517,50 @@ def test_fused_bn_counters_rearm_and_running_stats(gpu):
     assert torch.allclose(rv.double().cpu(), rv_ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("case,algo", [
+    ((128, 64, 8, 24, 64, 3, 3, 1, 1), (2, 1, 1, 4, 1, 1)),    # 384 tiles, 64-channel blocks
+    ((128, 64, 7, 7, 64, 3, 3, 1, 1), (1, 1, 2, 2, 1, 1)),     # 196 tiles: last group short
+    ((128, 128, 4, 4, 128, 3, 3, 1, 1), (1, 1, 4, 1, 4, 1)),   # 128-channel blocks, split-K
+    ((128, 32, 9, 11, 32, 3, 3, 1, 1), (1, 1, 1, 4, 1, 1)),    # 396 tiles: last group short, 32-channel blocks
+])
+@pytest.mark.parametrize("offset", [0.0, 3e4])
+def test_conv_fwd_two_level_bn_merge(gpu, case, algo, offset):
+    """Layers with too many row tiles for one merging workgroup: the two-level in-launch merge (no
+    tspm_bn_finalize launch) gives the statistics of the finalize path to within float rounding of
+    a double result, is deterministic, re-arms its counters and updates the running statistics."""
+    from abi_helpers import conv_fwd_with_stats
+    from tspm_amd import _lib as L
+    n, c, h, w, k, r, s_, st, pad = case
+    lib = L.lib()
+    shp = L.ConvShape(n, h, w, c, k, r, s_, st, pad, (h + 2 * pad - r) // st + 1, (w + 2 * pad - s_) // st + 1)
+    a = L.ConvAlgo(*algo)
+    assert lib.tspm_conv_fwd_bn_counters(ctypes.byref(shp), ctypes.byref(a)) > (k + 31) // 32, "not a two-level case"
+    g = torch.Generator().manual_seed(41)
+    x = (torch.randn(n, c, h, w, generator=g) + offset / 100).to(gpu)
+    wt = torch.randn(k, c, r, s_, generator=g) * 0.05
+    wt[:, :, r // 2, s_ // 2] += offset / (c * 100)
+    wt = wt.to(gpu)
+    runs = []
+    for two in (True, True, False):
+        rm, rv = torch.zeros(k, device=gpu), torch.ones(k, device=gpu)
+        y, mean, inv = conv_fwd_with_stats(x, wt, st, pad, algo, fused=True, running=(rm, rv), two_level=two)
+        torch.cuda.synchronize()
+        runs.append((y, mean, inv, rm, rv))
+    for t1, t2 in zip(runs[0], runs[1]):
+        assert torch.equal(t1, t2)
+    yd = runs[0][0].double().cpu()
+    mean_ref = yd.mean((0, 2, 3))
+    var_ref = yd.var((0, 2, 3), unbiased=False)
+    scale = yd.abs().amax((0, 2, 3)) + 1
+    for y, mean, inv, rm, rv in (runs[0], runs[2]):
+        assert ((mean.double().cpu() - mean_ref).abs() <= 1e-6 * scale).all()
+        assert torch.allclose(inv.double().cpu(), 1 / torch.sqrt(var_ref + 1e-5), rtol=1e-4)
+        assert torch.allclose(rv.double().cpu(), 0.9 + 0.1 * yd.var((0, 2, 3), unbiased=True), rtol=1e-5)
+    # two-level vs finalize: both merge in double, so they agree to float rounding
+    assert torch.allclose(runs[0][1], runs[2][1], rtol=2e-7, atol=1e-6 * float(scale.max()))
+    assert torch.allclose(runs[0][2], runs[2][2], rtol=1e-6)
+
+
 def test_wgrad_split_counters_rearm(gpu):
     """Split-K weight gradient with the in-launch slab reduction: repeated calls of different split
     counts through ONE zeroed workspace stay within the fp32 bound of the fp64 result (the last
