@@ -48,8 +48,8 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   // 4 reduction steps per round with all their loads issued before the MFMAs (the operands come from
   // L2 with ~0.5-1 us latency; one step per round left every round waiting on its own loads).  Same
   // MFMA / row-sum order as the one-step loop below, so results are bitwise unchanged.
-  constexpr int U = 4;
   int k0 = kb;
+  constexpr int U = 4;
   for (; k0 + 8 * U <= ke; k0 += 8 * U) {
     float a[U][4], b[U][4];
 #pragma unroll
@@ -125,9 +125,7 @@ int gemm_small(const GemmArgs& g, hipStream_t st) {
   switch (wk) {
     case 1: hipLaunchKernelGGL(k_gemm_small<1>, dim3(tiles), dim3(64), lds, st, g); break;
     case 2: hipLaunchKernelGGL(k_gemm_small<2>, dim3(tiles), dim3(128), lds, st, g); break;
-    case 4: hipLaunchKernelGGL(k_gemm_small<4>, dim3(tiles), dim3(256), lds, st, g); break;
-    case 8: hipLaunchKernelGGL(k_gemm_small<8>, dim3(tiles), dim3(512), lds, st, g); break;
-    default: hipLaunchKernelGGL(k_gemm_small<16>, dim3(tiles), dim3(1024), lds, st, g); break;
+    default: hipLaunchKernelGGL(k_gemm_small<4>, dim3(tiles), dim3(256), lds, st, g); break;
   }
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
