@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-int tspm_abi_version(void);  /* 10 */
+int tspm_abi_version(void);  /* 11 */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
 
@@ -329,6 +329,39 @@ int tspm_classify_update_ex(int32_t n, int32_t classes, const float* logits, con
 /* Sum `nslab` slabs of `count` floats (slab_stride apart) into out (deterministic slab order). */
 int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs, float* out,
                       tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * MMIMDb late-fusion path (BASELINE configs[3]; ABI 11).  The encoders (BatchNorm1d + Linear,
+ * models/mmimdb.py:63-93) and the MaxOut / output projections reuse tspm_bn_* (m = batch rows, HW = 1)
+ * and tspm_linear_*; these entry points add the pieces around them.
+ * ----------------------------------------------------------------------------------------------*/
+/* GatedBiModalNetwork.forward (models/gates/gated_bimodal.py): u[n,2d] holds fc_one(x1) in columns
+ * [0,d) and fc_two(x2) in [d,2d).  h = tanh(u) (the concatenated features, [n,2d], kept for the
+ * backward), gate[r] = sigmoid(sum_j wz[j]*h[r,j]) (hidden_sigmoid, no bias),
+ * z[r,j] = gate*h[r,j] + (1-gate)*h[r,d+j]. */
+int tspm_gmu_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const float* wz, float* h, int32_t ldh,
+                 float* gate, float* z, int32_t ldz, tspm_stream_t stream);
+/* Backward of tspm_gmu_fwd: du[n,2d] (gradient of both projections' outputs) and ds[n] (gradient of
+ * the gate pre-activation; hidden_sigmoid.weight.grad = ds^T @ h via tspm_linear_bwd_weight). */
+int tspm_gmu_bwd(int32_t n, int32_t d, const float* dz, int32_t lddz, const float* h, int32_t ldh,
+                 const float* gate, const float* wz, float* du, int32_t lddu, float* ds, tspm_stream_t stream);
+/* MaxOut(num_units=2) (models/maxout.py) + the Dropout after it (models/mmimdb.py:40-45): a[n,2d] is
+ * the product with both units' weights stacked ([2d, in] — layers.0.weight then layers.1.weight);
+ * y = max(a[:, :d], a[:, d:]) * (keep ? keep_scale : 0)  (keep NULL: no dropout). */
+int tspm_maxout_fwd(int32_t n, int32_t d, const float* a, int32_t lda, const uint8_t* keep, float keep_scale,
+                    float* y, int32_t ldy, tspm_stream_t stream);
+/* da[n,2d] from dy: the unit holding the max receives the (dropout-masked) gradient; ties split it in
+ * half (ATen's derivative of torch.maximum). */
+int tspm_maxout_bwd(int32_t n, int32_t d, const float* dy, int32_t lddy, const float* a, int32_t lda,
+                    const uint8_t* keep, float keep_scale, float* da, int32_t ldda, tspm_stream_t stream);
+/* BCEWithLogitsLoss (mean) — LossFunctionGroup{bce_with_logits: w} (experiment_utils/loss.py:52,
+ * configs/mmimdb/centralised/mmimdb_baseline.yaml): loss[0] = grad_scale * mean((1-t)*x - logsigmoid(x)),
+ * dlogits = (sigmoid(x) - t) * grad_scale / (n*classes) (nullable).  If stats != NULL (3 + 3*classes
+ * floats, accumulated): [0] += loss*n, [1] += n, [2] += sum of per-sample F1 (zero_division 0),
+ * [3+3k .. 5+3k] += tp, fp, fn of class k, with prediction = sigmoid(x) > threshold
+ * (models/mmimdb.py:236-237). */
+int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float* targets, float* loss,
+                    float* dlogits, float grad_scale, float threshold, float* stats, tspm_stream_t stream);
 
 #ifdef __cplusplus
 }

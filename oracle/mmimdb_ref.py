@@ -1,0 +1,153 @@
+"""TEST INFRASTRUCTURE ONLY — CPU restatement of the reference's MMIMDb late-fusion train step
+(BASELINE configs[3]).  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it; the product path never does.
+
+Restates, with plain ``torch.nn`` / ``torch.nn.functional`` on the CPU:
+  * ``MMIMDbModalityEncoder``  = BatchNorm1d(in) → Linear(in, out)          (MML_Suite/models/mmimdb.py:63-93)
+  * ``GatedBiModalNetwork``    = tanh(fc_one), tanh(fc_two), sigmoid(hidden_sigmoid(cat)),
+                                 g*h1 + (1-g)*h2, no biases                    (models/gates/gated_bimodal.py)
+  * ``MLPGenreClassifier``     = BN → MaxOut(2, no bias) → Dropout(.5) → BN → MaxOut → Dropout → BN → Linear
+                                                                               (models/mmimdb.py:20-60, models/maxout.py)
+  * ``MMIMDb.forward`` / ``train_step``: BCEWithLogits(mean) × weight 1.0, Adam (lr 1e-5, wd 1e-3)
+                                                                               (models/mmimdb.py:164-245,
+                                                                                configs/mmimdb/centralised/mmimdb_baseline.yaml)
+Module attribute names follow the reference so ``state_dict`` keys are identical; construction order
+(image encoder, text encoder, GMU, classifier) follows the YAML, so ``torch.manual_seed(s)`` before
+construction reproduces the reference's initial weights.  Dropout takes explicit keep masks.
+
+Pinned: ``tests/golden/mmimdb_step_b4.npz`` was produced by the REAL reference modules imported in the
+build container (``tests/golden/make_mmimdb_golden.py``); ``tests/test_oracle_golden.py`` checks this
+restatement against it.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+IMAGE_DIM, TEXT_DIM, EMBED, HIDDEN, GENRES = 4096, 300, 512, 512, 23
+
+
+class OracleMaxOut(nn.Module):
+    def __init__(self, i: int, o: int, units: int = 2, bias: bool = False):
+        super().__init__()
+        self.layers = nn.ModuleList([nn.Linear(i, o, bias=bias) for _ in range(units)])
+
+    def forward(self, x):
+        y = self.layers[0](x)
+        for l in self.layers[1:]:
+            y = torch.max(y, l(x))
+        return y
+
+
+class OracleEncoder(nn.Module):
+    def __init__(self, i: int, o: int):
+        super().__init__()
+        self.net = nn.Sequential(nn.BatchNorm1d(i), nn.Linear(i, o))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class OracleGMU(nn.Module):
+    def __init__(self, d1: int, d2: int, o1: int, o2: int):
+        super().__init__()
+        self.fc_one = nn.Linear(d1, o1, bias=False)
+        self.fc_two = nn.Linear(d2, o2, bias=False)
+        self.hidden_sigmoid = nn.Linear(o1 + o2, 1, bias=False)
+
+    def forward(self, a, b):
+        h1 = torch.tanh(self.fc_one(a))
+        h2 = torch.tanh(self.fc_two(b))
+        g = torch.sigmoid(self.hidden_sigmoid(torch.cat([h1, h2], dim=1)))
+        return g.view(g.size(0), 1) * h1 + (1 - g).view(g.size(0), 1) * h2
+
+
+class OracleClassifier(nn.Module):
+    def __init__(self, i: int, o: int, h: int):
+        super().__init__()
+        self.net = nn.Sequential(nn.BatchNorm1d(i), OracleMaxOut(i, h), nn.Dropout(0.5), nn.BatchNorm1d(h),
+                                 OracleMaxOut(h, h), nn.Dropout(0.5), nn.BatchNorm1d(h), nn.Linear(h, o))
+
+    def forward(self, x, keep1=None, keep2=None):
+        n = self.net
+        x = n[1](n[0](x))
+        x = _dropout(x, keep1, self.training)
+        x = n[4](n[3](x))
+        x = _dropout(x, keep2, self.training)
+        return n[7](n[6](x))
+
+
+def _dropout(x, keep, training):
+    if not training:
+        return x
+    if keep is None:
+        return F.dropout(x, 0.5, True)
+    return x * (keep.to(x.dtype) * 2.0)  # ATen: input * (bernoulli(1-p) / (1-p))
+
+
+class OracleMMIMDb(nn.Module):
+    def __init__(self, image_dim=IMAGE_DIM, text_dim=TEXT_DIM, embed=EMBED, hidden=HIDDEN, genres=GENRES):
+        super().__init__()
+        self.image_model = OracleEncoder(image_dim, embed)
+        self.text_model = OracleEncoder(text_dim, embed)
+        self.fusion_module = OracleGMU(embed, embed, embed, embed)
+        self.mm_mlp = OracleClassifier(embed, genres, hidden)
+
+    def forward(self, I, T, keep1=None, keep2=None):
+        return self.mm_mlp(self.fusion_module(self.image_model(I), self.text_model(T)), keep1, keep2)
+
+
+def build_oracle_mmimdb(seed: int = 0, **dims) -> OracleMMIMDb:
+    torch.manual_seed(seed)
+    return OracleMMIMDb(**dims)
+
+
+def synthetic_batch(n: int, seed: int = 1234, image_dim=IMAGE_DIM, text_dim=TEXT_DIM, genres=GENRES):
+    """MM-IMDb-shaped features: VGG16 fc7 image features (non-negative, ReLU output) and
+    mean word2vec text features; multi-hot genre labels with at least one genre per movie."""
+    g = torch.Generator().manual_seed(seed)
+    image = torch.relu(torch.randn(n, image_dim, generator=g))
+    text = 0.1 * torch.randn(n, text_dim, generator=g)
+    labels = (torch.rand(n, genres, generator=g) < 0.15).float()
+    first = torch.randint(0, genres, (n,), generator=g)
+    labels[torch.arange(n), first] = 1.0
+    return image, text, labels
+
+
+def bce_loss(logits, labels):
+    return F.binary_cross_entropy_with_logits(logits, labels)
+
+
+def train_step(model: OracleMMIMDb, opt, image, text, labels, keep1=None, keep2=None) -> Dict[str, torch.Tensor]:
+    """models/mmimdb.py:203-245 (minus the host metric recorder): zero_grad, forward, BCE, backward, Adam."""
+    model.train()
+    for p in model.parameters():
+        p.grad = None
+    logits = model(image, text, keep1, keep2)
+    loss = bce_loss(logits, labels)
+    loss.backward()
+    opt.step()
+    return {"loss": loss.detach(), "logits": logits.detach()}
+
+
+def f1_counts(logits: torch.Tensor, labels: torch.Tensor, threshold: float = 0.5) -> List[float]:
+    """The device metric counts of tspm_bce_logits (without the loss slots) restated on the CPU."""
+    p = torch.sigmoid(logits) > threshold
+    y = labels > 0.5
+    tp, fp, fn = (p & y).sum(1), (p & ~y).sum(1), (~p & y).sum(1)
+    den = 2 * tp + fp + fn
+    f1 = torch.where(den > 0, 2 * tp.double() / den.clamp(min=1), torch.zeros_like(den, dtype=torch.double))
+    out = [float(f1.sum())]
+    for k in range(logits.shape[1]):
+        pk, yk = p[:, k], y[:, k]
+        out += [float((pk & yk).sum()), float((pk & ~yk).sum()), float((~pk & yk).sum())]
+    return out
+
+
+def eval_forward(model: OracleMMIMDb, image, text) -> torch.Tensor:
+    model.eval()
+    with torch.no_grad():
+        return model(image, text)

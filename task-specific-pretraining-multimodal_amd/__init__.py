@@ -18,9 +18,10 @@ from .modules import AVMNIST, BasicBlock, ResNet18, ResNet34, ResNetEncoder, mod
 from .optim import FusedAdam
 from .step import FusedTrainStep
 from .monomodal import FusedMonoStep, MonomodalEncoder
-from . import plugin, ddp, data, monomodal
+from . import plugin, ddp, data, monomodal, mmimdb
+from .mmimdb import MMIMDb, FusedMMIMDbStep
 
 __all__ = ["AVMNIST", "BasicBlock", "ResNet18", "ResNet34", "ResNetEncoder", "FusedAdam", "FusedTrainStep",
            "EncoderEngine", "prepare_encoder_layout", "TspmError", "TspmLibraryError", "plugin", "ddp", "data",
-           "modality_key", "MonomodalEncoder", "FusedMonoStep", "monomodal"]
+           "modality_key", "MonomodalEncoder", "FusedMonoStep", "monomodal", "mmimdb", "MMIMDb", "FusedMMIMDbStep"]
 __version__ = "0.1.0"

@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -108,6 +108,11 @@ _SIGS = {
     "tspm_classify_update_ex": (c_int32, [c_int32, c_int32, _P, _P, _P, c_int32, _P, _P, _P, _P, _P, c_int64, c_int32,
                                           _P]),
     "tspm_reduce_slabs": (c_int32, [c_int64, c_int32, c_int64, _P, _P, _P]),
+    "tspm_gmu_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _P, c_int32, _P]),
+    "tspm_gmu_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, c_int32, _P, _P]),
+    "tspm_maxout_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
+    "tspm_maxout_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
+    "tspm_bce_logits": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, c_float, _P, _P]),
 }
 
 EXPORTED = tuple(_SIGS)

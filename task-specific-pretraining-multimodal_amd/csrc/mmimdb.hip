@@ -1,0 +1,227 @@
+// MMIMDb late-fusion path (BASELINE configs[3]): the element-wise and row-reduction
+// pieces around the small GEMMs —
+//   * GatedBiModalNetwork (MML_Suite/models/gates/gated_bimodal.py): tanh of both projections, the
+//     scalar gate sigmoid(w_z · [h1, h2]) per row, and z = g*h1 + (1-g)*h2, plus its backward;
+//   * MaxOut(num_units=2, no bias) (models/maxout.py) fused with the Dropout(0.5) that follows it in
+//     MLPGenreClassifier (models/mmimdb.py:38-47), plus the backward of torch.maximum (ties split the
+//     gradient in half, as ATen's derivative of maximum does);
+//   * BCEWithLogitsLoss(mean) (experiment_utils/loss.py:52) with on-device multilabel counts for the
+//     f1_{samples,macro,weighted,micro} metrics of configs/mmimdb/centralised/mmimdb_baseline.yaml
+//     (prediction = sigmoid(x) > threshold, models/mmimdb.py:236-237).
+// Every kernel is HBM/latency bound (a few hundred KB per launch); rows map to workgroups so the
+// row reductions are wave shuffles + one LDS step in a fixed order (deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int kRowThreads = 256;
+
+// Block-wide sum in a fixed order: wave shuffle tree, then wave 0 adds the 4 wave totals.
+TSPM_DEV float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < kRowThreads / 64; ++w) t += red[w];
+  return t;
+}
+
+// One workgroup per row.  u: [n, 2d] (fc_one output in columns [0,d), fc_two output in [d,2d)).
+__global__ __launch_bounds__(kRowThreads) void k_gmu_fwd(int d, const float* __restrict__ u, int ldu,
+                                                         const float* __restrict__ wz, float* __restrict__ h,
+                                                         int ldh, float* __restrict__ gate, float* __restrict__ z,
+                                                         int ldz) {
+  __shared__ float red[kRowThreads / 64];
+  const long long r = blockIdx.x;
+  const float* ur = u + r * ldu;
+  float* hr = h + r * ldh;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < 2 * d; j += kRowThreads) {
+    const float t = tanhf(ur[j]);
+    hr[j] = t;
+    s = fmaf(wz[j], t, s);
+  }
+  s = block_sum(s, red);
+  const float g = 1.f / (1.f + expf(-s));
+  if (threadIdx.x == 0) gate[r] = g;
+  const float g1 = 1.f - g;
+  float* zr = z + r * ldz;
+  for (int j = threadIdx.x; j < d; j += kRowThreads) zr[j] = g * hr[j] + g1 * hr[d + j];
+}
+
+// dz -> du [n,2d] (through gate and tanh) and ds[n] = d(loss)/d(gate pre-activation) (the weight
+// gradient of hidden_sigmoid is then ds^T @ h, a small GEMM).
+__global__ __launch_bounds__(kRowThreads) void k_gmu_bwd(int d, const float* __restrict__ dz, int lddz,
+                                                         const float* __restrict__ h, int ldh,
+                                                         const float* __restrict__ gate,
+                                                         const float* __restrict__ wz, float* __restrict__ du,
+                                                         int lddu, float* __restrict__ ds) {
+  __shared__ float red[kRowThreads / 64];
+  const long long r = blockIdx.x;
+  const float* hr = h + r * ldh;
+  const float* dzr = dz + r * lddz;
+  float a = 0.f;
+  for (int j = threadIdx.x; j < d; j += kRowThreads) a = fmaf(dzr[j], hr[j] - hr[d + j], a);
+  a = block_sum(a, red);
+  const float g = gate[r];
+  const float dsv = a * g * (1.f - g);
+  if (threadIdx.x == 0) ds[r] = dsv;
+  float* dur = du + r * lddu;
+  for (int j = threadIdx.x; j < d; j += kRowThreads) {
+    const float h1 = hr[j], h2 = hr[d + j];
+    const float d1 = fmaf(dsv, wz[j], g * dzr[j]);
+    const float d2 = fmaf(dsv, wz[d + j], (1.f - g) * dzr[j]);
+    dur[j] = d1 * (1.f - h1 * h1);
+    dur[d + j] = d2 * (1.f - h2 * h2);
+  }
+}
+
+// y[r,j] = max(a[r,j], a[r,d+j]) [* (keep ? scale : 0)]
+__global__ __launch_bounds__(256) void k_maxout_fwd(int n, int d, const float* __restrict__ a, int lda,
+                                                    const uint8_t* __restrict__ keep, float scale,
+                                                    float* __restrict__ y, int ldy) {
+  const long long total = (long long)n * d;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long r = t / d;
+    const int j = (int)(t - r * d);
+    const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
+    float v = a1 > a0 ? a1 : a0;
+    if (keep) v = v * (keep[t] ? scale : 0.f);
+    y[r * ldy + j] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_maxout_bwd(int n, int d, const float* __restrict__ dy, int lddy,
+                                                    const float* __restrict__ a, int lda,
+                                                    const uint8_t* __restrict__ keep, float scale,
+                                                    float* __restrict__ da, int ldda) {
+  const long long total = (long long)n * d;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long r = t / d;
+    const int j = (int)(t - r * d);
+    float g = dy[r * lddy + j];
+    if (keep) g = g * (keep[t] ? scale : 0.f);
+    const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
+    const float half = 0.5f * g;
+    da[r * ldda + j] = a0 > a1 ? g : (a0 == a1 ? half : 0.f);
+    da[r * ldda + d + j] = a1 > a0 ? g : (a0 == a1 ? half : 0.f);
+  }
+}
+
+// Single workgroup: loss (mean over n*c), dlogits, and the metric counts.
+__global__ __launch_bounds__(kRowThreads) void k_bce_logits(int n, int c, const float* __restrict__ x,
+                                                            const float* __restrict__ t, float* __restrict__ loss,
+                                                            float* __restrict__ dx, float grad_scale, float threshold,
+                                                            float* __restrict__ stats) {
+  __shared__ float red[kRowThreads / 64];
+  const long long total = (long long)n * c;
+  const float inv = 1.f / (float)total;
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < total; i += kRowThreads) {
+    const float xv = x[i], tv = t[i];
+    // ATen: (1 - t) * x - log_sigmoid(x),  log_sigmoid(x) = min(x, 0) - log1p(exp(-|x|))
+    const float ls = fminf(xv, 0.f) - log1pf(expf(-fabsf(xv)));
+    acc += (1.f - tv) * xv - ls;
+    if (dx) dx[i] = (1.f / (1.f + expf(-xv)) - tv) * inv * grad_scale;
+  }
+  const float sum = block_sum(acc, red);
+  const float mean = sum * inv * grad_scale;
+  if (threadIdx.x == 0) {
+    loss[0] = mean;
+    if (stats) {
+      stats[0] += mean * (float)n;
+      stats[1] += (float)n;
+    }
+  }
+  if (!stats) return;
+  // stats[2] += sum over rows of the per-sample F1 (zero_division = 0); per class k:
+  // stats[3+3k+{0,1,2}] += tp, fp, fn.  Thread-exclusive slots, so plain read-modify-write.
+  float f1 = 0.f;
+  for (int r = threadIdx.x; r < n; r += kRowThreads) {
+    int tp = 0, fp = 0, fn = 0;
+    for (int k = 0; k < c; ++k) {
+      const bool p = 1.f / (1.f + expf(-x[(long long)r * c + k])) > threshold;
+      const bool y = t[(long long)r * c + k] > 0.5f;
+      tp += p && y;
+      fp += p && !y;
+      fn += !p && y;
+    }
+    const int den = 2 * tp + fp + fn;
+    f1 += den > 0 ? (2.f * tp) / (float)den : 0.f;
+  }
+  const float f1s = block_sum(f1, red);
+  if (threadIdx.x == 0) stats[2] += f1s;
+  for (int k = threadIdx.x; k < c; k += kRowThreads) {
+    float tp = 0.f, fp = 0.f, fn = 0.f;
+    for (int r = 0; r < n; ++r) {
+      const bool p = 1.f / (1.f + expf(-x[(long long)r * c + k])) > threshold;
+      const bool y = t[(long long)r * c + k] > 0.5f;
+      tp += (p && y) ? 1.f : 0.f;
+      fp += (p && !y) ? 1.f : 0.f;
+      fn += (!p && y) ? 1.f : 0.f;
+    }
+    stats[3 + 3 * k] += tp;
+    stats[4 + 3 * k] += fp;
+    stats[5 + 3 * k] += fn;
+  }
+}
+
+int ew_grid(long long work) {
+  long long b = cdiv64(work, 256);
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" int tspm_gmu_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const float* wz, float* h,
+                            int32_t ldh, float* gate, float* z, int32_t ldz, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || ldu < 2 * d || ldh < 2 * d || ldz < d || !u || !wz || !h || !gate || !z)
+    return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_gmu_fwd, dim3(n), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), d, u, ldu, wz, h,
+                     ldh, gate, z, ldz);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_gmu_bwd(int32_t n, int32_t d, const float* dz, int32_t lddz, const float* h, int32_t ldh,
+                            const float* gate, const float* wz, float* du, int32_t lddu, float* ds,
+                            tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || lddz < d || ldh < 2 * d || lddu < 2 * d || !dz || !h || !gate || !wz || !du || !ds)
+    return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_gmu_bwd, dim3(n), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), d, dz, lddz, h, ldh,
+                     gate, wz, du, lddu, ds);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_maxout_fwd(int32_t n, int32_t d, const float* a, int32_t lda, const uint8_t* keep,
+                               float keep_scale, float* y, int32_t ldy, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || lda < 2 * d || ldy < d || !a || !y) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_maxout_fwd, dim3(ew_grid((long long)n * d)), dim3(256), 0, static_cast<hipStream_t>(stream), n,
+                     d, a, lda, keep, keep_scale, y, ldy);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_maxout_bwd(int32_t n, int32_t d, const float* dy, int32_t lddy, const float* a, int32_t lda,
+                               const uint8_t* keep, float keep_scale, float* da, int32_t ldda, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || lddy < d || lda < 2 * d || ldda < 2 * d || !dy || !a || !da) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_maxout_bwd, dim3(ew_grid((long long)n * d)), dim3(256), 0, static_cast<hipStream_t>(stream), n,
+                     d, dy, lddy, a, lda, keep, keep_scale, da, ldda);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float* targets, float* loss,
+                               float* dlogits, float grad_scale, float threshold, float* stats, tspm_stream_t stream) {
+  if (n <= 0 || classes <= 0 || !logits || !targets || !loss) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_bce_logits, dim3(1), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), n, classes, logits,
+                     targets, loss, dlogits, grad_scale, threshold, stats);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}

@@ -1,0 +1,509 @@
+"""MMIMDb late-fusion path (BASELINE configs[3]) on the HIP kernels.
+
+Drop-in classes for the reference's YAML tags / resolver (config/yaml_constructors.py:126-142,
+config/resolvers.py:44-47) with the reference's constructor arguments, attribute names and
+``state_dict`` keys (MML_Suite/models/mmimdb.py, models/gates/gated_bimodal.py, models/maxout.py):
+
+    image_model / text_model : MMIMDbModalityEncoder  = BatchNorm1d(in) → Linear(in, out)
+    fusion_module            : GatedBiModalNetwork    = tanh(fc_one), tanh(fc_two), gate, mix
+    mm_mlp                   : MLPGenreClassifier     = BN → MaxOut → Dropout → BN → MaxOut → Dropout → BN → Linear
+
+The submodules hold parameters only; every computation runs in ``MMIMDbEngine`` as gfx950 HIP
+kernels behind the C ABI (include/tspm.h): BatchNorm1d = ``tspm_bn_stats/apply/bwd`` over [n, C]
+rows, Linear / MaxOut products = ``tspm_linear_*`` (MFMA small GEMM; the two MaxOut units' weights
+are adjacent in FusedAdam's flat buffer and run as ONE [2d, in] product), GMU / MaxOut+Dropout /
+BCEWithLogits = ``tspm_gmu_*``, ``tspm_maxout_*``, ``tspm_bce_logits``, Adam = ``tspm_adam_step``.
+``FusedMMIMDbStep`` captures forward + loss + backward + Adam in one HIP graph.  No CPU or ATen
+fallback: a CPU tensor raises ``TspmError``.
+
+Supported configuration = the reference's MMIMDb configs: GMU fusion (``multimodal_pooling`` is
+rejected), MaxOut with 2 units and no bias, Dropout 0.5, biasless GMU.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from .optim import FusedAdam
+from .step import shared_batches_tracked
+
+_BN_MOMENTUM_DEFAULT = 0.1
+
+
+# ------------------------------------------------------------------------------------------------
+# parameter containers (reference attribute names / state_dict keys)
+# ------------------------------------------------------------------------------------------------
+class MaxOut(nn.Module):
+    """models/maxout.py: ``layers`` = num_units × Linear(input_dim, output_dim)."""
+
+    def __init__(self, input_dim: int, output_dim: int, num_units: int = 2, use_bias: bool = True) -> None:
+        super().__init__()
+        self.input_dim, self.output_dim, self.num_units, self.use_bias = input_dim, output_dim, num_units, use_bias
+        self.layers = nn.ModuleList([nn.Linear(input_dim, output_dim, bias=use_bias) for _ in range(num_units)])
+
+    def forward(self, x):  # pragma: no cover - the engine runs the layer
+        raise L.TspmError("MaxOut runs inside MMIMDb's HIP engine (call the MMIMDb model)")
+
+
+class MMIMDbModalityEncoder(nn.Module):
+    """models/mmimdb.py:63-93."""
+
+    def __init__(self, input_dim: int, output_dim: int) -> None:
+        super().__init__()
+        self.net = nn.Sequential(nn.BatchNorm1d(input_dim), nn.Linear(input_dim, output_dim))
+
+    def forward(self, x):  # pragma: no cover
+        raise L.TspmError("MMIMDbModalityEncoder runs inside MMIMDb's HIP engine (call the MMIMDb model)")
+
+
+class GatedBiModalNetwork(nn.Module):
+    """models/gates/gated_bimodal.py."""
+
+    def __init__(self, input_one_dim: int, input_two_dim: int, output_one_dim: int, output_two_dim: int, *,
+                 use_bias: bool = False) -> None:
+        super().__init__()
+        self.fc_one = nn.Linear(input_one_dim, output_one_dim, bias=use_bias)
+        self.fc_two = nn.Linear(input_two_dim, output_two_dim, bias=use_bias)
+        self.hidden_sigmoid = nn.Linear(output_one_dim + output_two_dim, 1, bias=use_bias)
+        self.activation = nn.Tanh()
+        self.gate_activation = nn.Sigmoid()
+        self.use_bias = use_bias
+
+    def forward(self, a, b):  # pragma: no cover
+        raise L.TspmError("GatedBiModalNetwork runs inside MMIMDb's HIP engine (call the MMIMDb model)")
+
+
+class MLPGenreClassifier(nn.Module):
+    """models/mmimdb.py:20-60."""
+
+    def __init__(self, input_size: int, output_size: int, hidden_size: int) -> None:
+        super().__init__()
+        self.input_size, self.output_size, self.hidden_size = input_size, output_size, hidden_size
+        self.net = nn.Sequential(
+            nn.BatchNorm1d(input_size), MaxOut(input_size, hidden_size, use_bias=False), nn.Dropout(p=0.5),
+            nn.BatchNorm1d(hidden_size), MaxOut(hidden_size, hidden_size, use_bias=False), nn.Dropout(p=0.5),
+            nn.BatchNorm1d(hidden_size), nn.Linear(hidden_size, output_size))
+
+    def forward(self, x):  # pragma: no cover
+        raise L.TspmError("MLPGenreClassifier runs inside MMIMDb's HIP engine (call the MMIMDb model)")
+
+
+def _bce_weight(loss_functions) -> float:
+    """Weight of the single bce_with_logits term of a LossFunctionGroup (experiment_utils/loss.py:52,
+    98-148); anything else is not the MMIMDb configuration and raises."""
+    if loss_functions is None:
+        return 1.0
+    items = list(loss_functions.items())
+    if len(items) != 1:
+        raise L.TspmError("MMIMDb HIP step: expected one loss term (bce_with_logits)")
+    term = items[0][1]
+    fn = getattr(term, "loss_fn", None)
+    if not isinstance(fn, nn.BCEWithLogitsLoss) or fn.reduction != "mean" or fn.weight is not None \
+            or fn.pos_weight is not None:
+        raise L.TspmError("MMIMDb HIP step: the loss must be BCEWithLogitsLoss(reduction='mean')")
+    return float(getattr(term, "weight", 1.0))
+
+
+def _bn(m: nn.BatchNorm1d):
+    return m.weight, m.bias, m.running_mean, m.running_var, float(m.eps), float(
+        m.momentum if m.momentum is not None else _BN_MOMENTUM_DEFAULT)
+
+
+# ------------------------------------------------------------------------------------------------
+# the kernel schedule
+# ------------------------------------------------------------------------------------------------
+class MMIMDbEngine:
+    """Pre-allocated buffers for one batch size and the launch sequence of forward / backward."""
+
+    def __init__(self, model: "MMIMDb", n: int, device: torch.device):
+        if n < 2:
+            raise L.TspmError("BatchNorm1d in training mode needs more than one sample per batch")
+        self.model, self.n, self.dev = model, n, device
+        ie, te, gmu, clf = model.image_model, model.text_model, model.fusion_module, model.mm_mlp
+        self.di, self.dt = ie.net[0].num_features, te.net[0].num_features
+        self.e = ie.net[1].out_features
+        if te.net[1].out_features != self.e or gmu.fc_one.in_features != self.e or gmu.fc_two.in_features != self.e:
+            raise L.TspmError("MMIMDb HIP engine: both encoders and the GMU inputs must share one width")
+        self.d = gmu.fc_one.out_features
+        if gmu.fc_two.out_features != self.d or gmu.use_bias:
+            raise L.TspmError("MMIMDb HIP engine: GMU outputs must match and carry no bias")
+        if clf.input_size != self.d:
+            raise L.TspmError("MMIMDb HIP engine: classifier input_size must equal the GMU output width")
+        self.h, self.c = clf.hidden_size, clf.output_size
+        for mo in (clf.net[1], clf.net[4]):
+            if mo.num_units != 2 or mo.use_bias:
+                raise L.TspmError("MMIMDb HIP engine: MaxOut with 2 units and no bias (models/mmimdb.py:40-44)")
+        self.p = float(clf.net[2].p)
+        if abs(self.p - float(clf.net[5].p)) > 0 or not 0.0 <= self.p < 1.0:
+            raise L.TspmError("MMIMDb HIP engine: both dropouts must share p < 1")
+        for c in (self.di, self.dt, self.d, self.h):
+            if c % 4:
+                raise L.TspmError("MMIMDb HIP engine: feature widths must be multiples of 4")
+        f = dict(device=device, dtype=torch.float32)
+        e, d, h, c = self.e, self.d, self.h, self.c
+        z = lambda *s: torch.zeros(*s, **f)
+        self.I, self.T, self.labels = z(n, self.di), z(n, self.dt), z(n, c)
+        self.XnI, self.XnT, self.EI, self.ET = z(n, self.di), z(n, self.dt), z(n, e), z(n, e)
+        self.U, self.H, self.gate, self.Z, self.Zn = z(n, 2 * d), z(n, 2 * d), z(n), z(n, d), z(n, d)
+        self.A1, self.Y1, self.Y1n = z(n, 2 * h), z(n, h), z(n, h)
+        self.A2, self.Y2, self.Y2n = z(n, 2 * h), z(n, h), z(n, h)
+        self.logits, self.loss, self.dlogits = z(n, c), z(1), z(n, c)
+        self.dY2n, self.dY2, self.dA2, self.dY1n, self.dY1, self.dA1 = z(n, h), z(n, h), z(n, 2 * h), z(n, h), \
+            z(n, h), z(n, 2 * h)
+        self.dZn, self.dZ, self.dU, self.ds = z(n, d), z(n, d), z(n, 2 * d), z(n)
+        self.dEI, self.dET = z(n, e), z(n, e)
+        self.dXn = z(n, max(self.di, self.dt))
+        self.dX = z(n, max(self.di, self.dt))
+        self.keep = torch.ones(2, n, h, dtype=torch.uint8, device=device)
+        widths = (self.di, self.dt, d, h)
+        self.stat = {k: (z(w), z(w)) for k, w in zip(("i", "t", "b0", "b1", "b2"), widths + (h,))}
+        lib = L.lib()
+        ws = max([lib.tspm_bn_stats_workspace(n, w) for w in widths] + [lib.tspm_bn_bwd_workspace(n, w) for w in widths])
+        self.ws = torch.zeros(max(int(ws), 16) // 4 + 4, **f)
+        self.ws_bytes = self.ws.numel() * 4
+        self.stats = z(3 + 3 * c)
+        self.keep_override: Optional[torch.Tensor] = None
+        self.rng_ctr_ptr: Optional[int] = None
+        self._check_maxout_weights()
+
+    def _check_maxout_weights(self) -> None:
+        for mo in (self.model.mm_mlp.net[1], self.model.mm_mlp.net[4]):
+            w0, w1 = mo.layers[0].weight, mo.layers[1].weight
+            if w1.data_ptr() != w0.data_ptr() + w0.numel() * 4 or not (w0.is_contiguous() and w1.is_contiguous()):
+                raise L.TspmError("MaxOut units' weights must be adjacent (create FusedAdam over the model's "
+                                  "parameters before the first step)")
+            g0, g1 = w0.grad, w1.grad
+            if g0 is not None and (g1 is None or g1.data_ptr() != g0.data_ptr() + g0.numel() * 4):
+                raise L.TspmError("MaxOut units' gradients must be adjacent (FusedAdam's flat gradient buffer)")
+
+    # -- helpers ------------------------------------------------------------------------------------
+    def _bn_train(self, key, bn, x, width, out, sh):
+        lib = L.lib()
+        g, b, rm, rv, eps, mom = _bn(bn)
+        mean, inv = self.stat[key]
+        L.check(lib.tspm_bn_stats(self.n, width, x.data_ptr(), 1, 0, None, rm.data_ptr(), rv.data_ptr(), mom, eps,
+                                  mean.data_ptr(), inv.data_ptr(), self.ws.data_ptr(), self.ws_bytes, sh), "bn_stats")
+        L.check(lib.tspm_bn_apply(self.n, width, x.data_ptr(), mean.data_ptr(), inv.data_ptr(), g.data_ptr(),
+                                  b.data_ptr(), 0, None, None, None, None, None, 0, out.data_ptr(), None, 0, sh),
+                "bn_apply")
+
+    def _bn_eval(self, bn, x, width, out, sh):
+        g, b, rm, rv, eps, _ = _bn(bn)
+        L.check(L.lib().tspm_bn_apply_eval(self.n, width, x.data_ptr(), rm.data_ptr(), rv.data_ptr(), eps, g.data_ptr(),
+                                           b.data_ptr(), 0, None, None, None, None, None, 0, out.data_ptr(), sh),
+                "bn_apply_eval")
+
+    def _bn_bwd(self, key, bn, g_in, x, width, dx, sh):
+        mean, inv = self.stat[key]
+        L.check(L.lib().tspm_bn_bwd(self.n, width, g_in.data_ptr(), None, x.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                    bn.weight.data_ptr(), bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
+                                    dx.data_ptr(), None, None, None, None, None, None, None, None, None, None, 0,
+                                    self.ws.data_ptr(), self.ws_bytes, sh), "bn_bwd")
+
+    # -- forward ------------------------------------------------------------------------------------
+    def forward(self, sh: int, train: bool) -> None:
+        lib = L.lib()
+        m = self.model
+        n, e, d, h, c = self.n, self.e, self.d, self.h, self.c
+        ie, te, gmu, net = m.image_model.net, m.text_model.net, m.fusion_module, m.mm_mlp.net
+        bn = (lambda k, mod, x, w, o: self._bn_train(k, mod, x, w, o, sh)) if train else \
+            (lambda k, mod, x, w, o: self._bn_eval(mod, x, w, o, sh))
+        # encoders: BatchNorm1d → Linear (models/mmimdb.py:78-93)
+        bn("i", ie[0], self.I, self.di, self.XnI)
+        L.check(lib.tspm_linear_fwd(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
+                                    ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e, sh), "image fc")
+        bn("t", te[0], self.T, self.dt, self.XnT)
+        L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
+                                    te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, sh), "text fc")
+        # GMU (gated_bimodal.py): both projections into U = [fc_one | fc_two], then the gate kernel
+        L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(), None, 0, None, 1.0,
+                                    self.U.data_ptr(), 2 * d, sh), "gmu fc_one")
+        L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, gmu.fc_two.weight.data_ptr(), None, 0, None, 1.0,
+                                    self.U.data_ptr() + d * 4, 2 * d, sh), "gmu fc_two")
+        L.check(lib.tspm_gmu_fwd(n, d, self.U.data_ptr(), 2 * d, gmu.hidden_sigmoid.weight.data_ptr(),
+                                 self.H.data_ptr(), 2 * d, self.gate.data_ptr(), self.Z.data_ptr(), d, sh), "gmu")
+        # classifier (models/mmimdb.py:38-47)
+        keep, k1, k2, scale = None, None, None, 1.0
+        if train and self.p > 0:
+            scale = 1.0 / (1.0 - self.p)
+            if self.keep_override is None:
+                L.check(lib.tspm_dropout_mask(2 * n * h, self.p, self.model._rng_seed, self.rng_ctr_ptr,
+                                              self.keep.data_ptr(), sh), "dropout_mask")
+            k1, k2 = self.keep[0].data_ptr(), self.keep[1].data_ptr()
+        bn("b0", net[0], self.Z, d, self.Zn)
+        L.check(lib.tspm_linear_fwd(n, d, 2 * h, self.Zn.data_ptr(), d, net[1].layers[0].weight.data_ptr(), None, 0,
+                                    None, 1.0, self.A1.data_ptr(), 2 * h, sh), "maxout1")
+        L.check(lib.tspm_maxout_fwd(n, h, self.A1.data_ptr(), 2 * h, k1, scale, self.Y1.data_ptr(), h, sh), "maxout1")
+        bn("b1", net[3], self.Y1, h, self.Y1n)
+        L.check(lib.tspm_linear_fwd(n, h, 2 * h, self.Y1n.data_ptr(), h, net[4].layers[0].weight.data_ptr(), None, 0,
+                                    None, 1.0, self.A2.data_ptr(), 2 * h, sh), "maxout2")
+        L.check(lib.tspm_maxout_fwd(n, h, self.A2.data_ptr(), 2 * h, k2, scale, self.Y2.data_ptr(), h, sh), "maxout2")
+        bn("b2", net[6], self.Y2, h, self.Y2n)
+        L.check(lib.tspm_linear_fwd(n, h, c, self.Y2n.data_ptr(), h, net[7].weight.data_ptr(), net[7].bias.data_ptr(),
+                                    0, None, 1.0, self.logits.data_ptr(), c, sh), "output fc")
+
+    def loss_fn(self, sh: int, weight: float, with_grad: bool, stats: bool) -> None:
+        L.check(L.lib().tspm_bce_logits(self.n, self.c, self.logits.data_ptr(), self.labels.data_ptr(),
+                                        self.loss.data_ptr(), self.dlogits.data_ptr() if with_grad else None, weight,
+                                        float(self.model.binary_threshold), self.stats.data_ptr() if stats else None,
+                                        sh), "bce_with_logits")
+
+    # -- backward -----------------------------------------------------------------------------------
+    def backward(self, sh: int) -> None:
+        lib = L.lib()
+        m = self.model
+        n, e, d, h, c = self.n, self.e, self.d, self.h, self.c
+        ie, te, gmu, net = m.image_model.net, m.text_model.net, m.fusion_module, m.mm_mlp.net
+        scale = 1.0 / (1.0 - self.p) if self.p > 0 else 1.0
+        k1 = self.keep[0].data_ptr() if self.p > 0 else None
+        k2 = self.keep[1].data_ptr() if self.p > 0 else None
+        g = lambda p: p.grad.data_ptr()
+        # output Linear
+        L.check(lib.tspm_linear_bwd_weight(n, h, c, self.Y2n.data_ptr(), h, self.dlogits.data_ptr(), c,
+                                           g(net[7].weight), g(net[7].bias), sh), "output fc dW")
+        L.check(lib.tspm_linear_bwd_data(n, h, c, self.dlogits.data_ptr(), c, net[7].weight.data_ptr(),
+                                         self.dY2n.data_ptr(), h, sh), "output fc dX")
+        self._bn_bwd("b2", net[6], self.dY2n, self.Y2, h, self.dY2, sh)
+        # MaxOut 2 (+ dropout)
+        L.check(lib.tspm_maxout_bwd(n, h, self.dY2.data_ptr(), h, self.A2.data_ptr(), 2 * h, k2, scale,
+                                    self.dA2.data_ptr(), 2 * h, sh), "maxout2 bwd")
+        L.check(lib.tspm_linear_bwd_weight(n, h, 2 * h, self.Y1n.data_ptr(), h, self.dA2.data_ptr(), 2 * h,
+                                           g(net[4].layers[0].weight), None, sh), "maxout2 dW")
+        L.check(lib.tspm_linear_bwd_data(n, h, 2 * h, self.dA2.data_ptr(), 2 * h, net[4].layers[0].weight.data_ptr(),
+                                         self.dY1n.data_ptr(), h, sh), "maxout2 dX")
+        self._bn_bwd("b1", net[3], self.dY1n, self.Y1, h, self.dY1, sh)
+        # MaxOut 1 (+ dropout)
+        L.check(lib.tspm_maxout_bwd(n, h, self.dY1.data_ptr(), h, self.A1.data_ptr(), 2 * h, k1, scale,
+                                    self.dA1.data_ptr(), 2 * h, sh), "maxout1 bwd")
+        L.check(lib.tspm_linear_bwd_weight(n, d, 2 * h, self.Zn.data_ptr(), d, self.dA1.data_ptr(), 2 * h,
+                                           g(net[1].layers[0].weight), None, sh), "maxout1 dW")
+        L.check(lib.tspm_linear_bwd_data(n, d, 2 * h, self.dA1.data_ptr(), 2 * h, net[1].layers[0].weight.data_ptr(),
+                                         self.dZn.data_ptr(), d, sh), "maxout1 dX")
+        self._bn_bwd("b0", net[0], self.dZn, self.Z, d, self.dZ, sh)
+        # GMU
+        L.check(lib.tspm_gmu_bwd(n, d, self.dZ.data_ptr(), d, self.H.data_ptr(), 2 * d, self.gate.data_ptr(),
+                                 gmu.hidden_sigmoid.weight.data_ptr(), self.dU.data_ptr(), 2 * d, self.ds.data_ptr(), sh),
+                "gmu bwd")
+        L.check(lib.tspm_linear_bwd_weight(n, 2 * d, 1, self.H.data_ptr(), 2 * d, self.ds.data_ptr(), 1,
+                                           g(gmu.hidden_sigmoid.weight), None, sh), "gmu gate dW")
+        dU1, dU2 = self.dU.data_ptr(), self.dU.data_ptr() + d * 4
+        for (dUp, fc, E, dE) in ((dU1, gmu.fc_one, self.EI, self.dEI), (dU2, gmu.fc_two, self.ET, self.dET)):
+            L.check(lib.tspm_linear_bwd_weight(n, e, d, E.data_ptr(), e, dUp, 2 * d, g(fc.weight), None, sh), "gmu dW")
+            L.check(lib.tspm_linear_bwd_data(n, e, d, dUp, 2 * d, fc.weight.data_ptr(), dE.data_ptr(), e, sh), "gmu dX")
+        # encoders (the input-feature gradient is computed into scratch; nothing consumes it)
+        for key, enc, Xn, X, dE, w in (("i", ie, self.XnI, self.I, self.dEI, self.di),
+                                       ("t", te, self.XnT, self.T, self.dET, self.dt)):
+            L.check(lib.tspm_linear_bwd_weight(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, g(enc[1].weight),
+                                               g(enc[1].bias), sh), "encoder fc dW")
+            L.check(lib.tspm_linear_bwd_data(n, w, e, dE.data_ptr(), e, enc[1].weight.data_ptr(), self.dXn.data_ptr(),
+                                             w, sh), "encoder fc dX")
+            self._bn_bwd(key, enc[0], self.dXn, X, w, self.dX, sh)
+
+
+# ------------------------------------------------------------------------------------------------
+# the model
+# ------------------------------------------------------------------------------------------------
+class MMIMDb(nn.Module):
+    """Drop-in for MML_Suite/models/mmimdb.py:96-338 (GMU fusion)."""
+
+    def __init__(self, image_encoder: MMIMDbModalityEncoder, text_encoder: MMIMDbModalityEncoder,
+                 gated_bimodal_network: Optional[GatedBiModalNetwork] = None,
+                 multimodal_pooling: Optional[Dict[str, Any]] = None, classifier: MLPGenreClassifier = None,
+                 binary_threshold: float = 0.5) -> None:
+        super().__init__()
+        if multimodal_pooling is not None:
+            raise NotImplementedError("MMIMDb HIP path: multimodal_pooling fusion is not on the configs[3] path; "
+                                      "use gated_bimodal_network (configs/mmimdb/centralised/mmimdb_baseline.yaml)")
+        if gated_bimodal_network is None:
+            raise ValueError("Either gated_bimodal_network or multimodal_pooling must be provided")
+        self.image_model = image_encoder
+        self.text_model = text_encoder
+        self.fusion_module = gated_bimodal_network
+        self.fusion_type = "gated"
+        self.mm_mlp = classifier
+        self.binary_threshold = binary_threshold
+        self.monitor = None
+        self._rng_seed = int(torch.initial_seed()) & ((1 << 63) - 1)
+        self._steps: Dict[Any, Any] = {}
+
+    def get_encoder(self, modality):
+        name = str(getattr(modality, "value", modality)).lower()
+        if "image" in name:
+            return self.image_model
+        if "text" in name:
+            return self.text_model
+        raise ValueError(f"Invalid modality: {modality}. Must be image or text")
+
+    def logits_transform(self, logits: torch.Tensor):
+        return (torch.sigmoid(logits).detach().cpu().numpy() > self.binary_threshold).astype(int)
+
+    def _engine(self, n: int, device) -> MMIMDbEngine:
+        key = ("eng", n)
+        eng = self._steps.get(key)
+        if eng is None:
+            eng = MMIMDbEngine(self, n, device)
+            self._steps[key] = eng
+        return eng
+
+    @torch.no_grad()
+    def forward(self, I: torch.Tensor, T: torch.Tensor, *, is_embd_I: bool = False,
+                is_embd_T: bool = False) -> torch.Tensor:
+        """HIP forward (models/mmimdb.py:164-200).  Training mode uses batch statistics, updates the
+        running statistics and draws fresh dropout masks, as the reference's forward does."""
+        if is_embd_I or is_embd_T:
+            raise NotImplementedError("MMIMDb HIP path: pre-embedded inputs are not on the configs[3] path")
+        for t, nm in ((I, "I"), (T, "T")):
+            L.require_cuda_f32(t, nm)
+        eng = self._engine(I.shape[0], I.device)
+        eng.I.copy_(I)
+        eng.T.copy_(T)
+        sh = L.stream_handle()
+        if self.training and eng.rng_ctr_ptr is None:
+            eng._host_ctr = torch.zeros(1, dtype=torch.int64, device=I.device)
+            eng.rng_ctr_ptr = eng._host_ctr.data_ptr()
+        eng.forward(sh, self.training)
+        if self.training:
+            eng._host_ctr.add_(1)
+            nbt = shared_batches_tracked(self, I.device, (nn.BatchNorm1d,))
+            nbt.add_(1)
+        return eng.logits.clone()
+
+    def train_step(self, batch: Dict[str, Any], optimizer, loss_functions, device, metric_recorder=None,
+                   epoch: int = 0) -> Dict[str, Any]:
+        """models/mmimdb.py:203-245 on the fused HIP step."""
+        I, T, labels = _batch_tensors(batch, device)
+        key = ("train", id(optimizer), id(loss_functions), I.shape[0])
+        st = self._steps.get(key)
+        if st is None:
+            st = FusedMMIMDbStep(self, optimizer, loss_functions, I.shape[0])
+            self._steps[key] = st
+        out = st.step(I, T, labels)
+        _record(metric_recorder, out["logits"], labels, batch.get("pattern_name"), self.binary_threshold)
+        return {"loss": out["loss"].item()}
+
+    @torch.no_grad()
+    def validation_step(self, batch: Dict[str, Any], loss_functions, device, metric_recorder=None,
+                        return_test_info: bool = False, epoch: int = None) -> Dict[str, Any]:
+        """models/mmimdb.py:247-290: eval-mode forward + BCE on the HIP kernels."""
+        self.eval()
+        I, T, labels = _batch_tensors(batch, device)
+        eng = self._engine(I.shape[0], I.device)
+        eng.I.copy_(I)
+        eng.T.copy_(T)
+        eng.labels.copy_(labels)
+        sh = L.stream_handle()
+        eng.forward(sh, False)
+        eng.loss_fn(sh, _bce_weight(loss_functions), False, False)
+        _record(metric_recorder, eng.logits, labels, batch.get("pattern_name"), self.binary_threshold)
+        return {"loss": eng.loss.item()}
+
+
+def _batch_tensors(batch, device):
+    def get(name):
+        for k, v in batch.items():
+            if str(getattr(k, "value", k)).lower() == name:
+                return v
+        raise KeyError(name)
+    I = get("image").to(device, non_blocking=True).float()
+    T = get("text").to(device, non_blocking=True).float()
+    labels = get("label").to(device, non_blocking=True).float()
+    return I, T, labels
+
+
+def _record(rec, logits, labels, patterns, threshold):
+    if rec is None or not hasattr(rec, "update_group_all"):
+        return
+    import numpy as np
+    preds = (torch.sigmoid(logits).detach().cpu().numpy() > threshold).astype(int)
+    rec.update_group_all("classification", predictions=preds, targets=labels.detach().cpu().numpy(),
+                         m_types=np.array(patterns if patterns is not None else ["it"] * len(preds)))
+
+
+class FusedMMIMDbStep:
+    """One MMIMDb train step (zero_grad-free: the backward overwrites every gradient) — forward, BCE,
+    backward and Adam — as one HIP graph replayed per batch (captured on the second call)."""
+
+    def __init__(self, model: MMIMDb, optimizer: FusedAdam, loss_functions, batch: int, use_graph: bool = True,
+                 allreduce=None):
+        if not isinstance(optimizer, FusedAdam):
+            raise L.TspmError("FusedMMIMDbStep needs FusedAdam (the flat gradient buffer the kernels write)")
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise L.TspmError("FusedMMIMDbStep runs on the MI355X: move the model to cuda first")
+        self.model, self.opt, self.N = model, optimizer, batch
+        self.weight = _bce_weight(loss_functions)
+        self.eng = MMIMDbEngine(model, batch, dev)
+        fgs = optimizer.flat_groups()
+        self.eng.rng_ctr_ptr = fgs[0].hyper.data_ptr() + L.HYPER_STEP_OFFSET
+        self.nbt = shared_batches_tracked(model, dev, (nn.BatchNorm1d,))
+        self.use_graph, self.allreduce = use_graph, allreduce
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.calls = 0
+        self.log_stats = False
+
+    @property
+    def keep_override(self):
+        return self.eng.keep_override
+
+    @keep_override.setter
+    def keep_override(self, v):
+        self.eng.keep_override = v
+
+    def _fwd_bwd(self) -> None:
+        sh = L.stream_handle()
+        self.eng.forward(sh, True)
+        self.eng.loss_fn(sh, self.weight, True, self.log_stats)
+        self.eng.backward(sh)
+        self.nbt.add_(1)
+
+    def _all(self) -> None:
+        self._fwd_bwd()
+        if self.allreduce is None:
+            self.opt.launch(L.stream_handle())
+
+    def step(self, I: torch.Tensor, T: torch.Tensor, labels: torch.Tensor) -> Dict[str, torch.Tensor]:
+        e = self.eng
+        e.I.copy_(I, non_blocking=True)
+        e.T.copy_(T, non_blocking=True)
+        e.labels.copy_(labels, non_blocking=True)
+        self.run()
+        return {"loss": e.loss, "logits": e.logits}
+
+    def run(self) -> None:
+        self.model.train()
+        self.opt.sync_hyper()
+        if self.eng.keep_override is not None:
+            self.eng.keep.copy_(self.eng.keep_override.reshape(self.eng.keep.shape).to(torch.uint8), non_blocking=True)
+        if not self.use_graph or self.calls == 0:
+            self._all()
+        else:
+            if self.graph is None:
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._all()
+                self.graph = g
+            self.graph.replay()
+        if self.allreduce is not None:
+            self.allreduce()
+            self.opt.launch(L.stream_handle())
+        self.opt.note_steps(1)
+        self.calls += 1
+
+
+def f1_metrics(stats: torch.Tensor, classes: int) -> Dict[str, float]:
+    """f1_samples / f1_macro / f1_weighted / f1_micro (sklearn.metrics.f1_score, zero_division=0, as
+    configured in mmimdb_baseline.yaml) from the counts tspm_bce_logits accumulates."""
+    s = stats.detach().double().cpu()
+    n = max(float(s[1]), 1.0)
+    tp, fp, fn = s[3::3][:classes], s[4::3][:classes], s[5::3][:classes]
+    den = 2 * tp + fp + fn
+    f1k = torch.where(den > 0, 2 * tp / den.clamp(min=1e-300), torch.zeros_like(den))
+    sup = tp + fn
+    micro_den = float(2 * tp.sum() + fp.sum() + fn.sum())
+    return {"loss": float(s[0]) / n, "f1_samples": float(s[2]) / n, "f1_macro": float(f1k.mean()),
+            "f1_weighted": float((f1k * sup).sum() / sup.sum()) if float(sup.sum()) > 0 else 0.0,
+            "f1_micro": float(2 * tp.sum()) / micro_den if micro_den > 0 else 0.0}

@@ -21,9 +21,14 @@ from typing import Dict, Optional
 from . import data
 from .modules import AVMNIST, ResNet18, ResNet34, ResNetEncoder
 from .optim import FusedAdam
+from . import mmimdb as _mm
 
-TAGS = {"!ResNet18": ResNet18, "!ResNet34": ResNet34, "!ResNetEncoder": ResNetEncoder}
-MODELS = {"avmnist": AVMNIST}
+TAGS = {"!ResNet18": ResNet18, "!ResNet34": ResNet34, "!ResNetEncoder": ResNetEncoder,
+        # MMIMDb late-fusion path (config/yaml_constructors.py:126-142)
+        "!MMIMDbModalityEncoder": _mm.MMIMDbModalityEncoder, "!MaxOut": _mm.MaxOut,
+        "!GatedBiModalNetwork": _mm.GatedBiModalNetwork, "!MMIMDb": _mm.MMIMDb,
+        "!MLPGenreClassifier": _mm.MLPGenreClassifier}
+MODELS = {"avmnist": AVMNIST, "mmimdb": _mm.MMIMDb, "mmimdbmodalityencoder": _mm.MMIMDbModalityEncoder}
 ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder}
 OPTIMIZERS = {"adam": FusedAdam}
 DATASETS = {"avmnist": data.AVMNIST}

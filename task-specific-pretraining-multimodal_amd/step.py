@@ -50,11 +50,12 @@ def _ce_weight(loss_functions) -> Optional[float]:
     return float(w)
 
 
-def shared_batches_tracked(model: torch.nn.Module, dev: torch.device) -> torch.Tensor:
+def shared_batches_tracked(model: torch.nn.Module, dev: torch.device,
+                           types=(torch.nn.BatchNorm2d,)) -> torch.Tensor:
     """The ``num_batches_tracked`` counters of every BatchNorm2d of ``model`` re-pointed as views of ONE
     int64 device buffer (one add per step instead of one per BN), shared by every fused step of the
     model (e.g. a second one for a partial last batch)."""
-    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+    bns = [m for m in model.modules() if isinstance(m, types) and m.num_batches_tracked is not None]
     nbt = getattr(model, "_tspm_nbt", None)
     if not (nbt is not None and nbt.numel() == len(bns) and nbt.device == dev and all(
             m.num_batches_tracked.data_ptr() == nbt[i].data_ptr() for i, m in enumerate(bns))):

@@ -1,0 +1,181 @@
+"""MMIMDb late-fusion step (BASELINE configs[3]) on the HIP path against the CPU oracle
+(oracle/mmimdb_ref.py, pinned bit-exact to the real reference by tests/golden/make_mmimdb_golden.py).
+Criterion as tests/test_gpu_model.py: the oracle in fp64 is the truth; ours must stay within
+FACTOR (4x) the fp32 reference's own relative-L2 error plus a floor (2e-6 outputs, 2e-5 gradients),
+gradients may take the flip-tolerant bound (rel-L2 <= 2e-2 and cosine >= 0.9999: MaxOut argmax and
+threshold flips)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import tspm_amd
+from oracle import mmimdb_ref as orc
+from oracle.avmnist_ref import OracleAdam
+from test_gpu_model import FLOOR_OUT, check, check_grad, rel_l2
+from test_mmimdb_cpu import dropin
+from tspm_amd import _lib as L
+from tspm_amd import mmimdb as M
+
+pytestmark = pytest.mark.gpu
+LR, WD = 1e-5, 1e-3
+
+
+def _setup(gpu, n, seed=0, graph=True):
+    ours = dropin(seed).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    st = M.FusedMMIMDbStep(ours, opt, None, n, use_graph=graph)
+    o32 = orc.build_oracle_mmimdb(seed)
+    o64 = copy.deepcopy(o32).double()
+    return ours, opt, st, o32, o64
+
+
+def _keep(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(2, n, 512, generator=g) >= 0.5).to(torch.uint8)
+
+
+@pytest.mark.parametrize("n", [4, 64, 128, 256])
+def test_fused_step_vs_oracle(gpu, n):
+    ours, opt, st, o32, o64 = _setup(gpu, n)
+    op32 = OracleAdam(list(o32.parameters()), lr=LR, weight_decay=WD)
+    op64 = OracleAdam(list(o64.parameters()), lr=LR, weight_decay=WD)
+    I, T, y = orc.synthetic_batch(n, seed=77)
+    for s in range(3):
+        keep = _keep(n, 10 + s)
+        st.keep_override = keep.to(gpu)
+        out = st.step(I.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        r32 = orc.train_step(o32, op32, I, T, y, keep[0], keep[1])
+        r64 = orc.train_step(o64, op64, I.double(), T.double(), y.double(), keep[0], keep[1])
+        check(f"logits s{s}", out["logits"], r32["logits"], r64["logits"], FLOOR_OUT)
+        check(f"loss s{s}", out["loss"], r32["loss"], r64["loss"], FLOOR_OUT)
+        if s == 0:
+            p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
+            for name, p in ours.named_parameters():
+                check_grad(name, p.grad, p32[name].grad, p64[name].grad)
+    for k, v in ours.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            assert rel_l2(v, o64.state_dict()[k]) < 1e-4, k
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == 3, k
+
+
+def test_fused_step_vs_golden_reference(gpu):
+    """3 fused steps (eager, then captured graph) on the vectors the real MML_Suite MMIMDb.train_step
+    produced (B=4, seed-0 weights, the reference's dropout masks)."""
+    mg = dict(np.load("tests/golden/mmimdb_step_b4.npz", allow_pickle=False))
+    ours, opt, st, _, o64 = _setup(gpu, 4)
+    op64 = OracleAdam(list(o64.parameters()), lr=LR, weight_decay=WD)
+    I, T, y = (torch.from_numpy(mg[k]) for k in ("image", "text", "labels"))
+    for s in range(3):
+        k1, k2 = torch.from_numpy(mg["keep1"][s]), torch.from_numpy(mg["keep2"][s])
+        st.keep_override = torch.stack([k1, k2]).to(gpu)
+        out = st.step(I.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        r64 = orc.train_step(o64, op64, I.double(), T.double(), y.double(), k1, k2)
+        check(f"logits s{s}", out["logits"], torch.from_numpy(mg["logits"][s]), r64["logits"], FLOOR_OUT)
+        assert abs(out["loss"].item() - float(mg["losses"][s])) <= 1e-5 * abs(float(mg["losses"][s]))
+        if s == 0:
+            gn = np.array([p.grad.double().norm().item() for p in ours.parameters()])
+            np.testing.assert_allclose(gn, mg["grad_norm_step1"], rtol=2e-3, atol=1e-9)
+    ours.eval()
+    ev = ours(I.to(gpu), T.to(gpu))
+    ref_ev = orc.eval_forward(o64, I.double(), T.double())
+    check("eval logits", ev, torch.from_numpy(mg["eval_logits"]), ref_ev, 1e-4)
+
+
+def test_graph_replay_equals_eager(gpu):
+    n = 128
+    a, _, sa, _, _ = _setup(gpu, n, graph=True)
+    b, _, sb, _, _ = _setup(gpu, n, graph=False)
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=8))
+    for s in range(4):
+        keep = _keep(n, 40 + s).to(gpu)
+        sa.keep_override, sb.keep_override = keep, keep
+        sa.step(I, T, y)
+        sb.step(I, T, y)
+    torch.cuda.synchronize()
+    for (na, pa), (_, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(pa, pb), na
+
+
+def test_device_dropout_masks_fresh_per_step(gpu):
+    n = 64
+    ours, opt, st, _, _ = _setup(gpu, n)
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=9))
+    masks = []
+    for _ in range(3):
+        st.step(I, T, y)
+        masks.append(st.eng.keep.clone())
+    torch.cuda.synchronize()
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    frac = torch.stack(masks).float().mean().item()
+    assert 0.47 < frac < 0.53
+
+
+def test_validation_step_and_metrics(gpu):
+    n = 96
+    ours = dropin(1).to(gpu)
+    o64 = orc.build_oracle_mmimdb(1).double()
+    I, T, y = orc.synthetic_batch(n, seed=21)
+    batch = {"image": I, "text": T, "label": y, "pattern_name": ["it"] * n}
+    r = ours.validation_step(batch, None, gpu, None)
+    ref = orc.eval_forward(o64, I.double(), T.double())
+    lref = orc.bce_loss(ref, y.double()).item()
+    assert abs(r["loss"] - lref) <= 1e-5 * abs(lref)
+    eng = ours._engine(n, gpu)
+    eng.stats.zero_()
+    eng.loss_fn(L.stream_handle(), 1.0, False, True)
+    torch.cuda.synchronize()
+    counts = orc.f1_counts(eng.logits.cpu(), y)
+    s = eng.stats.cpu()
+    assert s[1].item() == n
+    np.testing.assert_allclose(s[2:].numpy(), np.array(counts, dtype=np.float32), rtol=1e-6, atol=1e-4)
+
+
+def test_maxout_ties_split_gradient(gpu):
+    n, d = 8, 64
+    a = torch.randn(n, 2 * d, device=gpu)
+    a[:, d:d + 16] = a[:, :16]  # ties
+    dy = torch.randn(n, d, device=gpu)
+    keep = (torch.rand(n, d, device=gpu) > 0.5).to(torch.uint8)
+    y = torch.empty(n, d, device=gpu)
+    da = torch.empty(n, 2 * d, device=gpu)
+    sh = L.stream_handle()
+    L.check(L.lib().tspm_maxout_fwd(n, d, a.data_ptr(), 2 * d, keep.data_ptr(), 2.0, y.data_ptr(), d, sh), "fwd")
+    L.check(L.lib().tspm_maxout_bwd(n, d, dy.data_ptr(), d, a.data_ptr(), 2 * d, keep.data_ptr(), 2.0, da.data_ptr(),
+                                    2 * d, sh), "bwd")
+    torch.cuda.synchronize()
+    a0 = a[:, :d].cpu().requires_grad_(True)
+    a1 = a[:, d:].cpu().requires_grad_(True)
+    ref = torch.max(a0, a1) * (keep.cpu().float() * 2.0)
+    ref.backward(dy.cpu())
+    assert torch.equal(y.cpu(), ref.detach())
+    assert torch.equal(da[:, :d].cpu(), a0.grad) and torch.equal(da[:, d:].cpu(), a1.grad)
+
+
+def test_gmu_kernels_vs_fp64(gpu):
+    n, d = 32, 512
+    g = torch.Generator().manual_seed(4)
+    u = torch.randn(n, 2 * d, generator=g)
+    wz = 0.05 * torch.randn(2 * d, generator=g)
+    dz = torch.randn(n, d, generator=g)
+    ud, wzd = u.to(gpu), wz.to(gpu)
+    h, gate, z = torch.empty(n, 2 * d, device=gpu), torch.empty(n, device=gpu), torch.empty(n, d, device=gpu)
+    du, ds = torch.empty(n, 2 * d, device=gpu), torch.empty(n, device=gpu)
+    sh = L.stream_handle()
+    L.check(L.lib().tspm_gmu_fwd(n, d, ud.data_ptr(), 2 * d, wzd.data_ptr(), h.data_ptr(), 2 * d, gate.data_ptr(),
+                                 z.data_ptr(), d, sh), "gmu_fwd")
+    dzd = dz.to(gpu)
+    L.check(L.lib().tspm_gmu_bwd(n, d, dzd.data_ptr(), d, h.data_ptr(), 2 * d, gate.data_ptr(), wzd.data_ptr(),
+                                 du.data_ptr(), 2 * d, ds.data_ptr(), sh), "gmu_bwd")
+    torch.cuda.synchronize()
+    u64 = u.double().requires_grad_(True)
+    hh = torch.tanh(u64)
+    gg = torch.sigmoid(hh @ wz.double())
+    zz = gg[:, None] * hh[:, :d] + (1 - gg[:, None]) * hh[:, d:]
+    zz.backward(dz.double())
+    assert rel_l2(z, zz) < 1e-6 and rel_l2(gate, gg) < 1e-6
+    assert rel_l2(du, u64.grad) < 1e-5
