@@ -27,6 +27,7 @@ struct GemmArgs {
   const uint8_t* keep;
   float kscale;
   float* rowsum;
+  int vec;  // set by gemm_small: a K-contiguous operand with 16-byte aligned rows (see the main loop)
 };
 
 template <int WK>
@@ -37,7 +38,8 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
   const int row = lane & 31, kh = lane >> 5;
   const int m = tm * 32 + row, col = tn * 32 + row;
-  const int kchunk = ((cdiv_dev(g.K, WK) + 7) / 8) * 8;
+  const int kq = g.vec ? 32 : 8;  // wave K-chunks stay multiples of the main loop's round
+  const int kchunk = ((cdiv_dev(g.K, WK) + kq - 1) / kq) * kq;
   const int kb = wave * kchunk, ke = min(g.K, kb + kchunk);
   const bool mok = m < g.M, nok = col < g.N;
   const float* Ap = g.A + (mok ? (long long)m * g.sam : 0);
@@ -50,6 +52,43 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   // MFMA / row-sum order as the one-step loop below, so results are bitwise unchanged.
   int k0 = kb;
   constexpr int U = 4;
+  // K-contiguous operands (sak == 1 / sbk == 1: the nn.Linear forward x and w, the data-grad dy):
+  // 32 reduction steps per round in a permuted order — lane half kh loads 16 consecutive k
+  // (k0 + 16*kh .. +15) as four 16-byte loads, and MFMA (u, j) pairs k0+4u+j (kh 0) with
+  // k0+16+4u+j (kh 1).  Both operands use the same permutation, so every k is summed exactly once;
+  // each row's 128-byte line is fetched by one instruction group instead of 16 scalar loads.
+  // The uneven-K tail falls through to the loops below (whose k sets are disjoint from these).
+  if (g.vec) {
+    const bool av = g.sak == 1, bv = g.sbk == 1;
+    for (; k0 + 32 <= ke; k0 += 32) {
+      float a[U][4], b[U][4];
+      const int kk = k0 + 16 * kh;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (av) {
+          const float4 v = mok ? *reinterpret_cast<const float4*>(Ap + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+          a[u][0] = v.x; a[u][1] = v.y; a[u][2] = v.z; a[u][3] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[u][j] = mok ? Ap[(long long)(kk + 4 * u + j) * g.sak] : 0.f;
+        }
+        if (bv) {
+          const float4 v = nok ? *reinterpret_cast<const float4*>(Bp + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+          b[u][0] = v.x; b[u][1] = v.y; b[u][2] = v.z; b[u][3] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[u][j] = nok ? Bp[(long long)(kk + 4 * u + j) * g.sbk] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc = mfma32(a[u][j], b[u][j], acc);
+          rs += a[u][j];
+        }
+    }
+  }
   for (; k0 + 8 * U <= ke; k0 += 8 * U) {
     float a[U][4], b[U][4];
 #pragma unroll
@@ -117,7 +156,14 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   if (want_rs && lane < 32 && mok) g.rowsum[m] = rs;
 }
 
-int gemm_small(const GemmArgs& g, hipStream_t st) {
+int gemm_small(const GemmArgs& g0, hipStream_t st) {
+  GemmArgs g = g0;
+  auto rows16 = [](const float* p, long long ld) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
+  };
+  const bool av = g.sak == 1 && rows16(g.A, g.sam), bv = g.sbk == 1 && rows16(g.B, g.sbn);
+  g.vec = (av || bv) && (g.sak == 1 || g.sbk == 1) && g.K >= 64 ? 1 : 0;
+  if (g.vec && ((g.sak == 1 && !av) || (g.sbk == 1 && !bv))) g.vec = 0;
   const int tiles = cdiv(g.M, 32) * cdiv(g.N, 32);
   int wk = 1;
   while (wk < 4 && g.K / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams

@@ -15,8 +15,10 @@
 namespace {
 
 constexpr int kRowThreads = 256;
+constexpr int kLossThreads = 1024;
 
 // Block-wide sum in a fixed order: wave shuffle tree, then wave 0 adds the 4 wave totals.
+template <int NT = kRowThreads>
 TSPM_DEV float block_sum(float v, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -26,7 +28,7 @@ TSPM_DEV float block_sum(float v, float* red) {
   __syncthreads();
   float t = 0.f;
 #pragma unroll
-  for (int w = 0; w < kRowThreads / 64; ++w) t += red[w];
+  for (int w = 0; w < NT / 64; ++w) t += red[w];
   return t;
 }
 
@@ -113,22 +115,22 @@ __global__ __launch_bounds__(256) void k_maxout_bwd(int n, int d, const float* _
 }
 
 // Single workgroup: loss (mean over n*c), dlogits, and the metric counts.
-__global__ __launch_bounds__(kRowThreads) void k_bce_logits(int n, int c, const float* __restrict__ x,
+__global__ __launch_bounds__(kLossThreads) void k_bce_logits(int n, int c, const float* __restrict__ x,
                                                             const float* __restrict__ t, float* __restrict__ loss,
                                                             float* __restrict__ dx, float grad_scale, float threshold,
                                                             float* __restrict__ stats) {
-  __shared__ float red[kRowThreads / 64];
+  __shared__ float red[kLossThreads / 64];
   const long long total = (long long)n * c;
   const float inv = 1.f / (float)total;
   float acc = 0.f;
-  for (long long i = threadIdx.x; i < total; i += kRowThreads) {
+  for (long long i = threadIdx.x; i < total; i += kLossThreads) {
     const float xv = x[i], tv = t[i];
     // ATen: (1 - t) * x - log_sigmoid(x),  log_sigmoid(x) = min(x, 0) - log1p(exp(-|x|))
     const float ls = fminf(xv, 0.f) - log1pf(expf(-fabsf(xv)));
     acc += (1.f - tv) * xv - ls;
     if (dx) dx[i] = (1.f / (1.f + expf(-xv)) - tv) * inv * grad_scale;
   }
-  const float sum = block_sum(acc, red);
+  const float sum = block_sum<kLossThreads>(acc, red);
   const float mean = sum * inv * grad_scale;
   if (threadIdx.x == 0) {
     loss[0] = mean;
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(kRowThreads) void k_bce_logits(int n, int c, const 
   // stats[2] += sum over rows of the per-sample F1 (zero_division = 0); per class k:
   // stats[3+3k+{0,1,2}] += tp, fp, fn.  Thread-exclusive slots, so plain read-modify-write.
   float f1 = 0.f;
-  for (int r = threadIdx.x; r < n; r += kRowThreads) {
+  for (int r = threadIdx.x; r < n; r += kLossThreads) {
     int tp = 0, fp = 0, fn = 0;
     for (int k = 0; k < c; ++k) {
       const bool p = 1.f / (1.f + expf(-x[(long long)r * c + k])) > threshold;
@@ -153,9 +155,9 @@ __global__ __launch_bounds__(kRowThreads) void k_bce_logits(int n, int c, const 
     const int den = 2 * tp + fp + fn;
     f1 += den > 0 ? (2.f * tp) / (float)den : 0.f;
   }
-  const float f1s = block_sum(f1, red);
+  const float f1s = block_sum<kLossThreads>(f1, red);
   if (threadIdx.x == 0) stats[2] += f1s;
-  for (int k = threadIdx.x; k < c; k += kRowThreads) {
+  for (int k = threadIdx.x; k < c; k += kLossThreads) {
     float tp = 0.f, fp = 0.f, fn = 0.f;
     for (int r = 0; r < n; ++r) {
       const bool p = 1.f / (1.f + expf(-x[(long long)r * c + k])) > threshold;
@@ -220,7 +222,7 @@ extern "C" int tspm_maxout_bwd(int32_t n, int32_t d, const float* dy, int32_t ld
 extern "C" int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float* targets, float* loss,
                                float* dlogits, float grad_scale, float threshold, float* stats, tspm_stream_t stream) {
   if (n <= 0 || classes <= 0 || !logits || !targets || !loss) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_bce_logits, dim3(1), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), n, classes, logits,
+  hipLaunchKernelGGL(k_bce_logits, dim3(1), dim3(kLossThreads), 0, static_cast<hipStream_t>(stream), n, classes, logits,
                      targets, loss, dlogits, grad_scale, threshold, stats);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;

@@ -167,14 +167,20 @@ class MMIMDbEngine:
         self.stats = z(3 + 3 * c)
         self.keep_override: Optional[torch.Tensor] = None
         self.rng_ctr_ptr: Optional[int] = None
-        self._check_maxout_weights()
 
-    def _check_maxout_weights(self) -> None:
+    @staticmethod
+    def _adjacent(mo: MaxOut) -> bool:
+        w0, w1 = mo.layers[0].weight, mo.layers[1].weight
+        return w0.is_contiguous() and w1.is_contiguous() and w1.data_ptr() == w0.data_ptr() + w0.numel() * 4
+
+    def check_maxout_weights(self) -> None:
+        """The backward writes both MaxOut units' weight gradients with ONE product: weights and
+        gradients must be adjacent (FusedAdam's flat buffers)."""
         for mo in (self.model.mm_mlp.net[1], self.model.mm_mlp.net[4]):
-            w0, w1 = mo.layers[0].weight, mo.layers[1].weight
-            if w1.data_ptr() != w0.data_ptr() + w0.numel() * 4 or not (w0.is_contiguous() and w1.is_contiguous()):
+            if not self._adjacent(mo):
                 raise L.TspmError("MaxOut units' weights must be adjacent (create FusedAdam over the model's "
                                   "parameters before the first step)")
+            w0, w1 = mo.layers[0].weight, mo.layers[1].weight
             g0, g1 = w0.grad, w1.grad
             if g0 is not None and (g1 is None or g1.data_ptr() != g0.data_ptr() + g0.numel() * 4):
                 raise L.TspmError("MaxOut units' gradients must be adjacent (FusedAdam's flat gradient buffer)")
@@ -234,16 +240,26 @@ class MMIMDbEngine:
                                               self.keep.data_ptr(), sh), "dropout_mask")
             k1, k2 = self.keep[0].data_ptr(), self.keep[1].data_ptr()
         bn("b0", net[0], self.Z, d, self.Zn)
-        L.check(lib.tspm_linear_fwd(n, d, 2 * h, self.Zn.data_ptr(), d, net[1].layers[0].weight.data_ptr(), None, 0,
-                                    None, 1.0, self.A1.data_ptr(), 2 * h, sh), "maxout1")
+        self._maxout_product(net[1], self.Zn, d, self.A1, sh)
         L.check(lib.tspm_maxout_fwd(n, h, self.A1.data_ptr(), 2 * h, k1, scale, self.Y1.data_ptr(), h, sh), "maxout1")
         bn("b1", net[3], self.Y1, h, self.Y1n)
-        L.check(lib.tspm_linear_fwd(n, h, 2 * h, self.Y1n.data_ptr(), h, net[4].layers[0].weight.data_ptr(), None, 0,
-                                    None, 1.0, self.A2.data_ptr(), 2 * h, sh), "maxout2")
+        self._maxout_product(net[4], self.Y1n, h, self.A2, sh)
         L.check(lib.tspm_maxout_fwd(n, h, self.A2.data_ptr(), 2 * h, k2, scale, self.Y2.data_ptr(), h, sh), "maxout2")
         bn("b2", net[6], self.Y2, h, self.Y2n)
         L.check(lib.tspm_linear_fwd(n, h, c, self.Y2n.data_ptr(), h, net[7].weight.data_ptr(), net[7].bias.data_ptr(),
                                     0, None, 1.0, self.logits.data_ptr(), c, sh), "output fc")
+
+    def _maxout_product(self, mo: MaxOut, x, width, A, sh) -> None:
+        """A[:, :h] = x @ W0^T, A[:, h:] = x @ W1^T — one [2h, in] product when the units' weights are
+        adjacent (FusedAdam's flat buffer), else one product per unit into the strided halves."""
+        lib, n, h = L.lib(), self.n, self.h
+        if self._adjacent(mo):
+            L.check(lib.tspm_linear_fwd(n, width, 2 * h, x.data_ptr(), width, mo.layers[0].weight.data_ptr(), None,
+                                        0, None, 1.0, A.data_ptr(), 2 * h, sh), "maxout product")
+            return
+        for u in range(2):
+            L.check(lib.tspm_linear_fwd(n, width, h, x.data_ptr(), width, mo.layers[u].weight.data_ptr(), None, 0,
+                                        None, 1.0, A.data_ptr() + u * h * 4, 2 * h, sh), "maxout product")
 
     def loss_fn(self, sh: int, weight: float, with_grad: bool, stats: bool) -> None:
         L.check(L.lib().tspm_bce_logits(self.n, self.c, self.logits.data_ptr(), self.labels.data_ptr(),
@@ -436,6 +452,7 @@ class FusedMMIMDbStep:
         self.model, self.opt, self.N = model, optimizer, batch
         self.weight = _bce_weight(loss_functions)
         self.eng = MMIMDbEngine(model, batch, dev)
+        self.eng.check_maxout_weights()
         fgs = optimizer.flat_groups()
         self.eng.rng_ctr_ptr = fgs[0].hyper.data_ptr() + L.HYPER_STEP_OFFSET
         self.nbt = shared_batches_tracked(model, dev, (nn.BatchNorm1d,))
