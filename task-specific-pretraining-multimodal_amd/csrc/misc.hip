@@ -30,6 +30,38 @@ struct GemmArgs {
   int vec;  // set by gemm_small: a K-contiguous operand with 16-byte aligned rows (see the main loop)
 };
 
+// One round of UU*8 reduction steps for the K-contiguous path of k_gemm_small: lane half kh covers
+// k = kk .. kk+4*UU-1 (kk = k0 + 4*UU*kh) and MFMA (u, j) pairs k0+4u+j (kh 0) with k0+4*UU+4u+j (kh 1).
+template <int UU>
+TSPM_DEV void vec_round(const float* Ap, const float* Bp, long long sak, long long sbk, bool av, bool bv, bool mok,
+                        bool nok, int kk, f32x16& acc, float& rs) {
+  float a[UU][4], b[UU][4];
+#pragma unroll
+  for (int u = 0; u < UU; ++u) {
+    if (av) {
+      const float4 v = mok ? *reinterpret_cast<const float4*>(Ap + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[u][0] = v.x; a[u][1] = v.y; a[u][2] = v.z; a[u][3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[u][j] = mok ? Ap[(long long)(kk + 4 * u + j) * sak] : 0.f;
+    }
+    if (bv) {
+      const float4 v = nok ? *reinterpret_cast<const float4*>(Bp + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+      b[u][0] = v.x; b[u][1] = v.y; b[u][2] = v.z; b[u][3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[u][j] = nok ? Bp[(long long)(kk + 4 * u + j) * sbk] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UU; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc = mfma32(a[u][j], b[u][j], acc);
+      rs += a[u][j];
+    }
+}
+
 template <int WK>
 __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   extern __shared__ float lds[];
@@ -60,34 +92,9 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   // The uneven-K tail falls through to the loops below (whose k sets are disjoint from these).
   if (g.vec) {
     const bool av = g.sak == 1, bv = g.sbk == 1;
-    for (; k0 + 32 <= ke; k0 += 32) {
-      float a[U][4], b[U][4];
-      const int kk = k0 + 16 * kh;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (av) {
-          const float4 v = mok ? *reinterpret_cast<const float4*>(Ap + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
-          a[u][0] = v.x; a[u][1] = v.y; a[u][2] = v.z; a[u][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) a[u][j] = mok ? Ap[(long long)(kk + 4 * u + j) * g.sak] : 0.f;
-        }
-        if (bv) {
-          const float4 v = nok ? *reinterpret_cast<const float4*>(Bp + kk + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
-          b[u][0] = v.x; b[u][1] = v.y; b[u][2] = v.z; b[u][3] = v.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) b[u][j] = nok ? Bp[(long long)(kk + 4 * u + j) * g.sbk] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc = mfma32(a[u][j], b[u][j], acc);
-          rs += a[u][j];
-        }
-    }
+    // (64-step rounds, vec_round<8>, measured no faster on the MMIMDb shapes: 64 vs 62 us for the
+    // 256x512x4096 product — the 32x32 tile's operand re-reads bound it, not load latency)
+    for (; k0 + 32 <= ke; k0 += 32) vec_round<4>(Ap, Bp, g.sak, g.sbk, av, bv, mok, nok, k0 + 16 * kh, acc, rs);
   }
   for (; k0 + 8 * U <= ke; k0 += 8 * U) {
     float a[U][4], b[U][4];
@@ -162,7 +169,7 @@ int gemm_small(const GemmArgs& g0, hipStream_t st) {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
   };
   const bool av = g.sak == 1 && rows16(g.A, g.sam), bv = g.sbk == 1 && rows16(g.B, g.sbn);
-  g.vec = (av || bv) && (g.sak == 1 || g.sbk == 1) && g.K >= 64 ? 1 : 0;
+  g.vec = (av || bv) && (g.sak == 1 || g.sbk == 1) && g.K >= 128 ? 1 : 0;  // >= 32 k per wave
   if (g.vec && ((g.sak == 1 && !av) || (g.sbk == 1 && !bv))) g.vec = 0;
   const int tiles = cdiv(g.M, 32) * cdiv(g.N, 32);
   int wk = 1;
