@@ -87,7 +87,12 @@ def pmc_traffic(family: str = "conv"):
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.sh + pmc_traffic.py: FETCH_SIZE and
     WRITE_SIZE passes over this same bench command, gfx950 read correction applied).  None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
+    import re
+
+    def ver(p):  # newest = highest r<round>_v<version> (mtimes are equal on a fresh checkout)
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(p))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=ver)
     if not files:
         return None, None, None
     with open(files[-1]) as f:

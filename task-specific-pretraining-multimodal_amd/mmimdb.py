@@ -524,3 +524,95 @@ def f1_metrics(stats: torch.Tensor, classes: int) -> Dict[str, float]:
     return {"loss": float(s[0]) / n, "f1_samples": float(s[2]) / n, "f1_macro": float(f1k.mean()),
             "f1_weighted": float((f1k * sup).sum() / sup.sum()) if float(sup.sum()) > 0 else 0.0,
             "f1_micro": float(2 * tp.sum()) / micro_den if micro_den > 0 else 0.0}
+
+
+# ------------------------------------------------------------------------------------------------
+# input stage + epoch harness
+# ------------------------------------------------------------------------------------------------
+PATTERNS = {"it": (1.0, 1.0), "i": (1.0, 0.0), "t": (0.0, 1.0)}  # (image, text) presence
+
+
+class MMIMDbCorpus:
+    """HBM-resident MM-IMDb features (replaces the per-sample HDF5 reads + collate of
+    MML_Suite/data/mmimdb.py:122-200 and the step's ``.to(device)``; the HDF5 file itself needs h5py,
+    which this image lacks — construct from arrays, e.g. exported once with the reference's reader).
+    ``gather`` assembles a batch on device with the input-stage kernel (``tspm_avmnist_gather`` used
+    as a generic row gather: one launch per tensor, the missing-modality pattern as a row mask)."""
+
+    def __init__(self, image, text, labels, device):
+        t = lambda a: torch.as_tensor(a, dtype=torch.float32).contiguous().to(device)
+        self.image, self.text, self.labels = t(image), t(text), t(labels)
+        self.n = self.image.shape[0]
+        if self.text.shape[0] != self.n or self.labels.shape[0] != self.n:
+            raise L.TspmError("MMIMDbCorpus: image / text / labels row counts differ")
+        self.device = device
+        self._masks: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def _mask(self, n: int, pattern: str):
+        if pattern == "it":
+            return None, None
+        m = self._masks.setdefault(n, {})
+        if pattern not in m:
+            ip, tp = PATTERNS[pattern]
+            m[pattern] = (torch.full((n,), ip, device=self.device), torch.full((n,), tp, device=self.device))
+        return m[pattern]
+
+    def gather(self, index: torch.Tensor, I_out, T_out, Y_out, pattern: str = "it") -> None:
+        lib, sh, n = L.lib(), L.stream_handle(), index.numel()
+        im, tm = self._mask(n, pattern)
+        for src, w, mask, out in ((self.image, self.image.shape[1], im, I_out), (self.text, self.text.shape[1], tm, T_out),
+                                  (self.labels, self.labels.shape[1], None, Y_out)):
+            L.check(lib.tspm_avmnist_gather(n, index.data_ptr(), self.n, src.data_ptr(), w, None, 0, None, None,
+                                            L.ptr(mask), None, out.data_ptr(), None, None, sh), "mmimdb gather")
+
+
+def _evaluate(model: MMIMDb, corpus: MMIMDbCorpus, batch: int, weight: float, pattern: str) -> Dict[str, float]:
+    model.eval()
+    sh = L.stream_handle()
+    stats = None
+    for s in range(0, corpus.n, batch):
+        idx = torch.arange(s, min(s + batch, corpus.n), device=corpus.device)
+        if idx.numel() < 2:
+            break
+        eng = model._engine(idx.numel(), corpus.device)
+        if stats is None:
+            stats = torch.zeros_like(eng.stats)
+        eng.stats.zero_()
+        corpus.gather(idx, eng.I, eng.T, eng.labels, pattern)
+        eng.forward(sh, False)
+        eng.loss_fn(sh, weight, False, True)
+        stats += eng.stats
+    return f1_metrics(stats, model.mm_mlp.output_size)
+
+
+def fit_mmimdb(model: MMIMDb, optimizer: FusedAdam, train: MMIMDbCorpus, val: MMIMDbCorpus, batch: int,
+               epochs: int, loss_functions=None, patience: int = 25, seed: int = 0,
+               patterns=("it", "i", "t")) -> List[Dict[str, Any]]:
+    """The epoch loop of train_multimodal.py for the MMIMDb config (shuffled train batches, drop_last;
+    validation on each selected missing pattern with the absent modality zeroed; early stopping on
+    the full-pattern validation loss with the YAML's patience 25), every batch on the HIP path.
+    Returns one dict per epoch: train loss / f1s and ``val_{pattern}`` metrics."""
+    weight = _bce_weight(loss_functions)
+    step = FusedMMIMDbStep(model, optimizer, loss_functions, batch)
+    step.log_stats = True
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    history, best, bad = [], float("inf"), 0
+    for ep in range(epochs):
+        model.train()
+        step.eng.stats.zero_()
+        perm = torch.randperm(train.n, generator=gen).to(train.device)
+        for s in range(0, train.n - batch + 1, batch):
+            train.gather(perm[s:s + batch], step.eng.I, step.eng.T, step.eng.labels)
+            step.run()
+        rec = {"epoch": ep, "train": f1_metrics(step.eng.stats, model.mm_mlp.output_size)}
+        for p in patterns:
+            rec[f"val_{p}"] = _evaluate(model, val, batch, weight, p)
+        history.append(rec)
+        vl = rec[f"val_{patterns[0]}"]["loss"]
+        if vl < best - 1e-4:
+            best, bad = vl, 0
+        else:
+            bad += 1
+            if bad >= patience:
+                break
+    return history

@@ -207,3 +207,43 @@ def test_gmu_kernels_vs_fp64(gpu):
     zz.backward(dz.double())
     assert rel_l2(z, zz) < 1e-6 and rel_l2(gate, gg) < 1e-6
     assert rel_l2(du, u64.grad) < 1e-5
+
+
+def test_corpus_gather_and_patterns(gpu):
+    I, T, y = orc.synthetic_batch(50, seed=31)
+    c = M.MMIMDbCorpus(I, T, y, gpu)
+    idx = torch.tensor([7, 3, 49, 0, 3], device=gpu)
+    Io, To, Yo = (torch.empty(5, w, device=gpu) for w in (4096, 300, 23))
+    for pat, (ip, tp) in M.PATTERNS.items():
+        c.gather(idx, Io, To, Yo, pat)
+        torch.cuda.synchronize()
+        ii = idx.cpu()
+        assert torch.equal(Io.cpu(), I[ii] * ip) and torch.equal(To.cpu(), T[ii] * tp) and torch.equal(Yo.cpu(), y[ii])
+
+
+def test_fit_loop_metrics_match_oracle(gpu):
+    n_tr, n_va, B = 512, 200, 64
+    I, T, y = orc.synthetic_batch(n_tr, seed=41)
+    Iv, Tv, yv = orc.synthetic_batch(n_va, seed=42)
+    ours = dropin(2).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=1e-4, weight_decay=1e-3)
+    hist = M.fit_mmimdb(ours, opt, M.MMIMDbCorpus(I, T, y, gpu), M.MMIMDbCorpus(Iv, Tv, yv, gpu), B, epochs=3)
+    assert len(hist) == 3
+    assert hist[-1]["train"]["loss"] < hist[0]["train"]["loss"]
+    o = orc.build_oracle_mmimdb(2).double()
+    sd = {k: v.detach().cpu().double() if v.is_floating_point() else v.cpu() for k, v in ours.state_dict().items()}
+    o.load_state_dict(sd)
+    for pat, (ip, tp) in M.PATTERNS.items():
+        logits, loss_sum = [], 0.0
+        for s in range(0, n_va, B):
+            sl = slice(s, min(s + B, n_va))
+            lg = orc.eval_forward(o, Iv[sl].double() * ip, Tv[sl].double() * tp)
+            logits.append(lg)
+            loss_sum += orc.bce_loss(lg, yv[sl].double()).item() * lg.shape[0]
+        lg = torch.cat(logits)
+        c = orc.f1_counts(lg, yv)
+        ref = M.f1_metrics(torch.tensor([loss_sum, float(n_va)] + c, dtype=torch.float64), 23)
+        got = hist[-1][f"val_{pat}"]
+        assert abs(got["loss"] - ref["loss"]) <= 1e-4 * abs(ref["loss"]), pat
+        for k in ("f1_samples", "f1_macro", "f1_weighted", "f1_micro"):
+            assert abs(got[k] - ref[k]) <= 2e-2, (pat, k, got[k], ref[k])
