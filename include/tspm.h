@@ -354,6 +354,17 @@ int tspm_maxout_fwd(int32_t n, int32_t d, const float* a, int32_t lda, const uin
  * half (ATen's derivative of torch.maximum). */
 int tspm_maxout_bwd(int32_t n, int32_t d, const float* dy, int32_t lddy, const float* a, int32_t lda,
                     const uint8_t* keep, float keep_scale, float* da, int32_t ldda, tspm_stream_t stream);
+/* BatchNorm1d, training mode, over x[m, c] (m = batch rows; models/mmimdb.py:78,38-46), in one launch:
+ * batch mean / biased variance for y = gamma*(x-mean)*invstd + beta, running statistics updated with
+ * the unbiased variance (momentum, eps as nn.BatchNorm1d; NULL running buffers skip the update),
+ * save_mean / save_invstd [c] kept for the backward.  No workspace. */
+int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* gamma, const float* beta,
+                  float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                  float* save_invstd, float* y, tspm_stream_t stream);
+/* Its backward in one launch: dgamma = sum(g*xhat), dbeta = sum(g) (written), and (dx nullable)
+ * dx = gamma*invstd*(g - dbeta/m - xhat*dgamma/m). */
+int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const float* mean, const float* invstd,
+                  const float* gamma, float* dgamma, float* dbeta, float* dx, tspm_stream_t stream);
 /* BCEWithLogitsLoss (mean) — LossFunctionGroup{bce_with_logits: w} (experiment_utils/loss.py:52,
  * configs/mmimdb/centralised/mmimdb_baseline.yaml): loss[0] = grad_scale * mean((1-t)*x - logsigmoid(x)),
  * dlogits = (sigmoid(x) - t) * grad_scale / (n*classes) (nullable).  If stats != NULL (3 + 3*classes

@@ -172,6 +172,98 @@ __global__ __launch_bounds__(kLossThreads) void k_bce_logits(int n, int c, const
   }
 }
 
+// BatchNorm1d over [m, c] rows in ONE launch each way (m = the batch, at most a few thousand rows on
+// this path): one workgroup per 64 channels, 16 row groups of 64 lanes — lane = channel, so every row
+// read is one 256-byte coalesced segment; two-pass statistics (sum, then centred squares), row groups
+// combined through LDS in a fixed order (deterministic).  Replaces the stats/finalize/apply triple
+// (forward) and the partial/apply pair (backward) used for BatchNorm2d, whose launch overhead
+// dominates at these sizes.
+constexpr int kBnCh = 64, kBnGroups = 16;  // 1024 threads: 16 row groups keep the per-lane row chain short
+
+TSPM_DEV float bn_group_sum(float v, float* red) {
+  const int ch = threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
+  __syncthreads();
+  red[grp * kBnCh + ch] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int q = 0; q < kBnGroups; ++q) t += red[q * kBnCh + ch];
+  return t;
+}
+
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, int c, const float* __restrict__ x,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float* __restrict__ rmean, float* __restrict__ rvar,
+                                                                float momentum, float eps, float* __restrict__ smean,
+                                                                float* __restrict__ sinvstd, float* __restrict__ y) {
+  __shared__ float red[kBnCh * kBnGroups];
+  const int ch = blockIdx.x * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
+  const bool ok = ch < c;
+  float s = 0.f;
+  if (ok)
+#pragma unroll 4
+    for (int r = grp; r < m; r += kBnGroups) s += x[(long long)r * c + ch];
+  const float mean = bn_group_sum(s, red) / (float)m;
+  float q = 0.f;
+  if (ok)
+#pragma unroll 4
+    for (int r = grp; r < m; r += kBnGroups) {
+      const float d = x[(long long)r * c + ch] - mean;
+      q = fmaf(d, d, q);
+    }
+  const float m2 = bn_group_sum(q, red);
+  const float var = m2 / (float)m;
+  const float invstd = 1.f / sqrtf(var + eps);
+  if (!ok) return;
+  if (grp == 0) {
+    smean[ch] = mean;
+    sinvstd[ch] = invstd;
+    if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mean;
+    if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (m > 1 ? m2 / (float)(m - 1) : m2);
+  }
+  const float ga = gamma[ch], be = beta[ch];
+  for (int r = grp; r < m; r += kBnGroups) {
+    const long long i = (long long)r * c + ch;
+    y[i] = (x[i] - mean) * invstd * ga + be;
+  }
+}
+
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, int c, const float* __restrict__ g,
+                                                                const float* __restrict__ x,
+                                                                const float* __restrict__ mean_,
+                                                                const float* __restrict__ invstd_,
+                                                                const float* __restrict__ gamma,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                float* __restrict__ dx) {
+  __shared__ float red[kBnCh * kBnGroups];
+  const int ch = blockIdx.x * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
+  const bool ok = ch < c;
+  const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
+  float sg = 0.f, sgx = 0.f;
+  if (ok)
+#pragma unroll 4
+    for (int r = grp; r < m; r += kBnGroups) {
+      const long long i = (long long)r * c + ch;
+      const float gv = g[i];
+      sg += gv;
+      sgx = fmaf(gv, (x[i] - mean) * invstd, sgx);
+    }
+  const float tg = bn_group_sum(sg, red);
+  const float tgx = bn_group_sum(sgx, red);
+  if (!ok) return;
+  if (grp == 0) {
+    dgamma[ch] = tgx;
+    dbeta[ch] = tg;
+  }
+  if (!dx) return;
+  const float k = gamma[ch] * invstd, mg = tg / (float)m, mgx = tgx / (float)m;
+  for (int r = grp; r < m; r += kBnGroups) {
+    const long long i = (long long)r * c + ch;
+    dx[i] = k * (g[i] - mg - (x[i] - mean) * invstd * mgx);
+  }
+}
+
 int ew_grid(long long work) {
   long long b = cdiv64(work, 256);
   if (b > 4096) b = 4096;
@@ -224,6 +316,26 @@ extern "C" int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, 
   if (n <= 0 || classes <= 0 || !logits || !targets || !loss) return TSPM_ERR_INVALID;
   hipLaunchKernelGGL(k_bce_logits, dim3(1), dim3(kLossThreads), 0, static_cast<hipStream_t>(stream), n, classes, logits,
                      targets, loss, dlogits, grad_scale, threshold, stats);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* gamma, const float* beta,
+                             float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                             float* save_invstd, float* y, tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || !x || !gamma || !beta || !save_mean || !save_invstd || !y) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn1d_fwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+                     m, c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
+                             const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
+                             tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, dx);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

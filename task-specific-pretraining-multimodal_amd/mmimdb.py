@@ -9,8 +9,8 @@ config/resolvers.py:44-47) with the reference's constructor arguments, attribute
     mm_mlp                   : MLPGenreClassifier     = BN → MaxOut → Dropout → BN → MaxOut → Dropout → BN → Linear
 
 The submodules hold parameters only; every computation runs in ``MMIMDbEngine`` as gfx950 HIP
-kernels behind the C ABI (include/tspm.h): BatchNorm1d = ``tspm_bn_stats/apply/bwd`` over [n, C]
-rows, Linear / MaxOut products = ``tspm_linear_*`` (MFMA small GEMM; the two MaxOut units' weights
+kernels behind the C ABI (include/tspm.h): BatchNorm1d = ``tspm_bn1d_fwd/bwd`` (one launch each way)
+and ``tspm_bn_apply_eval`` over [n, C] rows, Linear / MaxOut products = ``tspm_linear_*`` (MFMA small GEMM; the two MaxOut units' weights
 are adjacent in FusedAdam's flat buffer and run as ONE [2d, in] product), GMU / MaxOut+Dropout /
 BCEWithLogits = ``tspm_gmu_*``, ``tspm_maxout_*``, ``tspm_bce_logits``, Adam = ``tspm_adam_step``.
 ``FusedMMIMDbStep`` captures forward + loss + backward + Adam in one HIP graph.  No CPU or ATen
@@ -156,14 +156,9 @@ class MMIMDbEngine:
         self.dZn, self.dZ, self.dU, self.ds = z(n, d), z(n, d), z(n, 2 * d), z(n)
         self.dEI, self.dET = z(n, e), z(n, e)
         self.dXn = z(n, max(self.di, self.dt))
-        self.dX = z(n, max(self.di, self.dt))
         self.keep = torch.ones(2, n, h, dtype=torch.uint8, device=device)
         widths = (self.di, self.dt, d, h)
         self.stat = {k: (z(w), z(w)) for k, w in zip(("i", "t", "b0", "b1", "b2"), widths + (h,))}
-        lib = L.lib()
-        ws = max([lib.tspm_bn_stats_workspace(n, w) for w in widths] + [lib.tspm_bn_bwd_workspace(n, w) for w in widths])
-        self.ws = torch.zeros(max(int(ws), 16) // 4 + 4, **f)
-        self.ws_bytes = self.ws.numel() * 4
         self.stats = z(3 + 3 * c)
         self.keep_override: Optional[torch.Tensor] = None
         self.rng_ctr_ptr: Optional[int] = None
@@ -187,14 +182,11 @@ class MMIMDbEngine:
 
     # -- helpers ------------------------------------------------------------------------------------
     def _bn_train(self, key, bn, x, width, out, sh):
-        lib = L.lib()
         g, b, rm, rv, eps, mom = _bn(bn)
         mean, inv = self.stat[key]
-        L.check(lib.tspm_bn_stats(self.n, width, x.data_ptr(), 1, 0, None, rm.data_ptr(), rv.data_ptr(), mom, eps,
-                                  mean.data_ptr(), inv.data_ptr(), self.ws.data_ptr(), self.ws_bytes, sh), "bn_stats")
-        L.check(lib.tspm_bn_apply(self.n, width, x.data_ptr(), mean.data_ptr(), inv.data_ptr(), g.data_ptr(),
-                                  b.data_ptr(), 0, None, None, None, None, None, 0, out.data_ptr(), None, 0, sh),
-                "bn_apply")
+        L.check(L.lib().tspm_bn1d_fwd(self.n, width, x.data_ptr(), g.data_ptr(), b.data_ptr(), rm.data_ptr(),
+                                      rv.data_ptr(), mom, eps, mean.data_ptr(), inv.data_ptr(), out.data_ptr(), sh),
+                "bn1d_fwd")
 
     def _bn_eval(self, bn, x, width, out, sh):
         g, b, rm, rv, eps, _ = _bn(bn)
@@ -204,10 +196,9 @@ class MMIMDbEngine:
 
     def _bn_bwd(self, key, bn, g_in, x, width, dx, sh):
         mean, inv = self.stat[key]
-        L.check(L.lib().tspm_bn_bwd(self.n, width, g_in.data_ptr(), None, x.data_ptr(), mean.data_ptr(), inv.data_ptr(),
-                                    bn.weight.data_ptr(), bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
-                                    dx.data_ptr(), None, None, None, None, None, None, None, None, None, None, 0,
-                                    self.ws.data_ptr(), self.ws_bytes, sh), "bn_bwd")
+        L.check(L.lib().tspm_bn1d_bwd(self.n, width, g_in.data_ptr(), x.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                      bn.weight.data_ptr(), bn.weight.grad.data_ptr(), bn.bias.grad.data_ptr(),
+                                      L.ptr(dx), sh), "bn1d_bwd")
 
     # -- forward ------------------------------------------------------------------------------------
     def forward(self, sh: int, train: bool) -> None:
@@ -309,14 +300,14 @@ class MMIMDbEngine:
         for (dUp, fc, E, dE) in ((dU1, gmu.fc_one, self.EI, self.dEI), (dU2, gmu.fc_two, self.ET, self.dET)):
             L.check(lib.tspm_linear_bwd_weight(n, e, d, E.data_ptr(), e, dUp, 2 * d, g(fc.weight), None, sh), "gmu dW")
             L.check(lib.tspm_linear_bwd_data(n, e, d, dUp, 2 * d, fc.weight.data_ptr(), dE.data_ptr(), e, sh), "gmu dX")
-        # encoders (the input-feature gradient is computed into scratch; nothing consumes it)
+        # encoders (the BatchNorm1d input-feature gradient is skipped: nothing consumes it)
         for key, enc, Xn, X, dE, w in (("i", ie, self.XnI, self.I, self.dEI, self.di),
                                        ("t", te, self.XnT, self.T, self.dET, self.dt)):
             L.check(lib.tspm_linear_bwd_weight(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, g(enc[1].weight),
                                                g(enc[1].bias), sh), "encoder fc dW")
             L.check(lib.tspm_linear_bwd_data(n, w, e, dE.data_ptr(), e, enc[1].weight.data_ptr(), self.dXn.data_ptr(),
                                              w, sh), "encoder fc dX")
-            self._bn_bwd(key, enc[0], self.dXn, X, w, self.dX, sh)
+            self._bn_bwd(key, enc[0], self.dXn, X, w, None, sh)  # input-feature gradient not needed
 
 
 # ------------------------------------------------------------------------------------------------

@@ -247,3 +247,32 @@ def test_fit_loop_metrics_match_oracle(gpu):
         assert abs(got["loss"] - ref["loss"]) <= 1e-4 * abs(ref["loss"]), pat
         for k in ("f1_samples", "f1_macro", "f1_weighted", "f1_micro"):
             assert abs(got[k] - ref[k]) <= 2e-2, (pat, k, got[k], ref[k])
+
+
+@pytest.mark.parametrize("m,c", [(4, 300), (128, 4096), (256, 512), (1000, 68)])
+def test_bn1d_kernels_vs_fp64(gpu, m, c):
+    g = torch.Generator().manual_seed(m + c)
+    x = torch.randn(m, c, generator=g) * 3 + 1
+    gy = torch.randn(m, c, generator=g)
+    gamma, beta = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g)
+    rm, rv = torch.randn(c, generator=g), torch.rand(c, generator=g) + 0.5
+    d = lambda t: t.to(gpu).contiguous()
+    xd, gd, bd, rmd, rvd = d(x), d(gamma), d(beta), d(rm), d(rv)
+    mean, inv, y = torch.empty(c, device=gpu), torch.empty(c, device=gpu), torch.empty(m, c, device=gpu)
+    dg, db, dx = torch.empty(c, device=gpu), torch.empty(c, device=gpu), torch.empty(m, c, device=gpu)
+    sh = L.stream_handle()
+    L.check(L.lib().tspm_bn1d_fwd(m, c, xd.data_ptr(), gd.data_ptr(), bd.data_ptr(), rmd.data_ptr(), rvd.data_ptr(),
+                                  0.1, 1e-5, mean.data_ptr(), inv.data_ptr(), y.data_ptr(), sh), "bn1d_fwd")
+    L.check(L.lib().tspm_bn1d_bwd(m, c, d(gy).data_ptr(), xd.data_ptr(), mean.data_ptr(), inv.data_ptr(), gd.data_ptr(),
+                                  dg.data_ptr(), db.data_ptr(), dx.data_ptr(), sh), "bn1d_bwd")
+    torch.cuda.synchronize()
+    bn = torch.nn.BatchNorm1d(c).double()
+    with torch.no_grad():
+        bn.weight.copy_(gamma.double()); bn.bias.copy_(beta.double())
+        bn.running_mean.copy_(rm.double()); bn.running_var.copy_(rv.double())
+    x64 = x.double().requires_grad_(True)
+    y64 = bn(x64)
+    y64.backward(gy.double())
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(rmd, bn.running_mean) < 1e-6 and rel_l2(rvd, bn.running_var) < 1e-6
+    assert rel_l2(dx, x64.grad) < 1e-5 and rel_l2(dg, bn.weight.grad) < 1e-5 and rel_l2(db, bn.bias.grad) < 1e-5
