@@ -240,6 +240,16 @@ int tspm_avgpool_bwd(int32_t npos, int32_t n, int32_t c, const float* dy, int32_
 int tspm_linear_fwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* w,
                     const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
                     int32_t ldy, tspm_stream_t stream);
+/* tspm_linear_fwd with the reduction split over `splits` workgroup slices (ABI 11): for long inputs
+ * with few output tiles (the MMIMDb image encoder, 4096 -> 512 at batch 256: 128 tiles for 256 CUs).
+ * Partial products go to the workspace (tspm_linear_fwd_splitk_workspace bytes; 0 = no split needed)
+ * and a second launch sums the slices in order and applies the epilogue.  Same results as
+ * tspm_linear_fwd up to summation order. */
+int tspm_linear_fwd_splitk(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* w,
+                           const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
+                           int32_t ldy, int32_t splits, void* workspace, size_t workspace_bytes,
+                           tspm_stream_t stream);
+size_t tspm_linear_fwd_splitk_workspace(int32_t n, int32_t in, int32_t out, int32_t splits);
 /* dx = dy @ w  (dx overwritten). */
 int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,
                          float* dx, int32_t ldx, tspm_stream_t stream);

@@ -28,6 +28,8 @@ struct GemmArgs {
   float kscale;
   float* rowsum;
   int vec;  // set by gemm_small: a K-contiguous operand with 16-byte aligned rows (see the main loop)
+  int kslice;   // split-K across workgroups (gridDim.y slices of kslice, multiple of 32); 0 = whole K
+  float* slab;  // split-K: raw partial products to slab[blockIdx.y][M][N] (epilogue in k_splitk_reduce)
 };
 
 // One round of UU*8 reduction steps for the K-contiguous path of k_gemm_small: lane half kh covers
@@ -71,8 +73,10 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   const int row = lane & 31, kh = lane >> 5;
   const int m = tm * 32 + row, col = tn * 32 + row;
   const int kq = g.vec ? 32 : 8;  // wave K-chunks stay multiples of the main loop's round
-  const int kchunk = ((cdiv_dev(g.K, WK) + kq - 1) / kq) * kq;
-  const int kb = wave * kchunk, ke = min(g.K, kb + kchunk);
+  const int kbase = g.kslice ? blockIdx.y * g.kslice : 0;
+  const int kend = g.kslice ? min(g.K, kbase + g.kslice) : g.K;
+  const int kchunk = ((cdiv_dev(kend - kbase, WK) + kq - 1) / kq) * kq;
+  const int kb = kbase + wave * kchunk, ke = min(kend, kb + kchunk);
   const bool mok = m < g.M, nok = col < g.N;
   const float* Ap = g.A + (mok ? (long long)m * g.sam : 0);
   const float* Bp = g.B + (nok ? (long long)col * g.sbn : 0);
@@ -148,6 +152,17 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
     }
   }
   const int ccol = tn * 32 + (lane & 31);
+  if (g.slab) {
+    if (ccol < g.N) {
+      float* sl = g.slab + (long long)blockIdx.y * g.M * g.N;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int cm = tm * 32 + acc_row(r, lane);
+        if (cm < g.M) sl[(long long)cm * g.N + ccol] = acc[r];
+      }
+    }
+    return;
+  }
   if (ccol < g.N) {
     const float bv = g.bias ? g.bias[ccol] : 0.f;
 #pragma unroll
@@ -163,7 +178,23 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   if (want_rs && lane < 32 && mok) g.rowsum[m] = rs;
 }
 
-int gemm_small(const GemmArgs& g0, hipStream_t st) {
+// Split-K combine: C = epi(sum over slices in order of slab[s]) with gemm_small's epilogue.
+__global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs g, int splits) {
+  const long long total = (long long)g.M * g.N;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int cm = (int)(t / g.N), ccol = (int)(t % g.N);
+    float v = 0.f;
+    for (int sidx = 0; sidx < splits; ++sidx) v += g.slab[(long long)sidx * total + t];
+    if (g.bias) v += g.bias[ccol];
+    if (g.relu) v = fmaxf(v, 0.f);
+    if (g.keep) v = g.keep[t] ? v * g.kscale : 0.f;
+    g.C[(long long)cm * g.ldc + ccol] = v;
+  }
+}
+
+int gemm_small(const GemmArgs& g0, hipStream_t st, int splits = 1);
+
+int gemm_small(const GemmArgs& g0, hipStream_t st, int splits) {
   GemmArgs g = g0;
   auto rows16 = [](const float* p, long long ld) {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
@@ -172,15 +203,29 @@ int gemm_small(const GemmArgs& g0, hipStream_t st) {
   g.vec = (av || bv) && (g.sak == 1 || g.sbk == 1) && g.K >= 128 ? 1 : 0;  // >= 32 k per wave
   if (g.vec && ((g.sak == 1 && !av) || (g.sbk == 1 && !bv))) g.vec = 0;
   const int tiles = cdiv(g.M, 32) * cdiv(g.N, 32);
+  const GemmArgs gf = g;  // the final epilogue's arguments
+  int kk = g.K;
+  if (splits > 1) {
+    g.kslice = ((cdiv(g.K, splits) + 31) / 32) * 32;
+    splits = cdiv(g.K, g.kslice);
+    kk = g.kslice;
+  } else {
+    g.slab = nullptr;
+  }
   int wk = 1;
-  while (wk < 4 && g.K / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams
+  while (wk < 4 && kk / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams
   const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  const dim3 grid(tiles, splits > 1 ? splits : 1);
   switch (wk) {
-    case 1: hipLaunchKernelGGL(k_gemm_small<1>, dim3(tiles), dim3(64), lds, st, g); break;
-    case 2: hipLaunchKernelGGL(k_gemm_small<2>, dim3(tiles), dim3(128), lds, st, g); break;
-    default: hipLaunchKernelGGL(k_gemm_small<4>, dim3(tiles), dim3(256), lds, st, g); break;
+    case 1: hipLaunchKernelGGL(k_gemm_small<1>, grid, dim3(64), lds, st, g); break;
+    case 2: hipLaunchKernelGGL(k_gemm_small<2>, grid, dim3(128), lds, st, g); break;
+    default: hipLaunchKernelGGL(k_gemm_small<4>, grid, dim3(256), lds, st, g); break;
   }
   TSPM_LAUNCH_CHECK();
+  if (splits > 1) {
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(grid_for((long long)g.M * g.N)), dim3(256), 0, st, gf, splits);
+    TSPM_LAUNCH_CHECK();
+  }
   return TSPM_OK;
 }
 
@@ -331,6 +376,24 @@ extern "C" int tspm_linear_fwd(int32_t n, int32_t in, int32_t out, const float* 
   // y[n,o] = sum_i x[n,i] w[o,i]:  A = x (m=n, k=i), B(k=i, n=o) = w[o,i]
   GemmArgs g{n, out, in, x, ldx, 1, w, 1, in, y, ldy, b, relu, keep, keep_scale, nullptr};
   return gemm_small(g, static_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t tspm_linear_fwd_splitk_workspace(int32_t n, int32_t in, int32_t out, int32_t splits) {
+  if (n <= 0 || in <= 0 || out <= 0 || splits <= 1) return 0;
+  const int ks = ((cdiv(in, splits) + 31) / 32) * 32;
+  return (size_t)cdiv(in, ks) * n * out * sizeof(float);
+}
+
+extern "C" int tspm_linear_fwd_splitk(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* w,
+                                      const float* b, int32_t relu, const uint8_t* keep, float keep_scale, float* y,
+                                      int32_t ldy, int32_t splits, void* workspace, size_t workspace_bytes,
+                                      tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !w || !y || splits < 1) return TSPM_ERR_INVALID;
+  const size_t need = tspm_linear_fwd_splitk_workspace(n, in, out, splits);
+  if (need > 0 && (!workspace || workspace_bytes < need)) return TSPM_ERR_WORKSPACE;
+  GemmArgs g{n, out, in, x, ldx, 1, w, 1, in, y, ldy, b, relu, keep, keep_scale, nullptr};
+  g.slab = static_cast<float*>(workspace);
+  return gemm_small(g, static_cast<hipStream_t>(stream), need > 0 ? splits : 1);
 }
 
 extern "C" int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,

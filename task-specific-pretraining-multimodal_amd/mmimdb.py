@@ -160,6 +160,15 @@ class MMIMDbEngine:
         widths = (self.di, self.dt, d, h)
         self.stat = {k: (z(w), z(w)) for k, w in zip(("i", "t", "b0", "b1", "b2"), widths + (h,))}
         self.stats = z(3 + 3 * c)
+        # split-K for the long encoder Linear when its output tiles cannot fill the chip
+        import os
+        self.enc_splits = int(os.environ.get("TSPM_MMIMDB_SPLITK", "4"))
+        tiles = -(-n // 32) * -(-e // 32)
+        if self.di < 2048 or tiles >= 256:
+            self.enc_splits = 1
+        wsb = L.lib().tspm_linear_fwd_splitk_workspace(n, self.di, e, self.enc_splits) if self.enc_splits > 1 else 0
+        self.ws = torch.zeros(max(int(wsb) // 4, 4), **f)
+        self.ws_bytes = self.ws.numel() * 4
         self.keep_override: Optional[torch.Tensor] = None
         self.rng_ctr_ptr: Optional[int] = None
 
@@ -210,8 +219,9 @@ class MMIMDbEngine:
             (lambda k, mod, x, w, o: self._bn_eval(mod, x, w, o, sh))
         # encoders: BatchNorm1d → Linear (models/mmimdb.py:78-93)
         bn("i", ie[0], self.I, self.di, self.XnI)
-        L.check(lib.tspm_linear_fwd(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
-                                    ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e, sh), "image fc")
+        L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
+                                           ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e, self.enc_splits,
+                                           self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
         bn("t", te[0], self.T, self.dt, self.XnT)
         L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
                                     te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, sh), "text fc")

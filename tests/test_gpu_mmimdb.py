@@ -276,3 +276,24 @@ def test_bn1d_kernels_vs_fp64(gpu, m, c):
     assert rel_l2(y, y64) < 1e-6
     assert rel_l2(rmd, bn.running_mean) < 1e-6 and rel_l2(rvd, bn.running_var) < 1e-6
     assert rel_l2(dx, x64.grad) < 1e-5 and rel_l2(dg, bn.weight.grad) < 1e-5 and rel_l2(db, bn.bias.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n,k,o,splits", [(256, 4096, 512, 4), (100, 4100, 70, 3), (8, 300, 512, 2)])
+def test_linear_splitk_vs_fp64(gpu, n, k, o, splits):
+    g = torch.Generator().manual_seed(n + k)
+    x, w, b = torch.randn(n, k, generator=g), torch.randn(o, k, generator=g) * 0.02, torch.randn(o, generator=g)
+    ws_b = L.lib().tspm_linear_fwd_splitk_workspace(n, k, o, splits)
+    ws = torch.empty(max(ws_b // 4, 1), device=gpu)
+    y = torch.empty(n, o, device=gpu)
+    xd, wd, bd = x.to(gpu), w.to(gpu), b.to(gpu)
+    L.check(L.lib().tspm_linear_fwd_splitk(n, k, o, xd.data_ptr(), k, wd.data_ptr(), bd.data_ptr(), 0, None, 1.0,
+                                           y.data_ptr(), o, splits, ws.data_ptr(), ws.numel() * 4, L.stream_handle()),
+            "splitk")
+    torch.cuda.synchronize()
+    ref = x.double() @ w.double().T + b.double()
+    assert rel_l2(y, ref) < 1e-5
+    if ws_b:
+        with pytest.raises(tspm_amd.TspmError):
+            L.check(L.lib().tspm_linear_fwd_splitk(n, k, o, xd.data_ptr(), k, wd.data_ptr(), bd.data_ptr(), 0, None,
+                                                   1.0, y.data_ptr(), o, splits, ws.data_ptr(), 4, L.stream_handle()),
+                    "splitk small ws")
