@@ -30,6 +30,7 @@ struct GemmArgs {
   int vec;  // set by gemm_small: a K-contiguous operand with 16-byte aligned rows (see the main loop)
   int kslice;   // split-K across workgroups (gridDim.y slices of kslice, multiple of 32); 0 = whole K
   float* slab;  // split-K: raw partial products to slab[blockIdx.y][M][N] (epilogue in k_splitk_reduce)
+  int quad;     // set by gemm_small: 64x64 tiles, one quadrant per wave (see k_gemm_small)
 };
 
 // One round of UU*8 reduction steps for the K-contiguous path of k_gemm_small: lane half kh covers
@@ -68,19 +69,25 @@ template <int WK>
 __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles_n = cdiv_dev(g.N, 32);
+  // quad mode (g.quad, WK == 4): a 64x64 output tile per workgroup, one 32x32 quadrant per wave over
+  // the whole K — the waves sharing A rows / B columns hit each other's lines in the CU's L1 instead
+  // of re-reading them from L2 (large weight-grad / data-grad products with >= 1024 32x32 tiles).
+  const bool quad = WK == 4 && g.quad;
+  const int ts = quad ? 64 : 32;
+  const int tiles_n = cdiv_dev(g.N, ts);
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
   const int row = lane & 31, kh = lane >> 5;
-  const int m = tm * 32 + row, col = tn * 32 + row;
+  const int row0 = tm * ts + (quad ? (wave >> 1) * 32 : 0), col0 = tn * ts + (quad ? (wave & 1) * 32 : 0);
+  const int m = row0 + row, col = col0 + row;
   const int kq = g.vec ? 32 : 8;  // wave K-chunks stay multiples of the main loop's round
   const int kbase = g.kslice ? blockIdx.y * g.kslice : 0;
   const int kend = g.kslice ? min(g.K, kbase + g.kslice) : g.K;
-  const int kchunk = ((cdiv_dev(kend - kbase, WK) + kq - 1) / kq) * kq;
-  const int kb = kbase + wave * kchunk, ke = min(kend, kb + kchunk);
+  const int kchunk = quad ? kend - kbase : ((cdiv_dev(kend - kbase, WK) + kq - 1) / kq) * kq;
+  const int kb = kbase + (quad ? 0 : wave * kchunk), ke = min(kend, kb + kchunk);
   const bool mok = m < g.M, nok = col < g.N;
   const float* Ap = g.A + (mok ? (long long)m * g.sam : 0);
   const float* Bp = g.B + (nok ? (long long)col * g.sbn : 0);
-  const bool want_rs = g.rowsum != nullptr && tn == 0;
+  const bool want_rs = g.rowsum != nullptr && col0 == 0;
   f32x16 acc = {};
   float rs = 0.f;
   // 4 reduction steps per round with all their loads issued before the MFMAs (the operands come from
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
     }
   }
   if (want_rs) rs += __shfl_xor(rs, 32, 64);
-  if (WK > 1) {
+  if (WK > 1 && !quad) {
     if (wave > 0) {
       float* dst = lds + (wave - 1) * (16 * 64 + 32);
 #pragma unroll
@@ -151,13 +158,13 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
       rs += src[16 * 64 + row];
     }
   }
-  const int ccol = tn * 32 + (lane & 31);
+  const int ccol = col0 + (lane & 31);
   if (g.slab) {
     if (ccol < g.N) {
       float* sl = g.slab + (long long)blockIdx.y * g.M * g.N;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int cm = tm * 32 + acc_row(r, lane);
+        const int cm = row0 + acc_row(r, lane);
         if (cm < g.M) sl[(long long)cm * g.N + ccol] = acc[r];
       }
     }
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
     const float bv = g.bias ? g.bias[ccol] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int cm = tm * 32 + acc_row(r, lane);
+      const int cm = row0 + acc_row(r, lane);
       if (cm >= g.M) continue;
       float v = acc[r] + bv;
       if (g.relu) v = fmaxf(v, 0.f);
@@ -176,6 +183,17 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
     }
   }
   if (want_rs && lane < 32 && mok) g.rowsum[m] = rs;
+}
+
+// Quad tiles are opt-in (TSPM_GEMM_QUAD=1; read once): measured on the MMIMDb image-encoder products
+// at batch 256 they did not pay — weight-grad 25.4 us (25.0 with 32x32 tiles), data-grad 36.8 us
+// (25-31) — the L1 sharing between a workgroup's waves does not materialise for these strides.
+bool getenv_flag_quad() {
+  static const bool v = [] {
+    const char* e = getenv("TSPM_GEMM_QUAD");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 // Split-K combine: C = epi(sum over slices in order of slab[s]) with gemm_small's epilogue.
@@ -214,8 +232,11 @@ int gemm_small(const GemmArgs& g0, hipStream_t st, int splits) {
   }
   int wk = 1;
   while (wk < 4 && kk / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams
-  const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
-  const dim3 grid(tiles, splits > 1 ? splits : 1);
+  // quad tiles where 32x32 tiles are plentiful (>= 1024) and K is short enough for one wave
+  g.quad = (splits <= 1 && tiles >= 1024 && g.K <= 1024 && getenv_flag_quad()) ? 1 : 0;
+  if (g.quad) wk = 4;
+  const size_t lds = g.quad ? 0 : (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  const dim3 grid(g.quad ? cdiv(g.M, 64) * cdiv(g.N, 64) : tiles, splits > 1 ? splits : 1);
   switch (wk) {
     case 1: hipLaunchKernelGGL(k_gemm_small<1>, grid, dim3(64), lds, st, g); break;
     case 2: hipLaunchKernelGGL(k_gemm_small<2>, grid, dim3(128), lds, st, g); break;

@@ -297,3 +297,21 @@ def test_linear_splitk_vs_fp64(gpu, n, k, o, splits):
             L.check(L.lib().tspm_linear_fwd_splitk(n, k, o, xd.data_ptr(), k, wd.data_ptr(), bd.data_ptr(), 0, None,
                                                    1.0, y.data_ptr(), o, splits, ws.data_ptr(), 4, L.stream_handle()),
                     "splitk small ws")
+
+
+@pytest.mark.parametrize("n,k,o", [(256, 4096, 512), (100, 4100, 300), (1024, 512, 1024)])
+def test_linear_backward_large_vs_fp64(gpu, n, k, o):
+    """Large weight-grad / data-grad products (the opt-in 64x64 quad-tile mode, TSPM_GEMM_QUAD=1, is
+    exercised by running this file with that variable set)."""
+    g = torch.Generator().manual_seed(n * 7 + k)
+    x, w, dy = torch.randn(n, k, generator=g), torch.randn(o, k, generator=g) * 0.02, torch.randn(n, o, generator=g)
+    xd, wd, dyd = x.to(gpu), w.to(gpu), dy.to(gpu)
+    dw, db, dx = torch.empty(o, k, device=gpu), torch.empty(o, device=gpu), torch.empty(n, k, device=gpu)
+    sh = L.stream_handle()
+    L.check(L.lib().tspm_linear_bwd_weight(n, k, o, xd.data_ptr(), k, dyd.data_ptr(), o, dw.data_ptr(), db.data_ptr(),
+                                           sh), "bwd_weight")
+    L.check(L.lib().tspm_linear_bwd_data(n, k, o, dyd.data_ptr(), o, wd.data_ptr(), dx.data_ptr(), k, sh), "bwd_data")
+    torch.cuda.synchronize()
+    assert rel_l2(dw, dy.double().T @ x.double()) < 1e-5
+    assert rel_l2(db, dy.double().sum(0)) < 1e-5
+    assert rel_l2(dx, dy.double() @ w.double()) < 1e-5
