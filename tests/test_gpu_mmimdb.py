@@ -315,3 +315,21 @@ def test_linear_backward_large_vs_fp64(gpu, n, k, o):
     assert rel_l2(dw, dy.double().T @ x.double()) < 1e-5
     assert rel_l2(db, dy.double().sum(0)) < 1e-5
     assert rel_l2(dx, dy.double() @ w.double()) < 1e-5
+
+
+def test_two_stream_step_equals_one_stream(gpu, monkeypatch):
+    """TSPM_MMIMDB_STREAMS=2 (text branch on a side stream) computes the same step bitwise."""
+    n = 64
+    a, _, sa, _, _ = _setup(gpu, n)
+    monkeypatch.setenv("TSPM_MMIMDB_STREAMS", "2")
+    b, _, sb, _, _ = _setup(gpu, n)
+    assert sb.eng.side is not None and sa.eng.side is None
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=12))
+    for s in range(3):
+        keep = _keep(n, 60 + s).to(gpu)
+        sa.keep_override, sb.keep_override = keep, keep
+        sa.step(I, T, y)
+        sb.step(I, T, y)
+    torch.cuda.synchronize()
+    for (na, pa), (_, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(pa, pb), na
