@@ -333,3 +333,38 @@ def test_two_stream_step_equals_one_stream(gpu, monkeypatch):
     torch.cuda.synchronize()
     for (na, pa), (_, pb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert torch.equal(pa, pb), na
+
+
+def test_rccl_allreduce_step_equals_plain_step(gpu):
+    """The DP path of the MMIMDb step (captured fwd/bwd graph | RCCL all-reduce of the flat gradient |
+    Adam) under a 1-rank RCCL group (all-reduce = identity) gives bitwise the plain step's parameters."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from tspm_amd import ddp
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+        created = True
+    try:
+        n, res = 64, []
+        I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=13))
+        for dp in (False, True):
+            ours = dropin(5).to(gpu)
+            opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+            ar = ddp.GradAllReduce([fg.grad for fg in opt.flat_groups()]) if dp else None
+            st = M.FusedMMIMDbStep(ours, opt, None, n, allreduce=ar)
+            for s in range(4):
+                st.keep_override = _keep(n, 70 + s).to(gpu)
+                st.step(I, T, y)
+            torch.cuda.synchronize()
+            res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
+        assert torch.equal(res[0], res[1])
+    finally:
+        if created:
+            dist.destroy_process_group()
