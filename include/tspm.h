@@ -256,6 +256,11 @@ int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, in
 /* dw = dy^T @ x, db = sum_n dy (both overwritten). */
 int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx,
                            const float* dy, int32_t ldy, float* dw, float* db, tspm_stream_t stream);
+/* Both backward products of one nn.Linear in ONE launch (ABI 11): dw = dy^T @ x, db = sum_n dy
+ * (db nullable), and, if dx != NULL, dx = dy @ w (row stride lddx) — bitwise the results of
+ * tspm_linear_bwd_weight + tspm_linear_bwd_data (same per-product reduction split). */
+int tspm_linear_bwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy, int32_t ldy,
+                    const float* w, float* dw, float* db, float* dx, int32_t lddx, tspm_stream_t stream);
 /* In-place gradient masking through a ReLU(+dropout) output y: g = (y > 0) ? g * scale : 0
  * (scale = 1/(1-p) when y is the post-dropout output — y > 0 implies the unit was kept). */
 int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,

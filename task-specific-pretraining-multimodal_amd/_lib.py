@@ -98,6 +98,7 @@ _SIGS = {
     "tspm_linear_fwd_splitk": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, c_float, _P,
                                          c_int32, c_int32, _P, c_size_t, _P]),
     "tspm_linear_fwd_splitk_workspace": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
+    "tspm_linear_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, _P, c_int32, _P]),
     "tspm_linear_bwd_data": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P]),
     "tspm_linear_bwd_weight": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P]),
     "tspm_act_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, c_float, _P]),

@@ -31,6 +31,7 @@ struct GemmArgs {
   int kslice;   // split-K across workgroups (gridDim.y slices of kslice, multiple of 32); 0 = whole K
   float* slab;  // split-K: raw partial products to slab[blockIdx.y][M][N] (epilogue in k_splitk_reduce)
   int quad;     // set by gemm_small: 64x64 tiles, one quadrant per wave (see k_gemm_small)
+  int wkeff;    // pair launches: the product's own wave count (K split as in its own launch; extra waves idle)
 };
 
 // One round of UU*8 reduction steps for the K-contiguous path of k_gemm_small: lane half kh covers
@@ -66,8 +67,7 @@ TSPM_DEV void vec_round(const float* Ap, const float* Bp, long long sak, long lo
 }
 
 template <int WK>
-__global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
-  extern __shared__ float lds[];
+TSPM_DEV void gemm_body(const GemmArgs& g, int bid, float* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // quad mode (g.quad, WK == 4): a 64x64 output tile per workgroup, one 32x32 quadrant per wave over
   // the whole K — the waves sharing A rows / B columns hit each other's lines in the CU's L1 instead
@@ -75,14 +75,15 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
   const bool quad = WK == 4 && g.quad;
   const int ts = quad ? 64 : 32;
   const int tiles_n = cdiv_dev(g.N, ts);
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int row = lane & 31, kh = lane >> 5;
   const int row0 = tm * ts + (quad ? (wave >> 1) * 32 : 0), col0 = tn * ts + (quad ? (wave & 1) * 32 : 0);
   const int m = row0 + row, col = col0 + row;
   const int kq = g.vec ? 32 : 8;  // wave K-chunks stay multiples of the main loop's round
   const int kbase = g.kslice ? blockIdx.y * g.kslice : 0;
   const int kend = g.kslice ? min(g.K, kbase + g.kslice) : g.K;
-  const int kchunk = quad ? kend - kbase : ((cdiv_dev(kend - kbase, WK) + kq - 1) / kq) * kq;
+  const int wks = g.wkeff > 0 ? g.wkeff : WK;
+  const int kchunk = quad ? kend - kbase : ((cdiv_dev(kend - kbase, wks) + kq - 1) / kq) * kq;
   const int kb = kbase + (quad ? 0 : wave * kchunk), ke = min(kend, kb + kchunk);
   const bool mok = m < g.M, nok = col < g.N;
   const float* Ap = g.A + (mok ? (long long)m * g.sam : 0);
@@ -183,6 +184,24 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
     }
   }
   if (want_rs && lane < 32 && mok) g.rowsum[m] = rs;
+}
+
+template <int WK>
+__global__ __launch_bounds__(64 * WK) void k_gemm_small(GemmArgs g) {
+  extern __shared__ float lds[];
+  gemm_body<WK>(g, blockIdx.x, lds);
+}
+
+// Two independent products in one launch (the weight-grad and data-grad of one nn.Linear): blocks
+// [0, tiles_a) run `a`, the rest run `b` — a workgroup-uniform branch, same body, same results as two
+// launches.
+template <int WK>
+__global__ __launch_bounds__(64 * WK) void k_gemm_pair(GemmArgs a, GemmArgs b, int tiles_a) {
+  extern __shared__ float lds[];
+  if ((int)blockIdx.x < tiles_a)
+    gemm_body<WK>(a, blockIdx.x, lds);
+  else
+    gemm_body<WK>(b, blockIdx.x - tiles_a, lds);
 }
 
 // Quad tiles are opt-in (TSPM_GEMM_QUAD=1; read once): measured on the MMIMDb image-encoder products
@@ -431,6 +450,47 @@ extern "C" int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const 
   // dw[o,i] = sum_n dy[n,o] x[n,i]  (A(m=o, k=n) = dy[n,o]);  db[o] = sum_n dy[n,o]
   GemmArgs g{out, in, n, dy, 1, ldy, x, ldx, 1, dw, in, nullptr, 0, nullptr, 1.f, db};
   return gemm_small(g, static_cast<hipStream_t>(stream));
+}
+
+// K-contiguity / vector decision and wave count of gemm_small, for a pair launch (no split, no quad).
+int gemm_wk(GemmArgs& g) {
+  auto rows16 = [](const float* p, long long ld) {
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
+  };
+  const bool av = g.sak == 1 && rows16(g.A, g.sam), bv = g.sbk == 1 && rows16(g.B, g.sbn);
+  g.vec = (av || bv) && (g.sak == 1 || g.sbk == 1) && g.K >= 128 ? 1 : 0;
+  if (g.vec && ((g.sak == 1 && !av) || (g.sbk == 1 && !bv))) g.vec = 0;
+  g.kslice = 0;
+  g.slab = nullptr;
+  g.quad = 0;
+  int wk = 1;
+  while (wk < 4 && g.K / (wk * 2) >= 32) wk *= 2;
+  g.wkeff = wk;
+  return wk;
+}
+
+extern "C" int tspm_linear_bwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy,
+                               int32_t ldy, const float* w, float* dw, float* db, float* dx, int32_t lddx,
+                               tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !dy || !dw) return TSPM_ERR_INVALID;
+  if (dx && (!w || lddx < in)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // dw[o,i] = sum_n dy[n,o] x[n,i] (+ db = row sums);  dx[n,i] = sum_o dy[n,o] w[o,i]
+  GemmArgs a{out, in, n, dy, 1, ldy, x, ldx, 1, dw, in, nullptr, 0, nullptr, 1.f, db};
+  if (!dx) return gemm_small(a, st);
+  GemmArgs b{n, in, out, dy, ldy, 1, w, in, 1, dx, lddx, nullptr, 0, nullptr, 1.f, nullptr};
+  const int wa = gemm_wk(a), wb = gemm_wk(b);
+  const int wk = wa > wb ? wa : wb;  // a product with fewer waves of its own leaves the extra ones idle
+  // (empty K range, zero partials in the fixed-order combine): bitwise the two separate launches
+  const int ta = cdiv(a.M, 32) * cdiv(a.N, 32), tb = cdiv(b.M, 32) * cdiv(b.N, 32);
+  const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  switch (wk) {
+    case 1: hipLaunchKernelGGL(k_gemm_pair<1>, dim3(ta + tb), dim3(64), lds, st, a, b, ta); break;
+    case 2: hipLaunchKernelGGL(k_gemm_pair<2>, dim3(ta + tb), dim3(128), lds, st, a, b, ta); break;
+    default: hipLaunchKernelGGL(k_gemm_pair<4>, dim3(ta + tb), dim3(256), lds, st, a, b, ta); break;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
 }
 
 extern "C" int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,

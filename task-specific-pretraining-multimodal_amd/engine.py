@@ -18,6 +18,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 
 from . import _lib as L
+from .linear import linear_bwd
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
@@ -563,13 +564,10 @@ class EncoderEngine:
         N = self.N
         if phase in (0, 1):
             fc = self.enc.fc
-            L.check(lib.tspm_linear_bwd_weight(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
-                                               g_emb.data_ptr(), ld_g, self._grad(fc.weight).data_ptr(),
-                                               self._grad(fc.bias).data_ptr() if fc.bias is not None else None, sh),
-                    "linear_bwd_weight(fc)")
-            L.check(lib.tspm_linear_bwd_data(N, self.final_c, self.hidden, g_emb.data_ptr(), ld_g,
-                                             fc.weight.data_ptr(), self.g_pooled.data_ptr(), self.final_c, sh),
-                    "linear_bwd_data(fc)")
+            linear_bwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c, g_emb.data_ptr(), ld_g,
+                       fc.weight.data_ptr(), self._grad(fc.weight).data_ptr(),
+                       self._grad(fc.bias).data_ptr() if fc.bias is not None else None, self.g_pooled.data_ptr(),
+                       self.final_c, sh)
             h, w = self.final_hw
             G, Gn = self.gA, self.gB
             L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(),

@@ -27,6 +27,7 @@ import torch
 from torch import nn
 
 from . import _lib as L
+from .linear import linear_bwd
 from .optim import FusedAdam
 from .step import shared_batches_tracked
 
@@ -298,26 +299,20 @@ class MMIMDbEngine:
         k2 = self.keep[1].data_ptr() if self.p > 0 else None
         g = lambda p: p.grad.data_ptr()
         # output Linear
-        L.check(lib.tspm_linear_bwd_weight(n, h, c, self.Y2n.data_ptr(), h, self.dlogits.data_ptr(), c,
-                                           g(net[7].weight), g(net[7].bias), sh), "output fc dW")
-        L.check(lib.tspm_linear_bwd_data(n, h, c, self.dlogits.data_ptr(), c, net[7].weight.data_ptr(),
-                                         self.dY2n.data_ptr(), h, sh), "output fc dX")
+        linear_bwd(n, h, c, self.Y2n.data_ptr(), h, self.dlogits.data_ptr(), c, net[7].weight.data_ptr(),
+                   g(net[7].weight), g(net[7].bias), self.dY2n.data_ptr(), h, sh)
         self._bn_bwd("b2", net[6], self.dY2n, self.Y2, h, self.dY2, sh)
         # MaxOut 2 (+ dropout)
         L.check(lib.tspm_maxout_bwd(n, h, self.dY2.data_ptr(), h, self.A2.data_ptr(), 2 * h, k2, scale,
                                     self.dA2.data_ptr(), 2 * h, sh), "maxout2 bwd")
-        L.check(lib.tspm_linear_bwd_weight(n, h, 2 * h, self.Y1n.data_ptr(), h, self.dA2.data_ptr(), 2 * h,
-                                           g(net[4].layers[0].weight), None, sh), "maxout2 dW")
-        L.check(lib.tspm_linear_bwd_data(n, h, 2 * h, self.dA2.data_ptr(), 2 * h, net[4].layers[0].weight.data_ptr(),
-                                         self.dY1n.data_ptr(), h, sh), "maxout2 dX")
+        linear_bwd(n, h, 2 * h, self.Y1n.data_ptr(), h, self.dA2.data_ptr(), 2 * h, net[4].layers[0].weight.data_ptr(),
+                   g(net[4].layers[0].weight), None, self.dY1n.data_ptr(), h, sh)
         self._bn_bwd("b1", net[3], self.dY1n, self.Y1, h, self.dY1, sh)
         # MaxOut 1 (+ dropout)
         L.check(lib.tspm_maxout_bwd(n, h, self.dY1.data_ptr(), h, self.A1.data_ptr(), 2 * h, k1, scale,
                                     self.dA1.data_ptr(), 2 * h, sh), "maxout1 bwd")
-        L.check(lib.tspm_linear_bwd_weight(n, d, 2 * h, self.Zn.data_ptr(), d, self.dA1.data_ptr(), 2 * h,
-                                           g(net[1].layers[0].weight), None, sh), "maxout1 dW")
-        L.check(lib.tspm_linear_bwd_data(n, d, 2 * h, self.dA1.data_ptr(), 2 * h, net[1].layers[0].weight.data_ptr(),
-                                         self.dZn.data_ptr(), d, sh), "maxout1 dX")
+        linear_bwd(n, d, 2 * h, self.Zn.data_ptr(), d, self.dA1.data_ptr(), 2 * h, net[1].layers[0].weight.data_ptr(),
+                   g(net[1].layers[0].weight), None, self.dZn.data_ptr(), d, sh)
         self._bn_bwd("b0", net[0], self.dZn, self.Z, d, self.dZ, sh)
         # GMU
         L.check(lib.tspm_gmu_bwd(n, d, self.dZ.data_ptr(), d, self.H.data_ptr(), 2 * d, self.gate.data_ptr(),
@@ -330,13 +325,11 @@ class MMIMDbEngine:
         for (dUp, fc, E, dE, key, enc, Xn, X, w, dXn, q) in (
                 (dU2, gmu.fc_two, self.ET, self.dET, "t", te, self.XnT, self.T, self.dt, self.dXnT, st),
                 (dU1, gmu.fc_one, self.EI, self.dEI, "i", ie, self.XnI, self.I, self.di, self.dXn, sh)):
-            L.check(lib.tspm_linear_bwd_weight(n, e, d, E.data_ptr(), e, dUp, 2 * d, g(fc.weight), None, q), "gmu dW")
-            L.check(lib.tspm_linear_bwd_data(n, e, d, dUp, 2 * d, fc.weight.data_ptr(), dE.data_ptr(), e, q), "gmu dX")
+            linear_bwd(n, e, d, E.data_ptr(), e, dUp, 2 * d, fc.weight.data_ptr(), g(fc.weight), None, dE.data_ptr(),
+                       e, q)
             # encoder (the BatchNorm1d input-feature gradient is skipped: nothing consumes it)
-            L.check(lib.tspm_linear_bwd_weight(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, g(enc[1].weight),
-                                               g(enc[1].bias), q), "encoder fc dW")
-            L.check(lib.tspm_linear_bwd_data(n, w, e, dE.data_ptr(), e, enc[1].weight.data_ptr(), dXn.data_ptr(),
-                                             w, q), "encoder fc dX")
+            linear_bwd(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, enc[1].weight.data_ptr(), g(enc[1].weight),
+                       g(enc[1].bias), dXn.data_ptr(), w, q)
             self._bn_bwd(key, enc[0], dXn, X, w, None, q)
         self._join()
 

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
+from .linear import linear_bwd
 from .engine import EncoderEngine, prepare_encoder_layout
 from .metrics import ClassificationLog, DeviceMetricRecorder
 from .optim import FusedAdam
@@ -241,10 +242,8 @@ class FusedMonoStep(_MonoBuffers):
                                        self.dlogits.data_ptr(), self.ce_weight, self.stats.data_ptr(), sh),
                 "cross_entropy")
         self._classify(lib, sh)
-        L.check(lib.tspm_linear_bwd_weight(n, hid, K, self.emb.data_ptr(), hid, self.dlogits.data_ptr(), K,
-                                           cls.weight.grad.data_ptr(), cls.bias.grad.data_ptr(), sh), "classifier wgrad")
-        L.check(lib.tspm_linear_bwd_data(n, hid, K, self.dlogits.data_ptr(), K, cls.weight.data_ptr(),
-                                         self.demb.data_ptr(), hid, sh), "classifier dgrad")
+        linear_bwd(n, hid, K, self.emb.data_ptr(), hid, self.dlogits.data_ptr(), K, cls.weight.data_ptr(),
+                   cls.weight.grad.data_ptr(), cls.bias.grad.data_ptr(), self.demb.data_ptr(), hid, sh)
         self.eng.backward(self.demb, hid)
         self.nbt.add_(1)
         self.opt.launch(sh)

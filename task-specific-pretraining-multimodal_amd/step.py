@@ -25,6 +25,7 @@ from . import _lib as L
 from .engine import EncoderEngine, prepare_encoder_layout
 from .ddp import PhasedGradAllReduce
 from .optim import FusedAdam
+from .linear import linear_bwd
 
 NUM_CLASSES = 10
 
@@ -186,22 +187,17 @@ class FusedTrainStep:
         n, F, hd, h2 = self.N, self.F, self.hd, self.h2
         net = self.model.net
         g = lambda p: p.grad  # noqa: E731  (flat views)
-        L.check(lib.tspm_linear_bwd_weight(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, self.dlogits.data_ptr(),
-                                           NUM_CLASSES, g(net[5].weight).data_ptr(), g(net[5].bias).data_ptr(), sh),
-                "head fc5 wgrad")
-        L.check(lib.tspm_linear_bwd_data(n, h2, NUM_CLASSES, self.dlogits.data_ptr(), NUM_CLASSES,
-                                         net[5].weight.data_ptr(), self.dh.data_ptr(), h2, sh), "head fc5 dgrad")
+        # each layer's weight-grad and data-grad in one launch (tspm_linear_bwd, bitwise the two launches)
+        linear_bwd(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, self.dlogits.data_ptr(), NUM_CLASSES,
+                   net[5].weight.data_ptr(), g(net[5].weight).data_ptr(), g(net[5].bias).data_ptr(),
+                   self.dh.data_ptr(), h2, sh)
         L.check(lib.tspm_act_bwd(n, h2, self.dh.data_ptr(), h2, self.hh.data_ptr(), h2, 1.0, sh), "head relu")
-        L.check(lib.tspm_linear_bwd_weight(n, hd, h2, self.h1.data_ptr(), hd, self.dh.data_ptr(), h2,
-                                           g(net[3].weight).data_ptr(), g(net[3].bias).data_ptr(), sh), "head fc3 wgrad")
-        L.check(lib.tspm_linear_bwd_data(n, hd, h2, self.dh.data_ptr(), h2, net[3].weight.data_ptr(),
-                                         self.dh1.data_ptr(), hd, sh), "head fc3 dgrad")
+        linear_bwd(n, hd, h2, self.h1.data_ptr(), hd, self.dh.data_ptr(), h2, net[3].weight.data_ptr(),
+                   g(net[3].weight).data_ptr(), g(net[3].bias).data_ptr(), self.dh1.data_ptr(), hd, sh)
         L.check(lib.tspm_act_bwd(n, hd, self.dh1.data_ptr(), hd, self.h1.data_ptr(), hd, self._scale, sh),
                 "head relu+dropout")
-        L.check(lib.tspm_linear_bwd_weight(n, F, hd, self.fused.data_ptr(), F, self.dh1.data_ptr(), hd,
-                                           g(net[0].weight).data_ptr(), g(net[0].bias).data_ptr(), sh), "head fc0 wgrad")
-        L.check(lib.tspm_linear_bwd_data(n, F, hd, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
-                                         self.dfused.data_ptr(), F, sh), "head fc0 dgrad")
+        linear_bwd(n, F, hd, self.fused.data_ptr(), F, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
+                   g(net[0].weight).data_ptr(), g(net[0].bias).data_ptr(), self.dfused.data_ptr(), F, sh)
 
     def _fwd_bwd(self, phase: int = 0) -> None:
         """Enqueue forward + loss + backward on the current stream (+ the side stream).  phase 0:

@@ -368,3 +368,24 @@ def test_rccl_allreduce_step_equals_plain_step(gpu):
     finally:
         if created:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,fin,fout", [(128, 192, 128), (128, 512, 64), (256, 4096, 512), (7, 33, 10)])
+def test_linear_bwd_pair_bitwise_equals_two_launches(gpu, n, fin, fout):
+    g = torch.Generator().manual_seed(n + fin + fout)
+    x, w, dy = torch.randn(n, fin, generator=g), torch.randn(fout, fin, generator=g), torch.randn(n, fout, generator=g)
+    xd, wd, dyd = x.to(gpu), w.to(gpu), dy.to(gpu)
+    out = [(torch.empty(fout, fin, device=gpu), torch.empty(fout, device=gpu), torch.empty(n, fin, device=gpu))
+           for _ in range(2)]
+    sh, lib = L.stream_handle(), L.lib()
+    dw, db, dx = out[0]
+    L.check(lib.tspm_linear_bwd(n, fin, fout, xd.data_ptr(), fin, dyd.data_ptr(), fout, wd.data_ptr(), dw.data_ptr(),
+                                db.data_ptr(), dx.data_ptr(), fin, sh), "pair")
+    dw, db, dx = out[1]
+    L.check(lib.tspm_linear_bwd_weight(n, fin, fout, xd.data_ptr(), fin, dyd.data_ptr(), fout, dw.data_ptr(),
+                                       db.data_ptr(), sh), "w")
+    L.check(lib.tspm_linear_bwd_data(n, fin, fout, dyd.data_ptr(), fout, wd.data_ptr(), dx.data_ptr(), fin, sh), "d")
+    torch.cuda.synchronize()
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+    assert rel_l2(out[0][2], dy.double() @ w.double()) < 1e-5
