@@ -380,6 +380,11 @@ int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* gamma, cons
  * dx = gamma*invstd*(g - dbeta/m - xhat*dgamma/m). */
 int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const float* mean, const float* invstd,
                   const float* gamma, float* dgamma, float* dbeta, float* dx, tspm_stream_t stream);
+/* tspm_bn1d_bwd fused with the backward of the MaxOut(2)+Dropout that produced x (ABI 11): instead of
+ * dx, writes da[m, 2c] exactly as tspm_maxout_bwd(dx, a, keep, keep_scale) would (bitwise). */
+int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
+                         const float* invstd, const float* gamma, float* dgamma, float* dbeta, const float* a,
+                         const uint8_t* keep, float keep_scale, float* da, tspm_stream_t stream);
 /* BCEWithLogitsLoss (mean) — LossFunctionGroup{bce_with_logits: w} (experiment_utils/loss.py:52,
  * configs/mmimdb/centralised/mmimdb_baseline.yaml): loss[0] = grad_scale * mean((1-t)*x - logsigmoid(x)),
  * dlogits = (sigmoid(x) - t) * grad_scale / (n*classes) (nullable).  If stats != NULL (3 + 3*classes

@@ -235,7 +235,9 @@ __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, int c, co
                                                                 const float* __restrict__ invstd_,
                                                                 const float* __restrict__ gamma,
                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                float* __restrict__ dx) {
+                                                                float* __restrict__ dx, const float* __restrict__ mo_a,
+                                                                const uint8_t* __restrict__ mo_keep, float mo_scale,
+                                                                float* __restrict__ mo_da) {
   __shared__ float red[kBnCh * kBnGroups];
   const int ch = blockIdx.x * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
@@ -256,11 +258,19 @@ __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, int c, co
     dgamma[ch] = tgx;
     dbeta[ch] = tg;
   }
-  if (!dx) return;
+  if (!dx && !mo_da) return;
   const float k = gamma[ch] * invstd, mg = tg / (float)m, mgx = tgx / (float)m;
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
-    dx[i] = k * (g[i] - mg - (x[i] - mean) * invstd * mgx);
+    const float v = k * (g[i] - mg - (x[i] - mean) * invstd * mgx);
+    if (dx) dx[i] = v;
+    if (mo_da) {  // x was MaxOut(2)+Dropout of a[m, 2c]: route v as k_maxout_bwd does
+      const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;
+      const float a0 = mo_a[(long long)r * 2 * c + ch], a1 = mo_a[(long long)r * 2 * c + c + ch];
+      const float half = 0.5f * gv;
+      mo_da[(long long)r * 2 * c + ch] = a0 > a1 ? gv : (a0 == a1 ? half : 0.f);
+      mo_da[(long long)r * 2 * c + c + ch] = a1 > a0 ? gv : (a0 == a1 ? half : 0.f);
+    }
   }
 }
 
@@ -335,7 +345,19 @@ extern "C" int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* 
                              tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
   hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
-                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, dx);
+                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
+                                    const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                                    const float* a, const uint8_t* keep, float keep_scale, float* da,
+                                    tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta || !a || !da)
+    return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

@@ -389,3 +389,19 @@ def test_linear_bwd_pair_bitwise_equals_two_launches(gpu, n, fin, fout):
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
     assert rel_l2(out[0][2], dy.double() @ w.double()) < 1e-5
+
+
+def test_fused_bn_maxout_backward_equals_separate(gpu, monkeypatch):
+    """tspm_bn1d_bwd_maxout (BatchNorm1d backward + MaxOut/Dropout backward in one launch) gives bitwise
+    the step of the separate tspm_bn1d_bwd + tspm_maxout_bwd launches."""
+    n, res = 96, []
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=14))
+    for fuse in (True, False):
+        monkeypatch.setattr(M, "_FUSE_BN_MAXOUT", fuse)
+        ours, _, st, _, _ = _setup(gpu, n)
+        for s in range(3):
+            st.keep_override = _keep(n, 80 + s).to(gpu)
+            st.step(I, T, y)
+        torch.cuda.synchronize()
+        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
+    assert torch.equal(res[0], res[1])
