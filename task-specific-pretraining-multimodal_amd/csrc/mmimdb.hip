@@ -173,12 +173,17 @@ __global__ __launch_bounds__(kLossThreads) void k_bce_logits(int n, int c, const
 }
 
 // BatchNorm1d over [m, c] rows in ONE launch each way (m = the batch, at most a few thousand rows on
-// this path): one workgroup per 64 channels, 16 row groups of 64 lanes — lane = channel, so every row
-// read is one 256-byte coalesced segment; two-pass statistics (sum, then centred squares), row groups
+// this path): one workgroup per kBnCh channels, kBnGroups row groups — lane = channel, so every row
+// read is one coalesced segment; two-pass statistics (sum, then centred squares), row groups
 // combined through LDS in a fixed order (deterministic).  Replaces the stats/finalize/apply triple
 // (forward) and the partial/apply pair (backward) used for BatchNorm2d, whose launch overhead
 // dominates at these sizes.
-constexpr int kBnCh = 64, kBnGroups = 16;  // 1024 threads: 16 row groups keep the per-lane row chain short
+#ifndef TSPM_BN1D_CH
+#define TSPM_BN1D_CH 32
+#endif
+// 1024 threads: 32 channels (one 128-byte line per row) x 32 row groups keep the per-lane row chain
+// short and put c/32 workgroups on the chip (64 channels x 16 groups: 6.2-6.8 us per launch at c=512)
+constexpr int kBnCh = TSPM_BN1D_CH, kBnGroups = 1024 / TSPM_BN1D_CH;
 
 TSPM_DEV float bn_group_sum(float v, float* red) {
   const int ch = threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
