@@ -82,7 +82,7 @@ class ConvTimer:
         return len(self.events), flops, tot_ms
 
 
-def pmc_traffic(family: str = "conv"):
+def pmc_traffic(family: str = "conv", path: str = "main"):
     """HBM bytes per step of one kernel family from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.sh + pmc_traffic.py: FETCH_SIZE and
     WRITE_SIZE passes over this same bench command, gfx950 read correction applied).  None if absent."""
@@ -93,10 +93,15 @@ def pmc_traffic(family: str = "conv"):
         m = re.search(r"r(\d+)_v(\d+)", os.path.basename(p))
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=ver)
+    # "main": the AVMNIST summaries (r1_vN_pmc_traffic.json); "mmimdb": r1_vN_mmimdb_pmc_traffic.json
+    files = [f for f in files if ("_mmimdb_" in os.path.basename(f)) == (path == "mmimdb")]
     if not files:
         return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
+    if family == "step":
+        tot = d.get("per_step_total_bytes")
+        return (tot, None, os.path.relpath(files[-1], REPO)) if tot else (None, None, None)
     fam = d.get("per_step_bytes", {}).get(family)
     if not fam:
         return None, None, None
@@ -167,6 +172,7 @@ def mmimdb_bench(args) -> None:
     fps = mmimdb_flops_per_sample()
     tf = fps * value / 1e12
     nparam = sum(p.numel() for p in model.parameters())
+    traffic, _, traffic_src = pmc_traffic("step", "mmimdb") if B == 256 else (None, None, None)
     res = {"metric": "samples/sec MMIMDb image+text late-fusion (GMU) train step, 1 MI355X (BASELINE.json configs[3])",
            "value": round(value, 2), "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
@@ -177,7 +183,9 @@ def mmimdb_bench(args) -> None:
                       "per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}", "params": nparam},
            "roofline": {"bound": "mfma", "kernel": "whole step (k_gemm_small MFMA products dominate the FLOPs)",
                         "achieved": round(tf, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                        "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                        "traffic_unit": "HBM bytes per step, all kernels (PMC: 2 x FETCH_SIZE + WRITE_SIZE; batch 256)",
+                        "traffic_source": traffic_src,
                         "flop_per_sample": fps, "adam_bytes_per_step": 28 * nparam},
            "final_loss": round(st.eng.loss.item(), 5)}
     if not args.no_cpu_baseline and rank == 0:

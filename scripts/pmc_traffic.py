@@ -17,9 +17,10 @@ import sys
 from collections import defaultdict
 
 FAMILIES = [("conv", ("k_fwd_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k_conv_")),
-            ("bn", ("k_bn_",)), ("pool", ("k_maxpool", "k_avgpool")), ("adam", ("k_adam",)),
-            ("gather", ("k_avmnist_gather",)), ("head", ("k_gemm_small", "k_cross_entropy", "k_act_bwd",
-                                                         "k_dropout"))]
+            ("bn", ("k_bn_", "k_bn1d")), ("pool", ("k_maxpool", "k_avgpool")), ("adam", ("k_adam",)),
+            ("gather", ("k_avmnist_gather",)), ("head", ("k_gemm_small", "k_gemm_pair", "k_splitk_reduce",
+                                                         "k_cross_entropy", "k_act_bwd", "k_dropout")),
+            ("mmimdb_ew", ("k_gmu", "k_maxout", "k_bce"))]  # "head" = every small-GEMM (Linear) launch
 
 
 def family(name: str) -> str:
@@ -68,8 +69,9 @@ def main(fetch_dir: str, write_dir: str) -> None:
     rd = per_step(load(fetch_dir, "FETCH_SIZE"), 2.0)
     wr = per_step(load(write_dir, "WRITE_SIZE"), 1.0)
     fams = sorted({f for s, _ in rd + wr for f in s})
+    bench_args = sys.argv[3] if len(sys.argv) > 3 else "--steps 3 --warmup 2 --no-cpu-baseline"
     out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                     "`bench.py --steps 3 --warmup 2 --no-cpu-baseline`; read bytes = 2 x FETCH_SIZE "
+                     f"`bench.py {bench_args}`; read bytes = 2 x FETCH_SIZE "
                      "(gfx950 wide-read correction), write bytes = WRITE_SIZE; per step = dispatches "
                      "between consecutive k_adam launches; median over complete steps",
            "steps_read_pass": len(rd), "steps_write_pass": len(wr), "per_step_bytes": {}}
