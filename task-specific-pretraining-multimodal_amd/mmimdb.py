@@ -21,6 +21,7 @@ rejected), MaxOut with 2 units and no bias, Dropout 0.5, biasless GMU.
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional
 
 import torch
@@ -35,7 +36,7 @@ _BN_MOMENTUM_DEFAULT = 0.1
 # TSPM_MMIMDB_FUSE=1: BatchNorm1d backward + MaxOut backward in one launch (tspm_bn1d_bwd_maxout, bitwise
 # equal).  Off by default: measured 618k vs 653k samples/s at batch 256 — the BN kernel's 8 workgroups
 # (64 channels each) take on the routing that the wide element-wise kernel spreads over the chip.
-_FUSE_BN_MAXOUT = __import__("os").environ.get("TSPM_MMIMDB_FUSE", "0") == "1"
+_FUSE_BN_MAXOUT = os.environ.get("TSPM_MMIMDB_FUSE", "0") == "1"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -165,14 +166,12 @@ class MMIMDbEngine:
         # their gradients), joined by events before the gate / at the end of the backward.  Measured
         # (graph replay): 0.4385 vs 0.4278 ms at batch 256, 0.373 vs 0.365 at 128, 0.859 vs 0.876 at
         # 1024 — the two stream edges cost about what the overlap saves, so one stream is the default.
-        import os
         self.side = torch.cuda.Stream(device) if os.environ.get("TSPM_MMIMDB_STREAMS", "1") == "2" else None
         self.keep = torch.ones(2, n, h, dtype=torch.uint8, device=device)
         widths = (self.di, self.dt, d, h)
         self.stat = {k: (z(w), z(w)) for k, w in zip(("i", "t", "b0", "b1", "b2"), widths + (h,))}
         self.stats = z(3 + 3 * c)
         # split-K for the long encoder Linear when its output tiles cannot fill the chip
-        import os
         self.enc_splits = int(os.environ.get("TSPM_MMIMDB_SPLITK", "4"))
         tiles = -(-n // 32) * -(-e // 32)
         if self.di < 2048 or tiles >= 256:
