@@ -250,6 +250,11 @@ int tspm_linear_fwd_splitk(int32_t n, int32_t in, int32_t out, const float* x, i
                            int32_t ldy, int32_t splits, void* workspace, size_t workspace_bytes,
                            tspm_stream_t stream);
 size_t tspm_linear_fwd_splitk_workspace(int32_t n, int32_t in, int32_t out, int32_t splits);
+/* Two bias-free Linear forwards of the same shape in one launch (the GMU's fc_one / fc_two,
+ * models/gates/gated_bimodal.py; ABI 11): y0 = x0 @ w0^T, y1 = x1 @ w1^T, bitwise tspm_linear_fwd. */
+int tspm_linear_fwd_pair(int32_t n, int32_t in, int32_t out, const float* x0, int32_t ldx0, const float* w0,
+                         float* y0, int32_t ldy0, const float* x1, int32_t ldx1, const float* w1, float* y1,
+                         int32_t ldy1, tspm_stream_t stream);
 /* dx = dy @ w  (dx overwritten). */
 int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, int32_t ldy, const float* w,
                          float* dx, int32_t ldx, tspm_stream_t stream);
@@ -385,6 +390,17 @@ int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const fl
 int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
                          const float* invstd, const float* gamma, float* dgamma, float* dbeta, const float* a,
                          const uint8_t* keep, float keep_scale, float* da, tspm_stream_t stream);
+/* Two independent BatchNorm1d layers over the same m rows in one launch (the MMIMDb image and text
+ * encoders' input BNs; ABI 11): each half exactly as tspm_bn1d_fwd / tspm_bn1d_bwd (bitwise). */
+int tspm_bn1d_fwd_pair(int32_t m, int32_t c0, const float* x0, const float* gamma0, const float* beta0,
+                       float* running_mean0, float* running_var0, float momentum0, float eps0, float* save_mean0,
+                       float* save_invstd0, float* y0, int32_t c1, const float* x1, const float* gamma1,
+                       const float* beta1, float* running_mean1, float* running_var1, float momentum1, float eps1,
+                       float* save_mean1, float* save_invstd1, float* y1, tspm_stream_t stream);
+int tspm_bn1d_bwd_pair(int32_t m, int32_t c0, const float* g0, const float* x0, const float* mean0,
+                       const float* invstd0, const float* gamma0, float* dgamma0, float* dbeta0, float* dx0,
+                       int32_t c1, const float* g1, const float* x1, const float* mean1, const float* invstd1,
+                       const float* gamma1, float* dgamma1, float* dbeta1, float* dx1, tspm_stream_t stream);
 /* BCEWithLogitsLoss (mean) — LossFunctionGroup{bce_with_logits: w} (experiment_utils/loss.py:52,
  * configs/mmimdb/centralised/mmimdb_baseline.yaml): loss[0] = grad_scale * mean((1-t)*x - logsigmoid(x)),
  * dlogits = (sigmoid(x) - t) * grad_scale / (n*classes) (nullable).  If stats != NULL (3 + 3*classes

@@ -119,6 +119,10 @@ _SIGS = {
     "tspm_bn1d_fwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P]),
     "tspm_bn1d_bwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tspm_bn1d_bwd_maxout": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, c_float, _P, _P]),
+    "tspm_bn1d_fwd_pair": (c_int32, [c_int32] + ([c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P] * 2)
+                           + [_P]),
+    "tspm_bn1d_bwd_pair": (c_int32, [c_int32] + ([c_int32] + [_P] * 8) * 2 + [_P]),
+    "tspm_linear_fwd_pair": (c_int32, [c_int32, c_int32, c_int32] + [_P, c_int32, _P, _P, c_int32] * 2 + [_P]),
     "tspm_bce_logits": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, c_float, _P, _P]),
 }
 

@@ -493,6 +493,28 @@ extern "C" int tspm_linear_bwd(int32_t n, int32_t in, int32_t out, const float* 
   return TSPM_OK;
 }
 
+extern "C" int tspm_linear_fwd_pair(int32_t n, int32_t in, int32_t out, const float* x0, int32_t ldx0, const float* w0,
+                                    float* y0, int32_t ldy0, const float* x1, int32_t ldx1, const float* w1, float* y1,
+                                    int32_t ldy1, tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx0 < in || ldy0 < out || ldx1 < in || ldy1 < out || !x0 || !w0 || !y0 ||
+      !x1 || !w1 || !y1)
+    return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  GemmArgs a{n, out, in, x0, ldx0, 1, w0, 1, in, y0, ldy0, nullptr, 0, nullptr, 1.f, nullptr};
+  GemmArgs b{n, out, in, x1, ldx1, 1, w1, 1, in, y1, ldy1, nullptr, 0, nullptr, 1.f, nullptr};
+  const int wa = gemm_wk(a), wb = gemm_wk(b);
+  const int wk = wa > wb ? wa : wb;
+  const int ta = cdiv(a.M, 32) * cdiv(a.N, 32), tb = cdiv(b.M, 32) * cdiv(b.N, 32);
+  const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  switch (wk) {
+    case 1: hipLaunchKernelGGL(k_gemm_pair<1>, dim3(ta + tb), dim3(64), lds, st, a, b, ta); break;
+    case 2: hipLaunchKernelGGL(k_gemm_pair<2>, dim3(ta + tb), dim3(128), lds, st, a, b, ta); break;
+    default: hipLaunchKernelGGL(k_gemm_pair<4>, dim3(ta + tb), dim3(256), lds, st, a, b, ta); break;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
 extern "C" int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,
                             tspm_stream_t stream) {
   if (n <= 0 || cols <= 0 || ldg < cols || ldy < cols || !g || !y) return TSPM_ERR_INVALID;

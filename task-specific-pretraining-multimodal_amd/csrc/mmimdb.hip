@@ -196,14 +196,43 @@ TSPM_DEV float bn_group_sum(float v, float* red) {
   return t;
 }
 
-__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, int c, const float* __restrict__ x,
-                                                                const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta,
-                                                                float* __restrict__ rmean, float* __restrict__ rvar,
-                                                                float momentum, float eps, float* __restrict__ smean,
-                                                                float* __restrict__ sinvstd, float* __restrict__ y) {
+struct Bn1dFwd {
+  int c;
+  const float* x;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  float momentum, eps;
+  float* smean;
+  float* sinvstd;
+  float* y;
+};
+
+TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, float* red);
+
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, Bn1dFwd p) {
   __shared__ float red[kBnCh * kBnGroups];
-  const int ch = blockIdx.x * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
+  bn1d_fwd_body(m, p, blockIdx.x, red);
+}
+
+// Two independent BatchNorm1d layers over the same rows (the MMIMDb image and text encoders' input
+// BNs) in one launch: blocks [0, nb0) take p0.
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd2(int m, Bn1dFwd p0, Bn1dFwd p1, int nb0) {
+  __shared__ float red[kBnCh * kBnGroups];
+  if ((int)blockIdx.x < nb0)
+    bn1d_fwd_body(m, p0, blockIdx.x, red);
+  else
+    bn1d_fwd_body(m, p1, blockIdx.x - nb0, red);
+}
+
+TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, float* red) {
+  const int c = p.c;
+  const float* __restrict__ x = p.x;
+  const float momentum = p.momentum, eps = p.eps;
+  float* __restrict__ rmean = p.rmean;
+  float* __restrict__ rvar = p.rvar;
+  const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
   float s = 0.f;
   if (ok)
@@ -222,29 +251,64 @@ __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, int c, co
   const float invstd = 1.f / sqrtf(var + eps);
   if (!ok) return;
   if (grp == 0) {
-    smean[ch] = mean;
-    sinvstd[ch] = invstd;
+    p.smean[ch] = mean;
+    p.sinvstd[ch] = invstd;
     if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mean;
     if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (m > 1 ? m2 / (float)(m - 1) : m2);
   }
-  const float ga = gamma[ch], be = beta[ch];
+  const float ga = p.gamma[ch], be = p.beta[ch];
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
-    y[i] = (x[i] - mean) * invstd * ga + be;
+    p.y[i] = (x[i] - mean) * invstd * ga + be;
   }
 }
 
-__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, int c, const float* __restrict__ g,
-                                                                const float* __restrict__ x,
-                                                                const float* __restrict__ mean_,
-                                                                const float* __restrict__ invstd_,
-                                                                const float* __restrict__ gamma,
-                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                float* __restrict__ dx, const float* __restrict__ mo_a,
-                                                                const uint8_t* __restrict__ mo_keep, float mo_scale,
-                                                                float* __restrict__ mo_da) {
+struct Bn1dBwd {
+  int c;
+  const float* g;
+  const float* x;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* dx;
+  const float* mo_a;       // optional fused MaxOut/Dropout backward (tspm_bn1d_bwd_maxout)
+  const uint8_t* mo_keep;
+  float mo_scale;
+  float* mo_da;
+};
+
+TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, float* red);
+
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, Bn1dBwd p) {
   __shared__ float red[kBnCh * kBnGroups];
-  const int ch = blockIdx.x * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
+  bn1d_bwd_body(m, p, blockIdx.x, red);
+}
+
+__global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd2(int m, Bn1dBwd p0, Bn1dBwd p1, int nb0) {
+  __shared__ float red[kBnCh * kBnGroups];
+  if ((int)blockIdx.x < nb0)
+    bn1d_bwd_body(m, p0, blockIdx.x, red);
+  else
+    bn1d_bwd_body(m, p1, blockIdx.x - nb0, red);
+}
+
+TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, float* red) {
+  const int c = p.c;
+  const float* __restrict__ g = p.g;
+  const float* __restrict__ x = p.x;
+  const float* __restrict__ mean_ = p.mean;
+  const float* __restrict__ invstd_ = p.invstd;
+  const float* __restrict__ gamma = p.gamma;
+  float* __restrict__ dgamma = p.dgamma;
+  float* __restrict__ dbeta = p.dbeta;
+  float* __restrict__ dx = p.dx;
+  const float* __restrict__ mo_a = p.mo_a;
+  const uint8_t* __restrict__ mo_keep = p.mo_keep;
+  const float mo_scale = p.mo_scale;
+  float* __restrict__ mo_da = p.mo_da;
+  const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
   const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
   float sg = 0.f, sgx = 0.f;
@@ -339,8 +403,9 @@ extern "C" int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* 
                              float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
                              float* save_invstd, float* y, tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !x || !gamma || !beta || !save_mean || !save_invstd || !y) return TSPM_ERR_INVALID;
+  const Bn1dFwd p{c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y};
   hipLaunchKernelGGL(k_bn1d_fwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
-                     m, c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y);
+                     m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }
@@ -349,8 +414,9 @@ extern "C" int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* 
                              const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
                              tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
+  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr};
   hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
-                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr);
+                     m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }
@@ -361,8 +427,44 @@ extern "C" int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const 
                                     tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta || !a || !da)
     return TSPM_ERR_INVALID;
+  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da};
   hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
-                     m, c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da);
+                     m, p);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_fwd_pair(int32_t m, int32_t c0, const float* x0, const float* gamma0, const float* beta0,
+                                  float* running_mean0, float* running_var0, float momentum0, float eps0,
+                                  float* save_mean0, float* save_invstd0, float* y0, int32_t c1, const float* x1,
+                                  const float* gamma1, const float* beta1, float* running_mean1, float* running_var1,
+                                  float momentum1, float eps1, float* save_mean1, float* save_invstd1, float* y1,
+                                  tspm_stream_t stream) {
+  if (m <= 0 || c0 <= 0 || c1 <= 0 || !x0 || !gamma0 || !beta0 || !save_mean0 || !save_invstd0 || !y0 || !x1 ||
+      !gamma1 || !beta1 || !save_mean1 || !save_invstd1 || !y1)
+    return TSPM_ERR_INVALID;
+  const Bn1dFwd p0{c0, x0, gamma0, beta0, running_mean0, running_var0, momentum0, eps0, save_mean0, save_invstd0, y0};
+  const Bn1dFwd p1{c1, x1, gamma1, beta1, running_mean1, running_var1, momentum1, eps1, save_mean1, save_invstd1, y1};
+  const int nb0 = cdiv(c0, kBnCh);
+  hipLaunchKernelGGL(k_bn1d_fwd2, dim3(nb0 + cdiv(c1, kBnCh)), dim3(kBnCh * kBnGroups), 0,
+                     static_cast<hipStream_t>(stream), m, p0, p1, nb0);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_bwd_pair(int32_t m, int32_t c0, const float* g0, const float* x0, const float* mean0,
+                                  const float* invstd0, const float* gamma0, float* dgamma0, float* dbeta0, float* dx0,
+                                  int32_t c1, const float* g1, const float* x1, const float* mean1,
+                                  const float* invstd1, const float* gamma1, float* dgamma1, float* dbeta1, float* dx1,
+                                  tspm_stream_t stream) {
+  if (m <= 0 || c0 <= 0 || c1 <= 0 || !g0 || !x0 || !mean0 || !invstd0 || !gamma0 || !dgamma0 || !dbeta0 || !g1 ||
+      !x1 || !mean1 || !invstd1 || !gamma1 || !dgamma1 || !dbeta1)
+    return TSPM_ERR_INVALID;
+  const Bn1dBwd p0{c0, g0, x0, mean0, invstd0, gamma0, dgamma0, dbeta0, dx0, nullptr, nullptr, 1.f, nullptr};
+  const Bn1dBwd p1{c1, g1, x1, mean1, invstd1, gamma1, dgamma1, dbeta1, dx1, nullptr, nullptr, 1.f, nullptr};
+  const int nb0 = cdiv(c0, kBnCh);
+  hipLaunchKernelGGL(k_bn1d_bwd2, dim3(nb0 + cdiv(c1, kBnCh)), dim3(kBnCh * kBnGroups), 0,
+                     static_cast<hipStream_t>(stream), m, p0, p1, nb0);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

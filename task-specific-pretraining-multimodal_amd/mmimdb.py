@@ -37,6 +37,9 @@ _BN_MOMENTUM_DEFAULT = 0.1
 # equal).  Off by default: measured 618k vs 653k samples/s at batch 256 — the BN kernel's 8 workgroups
 # (64 channels each) take on the routing that the wide element-wise kernel spreads over the chip.
 _FUSE_BN_MAXOUT = os.environ.get("TSPM_MMIMDB_FUSE", "0") == "1"
+# TSPM_MMIMDB_PAIRS=0: the independent image / text launches (input BatchNorm1d forward and backward, the
+# GMU projections) as separate launches instead of merged pairs (A/B; bitwise equal)
+_PAIRS = os.environ.get("TSPM_MMIMDB_PAIRS", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -217,6 +220,15 @@ class MMIMDbEngine:
                                       rv.data_ptr(), mom, eps, mean.data_ptr(), inv.data_ptr(), out.data_ptr(), sh),
                 "bn1d_fwd")
 
+    def _bn_train_pair(self, a, b, sh):
+        args = []
+        for key, bn, x, width, out in (a, b):
+            g, bb, rm, rv, eps, mom = _bn(bn)
+            mean, inv = self.stat[key]
+            args += [width, x.data_ptr(), g.data_ptr(), bb.data_ptr(), rm.data_ptr(), rv.data_ptr(), mom, eps,
+                     mean.data_ptr(), inv.data_ptr(), out.data_ptr()]
+        L.check(L.lib().tspm_bn1d_fwd_pair(self.n, *args, sh), "bn1d_fwd_pair")
+
     def _bn_eval(self, bn, x, width, out, sh):
         g, b, rm, rv, eps, _ = _bn(bn)
         L.check(L.lib().tspm_bn_apply_eval(self.n, width, x.data_ptr(), rm.data_ptr(), rv.data_ptr(), eps, g.data_ptr(),
@@ -253,19 +265,37 @@ class MMIMDbEngine:
         bn = lambda k, mod, x, w, o: bn_s(k, mod, x, w, o, sh)
         # encoders: BatchNorm1d → Linear (models/mmimdb.py:78-93), then the GMU projections into
         # U = [fc_one | fc_two]; the text branch runs on the side stream (joined before the gate)
-        st = self._fork()
-        bn_s("t", te[0], self.T, self.dt, self.XnT, st)
-        L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
-                                    te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, st), "text fc")
-        L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, gmu.fc_two.weight.data_ptr(), None, 0, None, 1.0,
-                                    self.U.data_ptr() + d * 4, 2 * d, st), "gmu fc_two")
-        bn("i", ie[0], self.I, self.di, self.XnI)
-        L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
-                                           ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e, self.enc_splits,
-                                           self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
-        L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(), None, 0, None, 1.0,
-                                    self.U.data_ptr(), 2 * d, sh), "gmu fc_one")
-        self._join()
+        pairs = _PAIRS and self.side is None
+        if pairs:  # one stream, independent pairs of launches merged (bitwise the separate launches)
+            if train:
+                self._bn_train_pair(("t", te[0], self.T, self.dt, self.XnT), ("i", ie[0], self.I, self.di, self.XnI),
+                                    sh)
+            else:
+                bn("t", te[0], self.T, self.dt, self.XnT)
+                bn("i", ie[0], self.I, self.di, self.XnI)
+            L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
+                                        te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, sh), "text fc")
+            L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
+                                               ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e,
+                                               self.enc_splits, self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
+            L.check(lib.tspm_linear_fwd_pair(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(),
+                                             self.U.data_ptr(), 2 * d, self.ET.data_ptr(), e,
+                                             gmu.fc_two.weight.data_ptr(), self.U.data_ptr() + d * 4, 2 * d, sh),
+                    "gmu fc_one/fc_two")
+        else:
+            st = self._fork()
+            bn_s("t", te[0], self.T, self.dt, self.XnT, st)
+            L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
+                                        te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, st), "text fc")
+            L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, gmu.fc_two.weight.data_ptr(), None, 0, None,
+                                        1.0, self.U.data_ptr() + d * 4, 2 * d, st), "gmu fc_two")
+            bn("i", ie[0], self.I, self.di, self.XnI)
+            L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
+                                               ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e,
+                                               self.enc_splits, self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
+            L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(), None, 0, None,
+                                        1.0, self.U.data_ptr(), 2 * d, sh), "gmu fc_one")
+            self._join()
         L.check(lib.tspm_gmu_fwd(n, d, self.U.data_ptr(), 2 * d, gmu.hidden_sigmoid.weight.data_ptr(),
                                  self.H.data_ptr(), 2 * d, self.gate.data_ptr(), self.Z.data_ptr(), d, sh), "gmu")
         # classifier (models/mmimdb.py:38-47)
@@ -342,8 +372,17 @@ class MMIMDbEngine:
             # encoder (the BatchNorm1d input-feature gradient is skipped: nothing consumes it)
             linear_bwd(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, enc[1].weight.data_ptr(), g(enc[1].weight),
                        g(enc[1].bias), dXn.data_ptr(), w, q)
-            self._bn_bwd(key, enc[0], dXn, X, w, None, q)
+            if not (_PAIRS and self.side is None):
+                self._bn_bwd(key, enc[0], dXn, X, w, None, q)
         self._join()
+        if _PAIRS and self.side is None:  # both input BatchNorm1d backwards in one launch
+            bt, bi = te[0], ie[0]
+            (mt, it), (mi, ii) = self.stat["t"], self.stat["i"]
+            L.check(lib.tspm_bn1d_bwd_pair(n, self.dt, self.dXnT.data_ptr(), self.T.data_ptr(), mt.data_ptr(),
+                                           it.data_ptr(), bt.weight.data_ptr(), g(bt.weight), g(bt.bias), None,
+                                           self.di, self.dXn.data_ptr(), self.I.data_ptr(), mi.data_ptr(),
+                                           ii.data_ptr(), bi.weight.data_ptr(), g(bi.weight), g(bi.bias), None, sh),
+                    "bn1d_bwd_pair")
 
 
 # ------------------------------------------------------------------------------------------------

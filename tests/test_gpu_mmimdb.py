@@ -405,3 +405,22 @@ def test_fused_bn_maxout_backward_equals_separate(gpu, monkeypatch):
         torch.cuda.synchronize()
         res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
     assert torch.equal(res[0], res[1])
+
+
+def test_paired_launches_equal_separate(gpu, monkeypatch):
+    """Merged image/text launch pairs (tspm_bn1d_fwd_pair / _bwd_pair, tspm_linear_fwd_pair) give bitwise
+    the step of the separate launches."""
+    n, res = 64, []
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=15))
+    for pairs in (True, False):
+        monkeypatch.setattr(M, "_PAIRS", pairs)
+        ours, _, st, _, _ = _setup(gpu, n)
+        for s in range(3):
+            st.keep_override = _keep(n, 90 + s).to(gpu)
+            st.step(I, T, y)
+        torch.cuda.synchronize()
+        ours.eval()
+        ev = ours(I, T)
+        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]
+                             + [ev.reshape(-1).cpu()]))
+    assert torch.equal(res[0], res[1])
