@@ -266,6 +266,19 @@ int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, i
  * tspm_linear_bwd_weight + tspm_linear_bwd_data (same per-product reduction split). */
 int tspm_linear_bwd(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy, int32_t ldy,
                     const float* w, float* dw, float* db, float* dx, int32_t lddx, tspm_stream_t stream);
+/* Backward of up to 2 independent nn.Linear layers in ONE launch (ABI 11; e.g. the GMU's fc_one and
+ * fc_two, or the MMIMDb image and text encoder Linears): each descriptor as tspm_linear_bwd (dx
+ * nullable), bitwise its results.  descs is a host array read at launch time. */
+typedef struct tspm_linear_bwd_desc {
+  int32_t n, in, out, ldx, ldy, lddx;
+  const float* x;
+  const float* dy;
+  const float* w;
+  float* dw;
+  float* db;
+  float* dx;
+} tspm_linear_bwd_desc;
+int tspm_linear_bwd_multi(int32_t count, const tspm_linear_bwd_desc* descs, tspm_stream_t stream);
 /* In-place gradient masking through a ReLU(+dropout) output y: g = (y > 0) ? g * scale : 0
  * (scale = 1/(1-p) when y is the post-dropout output — y > 0 implies the unit was kept). */
 int tspm_act_bwd(int32_t n, int32_t cols, float* g, int32_t ldg, const float* y, int32_t ldy, float scale,

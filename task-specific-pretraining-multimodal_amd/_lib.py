@@ -58,6 +58,12 @@ class AdamHyper(Structure):
 HYPER_STEP_OFFSET = 48  # byte offset of tspm_adam_hyper.step
 
 
+class LinearBwdDesc(Structure):
+    """tspm_linear_bwd_desc: one Linear's backward for tspm_linear_bwd_multi."""
+    _fields_ = [(n, c_int32) for n in ("n", "in_", "out", "ldx", "ldy", "lddx")] + \
+               [(n, c_void_p) for n in ("x", "dy", "w", "dw", "db", "dx")]
+
+
 # name -> (restype, argtypes)
 _P = c_void_p
 _SIGS = {
@@ -99,6 +105,7 @@ _SIGS = {
                                          c_int32, c_int32, _P, c_size_t, _P]),
     "tspm_linear_fwd_splitk_workspace": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
     "tspm_linear_bwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, _P, c_int32, _P]),
+    "tspm_linear_bwd_multi": (c_int32, [c_int32, POINTER(LinearBwdDesc), _P]),
     "tspm_linear_bwd_data": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P]),
     "tspm_linear_bwd_weight": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P]),
     "tspm_act_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, c_float, _P]),

@@ -452,6 +452,22 @@ extern "C" int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const 
   return gemm_small(g, static_cast<hipStream_t>(stream));
 }
 
+// Up to 4 independent products in one launch: blocks are dealt out to the problems in order.
+struct GemmMulti {
+  GemmArgs p[4];
+  int start[5];  // start[i] = first block of problem i, start[count] = total
+  int count;
+};
+
+template <int WK>
+__global__ __launch_bounds__(64 * WK) void k_gemm_multi(GemmMulti mp) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < mp.count && b >= mp.start[i + 1]) ++i;  // workgroup-uniform
+  gemm_body<WK>(mp.p[i], b - mp.start[i], lds);
+}
+
 // K-contiguity / vector decision and wave count of gemm_small, for a pair launch (no split, no quad).
 int gemm_wk(GemmArgs& g) {
   auto rows16 = [](const float* p, long long ld) {
@@ -510,6 +526,40 @@ extern "C" int tspm_linear_fwd_pair(int32_t n, int32_t in, int32_t out, const fl
     case 1: hipLaunchKernelGGL(k_gemm_pair<1>, dim3(ta + tb), dim3(64), lds, st, a, b, ta); break;
     case 2: hipLaunchKernelGGL(k_gemm_pair<2>, dim3(ta + tb), dim3(128), lds, st, a, b, ta); break;
     default: hipLaunchKernelGGL(k_gemm_pair<4>, dim3(ta + tb), dim3(256), lds, st, a, b, ta); break;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_linear_bwd_multi(int32_t count, const tspm_linear_bwd_desc* descs, tspm_stream_t stream) {
+  if (count < 1 || count > 2 || !descs) return TSPM_ERR_INVALID;
+  GemmMulti mp{};
+  int np = 0, wk = 1;
+  for (int i = 0; i < count; ++i) {
+    const tspm_linear_bwd_desc& d = descs[i];
+    if (d.n <= 0 || d.in <= 0 || d.out <= 0 || d.ldx < d.in || d.ldy < d.out || !d.x || !d.dy || !d.dw)
+      return TSPM_ERR_INVALID;
+    if (d.dx && (!d.w || d.lddx < d.in)) return TSPM_ERR_INVALID;
+    mp.p[np++] = GemmArgs{d.out, d.in, d.n, d.dy, 1, d.ldy, d.x, d.ldx, 1, d.dw, d.in, nullptr, 0, nullptr, 1.f, d.db};
+    if (d.dx)
+      mp.p[np++] = GemmArgs{d.n, d.in, d.out, d.dy, d.ldy, 1, d.w, d.in, 1, d.dx, d.lddx, nullptr, 0, nullptr, 1.f,
+                            nullptr};
+  }
+  int total = 0;
+  for (int i = 0; i < np; ++i) {
+    const int w = gemm_wk(mp.p[i]);
+    wk = w > wk ? w : wk;
+    mp.start[i] = total;
+    total += cdiv(mp.p[i].M, 32) * cdiv(mp.p[i].N, 32);
+  }
+  mp.start[np] = total;
+  mp.count = np;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t lds = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  switch (wk) {
+    case 1: hipLaunchKernelGGL(k_gemm_multi<1>, dim3(total), dim3(64), lds, st, mp); break;
+    case 2: hipLaunchKernelGGL(k_gemm_multi<2>, dim3(total), dim3(128), lds, st, mp); break;
+    default: hipLaunchKernelGGL(k_gemm_multi<4>, dim3(total), dim3(256), lds, st, mp); break;
   }
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;

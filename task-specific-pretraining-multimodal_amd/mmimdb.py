@@ -220,6 +220,18 @@ class MMIMDbEngine:
                                       rv.data_ptr(), mom, eps, mean.data_ptr(), inv.data_ptr(), out.data_ptr(), sh),
                 "bn1d_fwd")
 
+    @staticmethod
+    def _linear_bwd_multi(items, sh) -> None:
+        """items: (n, in, out, x, ldx, dy_ptr, ldy, weight, bias, dx, lddx) per Linear — one
+        tspm_linear_bwd_multi launch (bitwise the separate tspm_linear_bwd launches)."""
+        descs = (L.LinearBwdDesc * len(items))()
+        for dsc, (n, fin, fout, x, ldx, dy, ldy, w, b, dx, lddx) in zip(descs, items):
+            dsc.n, dsc.in_, dsc.out, dsc.ldx, dsc.ldy, dsc.lddx = n, fin, fout, ldx, ldy, lddx
+            dsc.x, dsc.dy, dsc.w = x.data_ptr(), dy, w.data_ptr()
+            dsc.dw, dsc.db = w.grad.data_ptr(), (b.grad.data_ptr() if b is not None else None)
+            dsc.dx = dx.data_ptr() if dx is not None else None
+        L.check(L.lib().tspm_linear_bwd_multi(len(items), descs, sh), "linear_bwd_multi")
+
     def _bn_train_pair(self, a, b, sh):
         args = []
         for key, bn, x, width, out in (a, b):
@@ -363,6 +375,22 @@ class MMIMDbEngine:
         L.check(lib.tspm_linear_bwd_weight(n, 2 * d, 1, self.H.data_ptr(), 2 * d, self.ds.data_ptr(), 1,
                                            g(gmu.hidden_sigmoid.weight), None, sh), "gmu gate dW")
         dU1, dU2 = self.dU.data_ptr(), self.dU.data_ptr() + d * 4
+        if _PAIRS and self.side is None:
+            # fc_two + fc_one backward in one launch, then both encoder Linears, then both input BNs
+            self._linear_bwd_multi([(n, e, d, self.ET, e, dU2, 2 * d, gmu.fc_two.weight, None, self.dET, e),
+                                    (n, e, d, self.EI, e, dU1, 2 * d, gmu.fc_one.weight, None, self.dEI, e)], sh)
+            self._linear_bwd_multi([(n, self.dt, e, self.XnT, self.dt, self.dET.data_ptr(), e, te[1].weight,
+                                     te[1].bias, self.dXnT, self.dt),
+                                    (n, self.di, e, self.XnI, self.di, self.dEI.data_ptr(), e, ie[1].weight,
+                                     ie[1].bias, self.dXn, self.di)], sh)
+            bt, bi = te[0], ie[0]
+            (mt, it), (mi, ii) = self.stat["t"], self.stat["i"]
+            L.check(lib.tspm_bn1d_bwd_pair(n, self.dt, self.dXnT.data_ptr(), self.T.data_ptr(), mt.data_ptr(),
+                                           it.data_ptr(), bt.weight.data_ptr(), g(bt.weight), g(bt.bias), None,
+                                           self.di, self.dXn.data_ptr(), self.I.data_ptr(), mi.data_ptr(),
+                                           ii.data_ptr(), bi.weight.data_ptr(), g(bi.weight), g(bi.bias), None, sh),
+                    "bn1d_bwd_pair")
+            return
         st = self._fork()  # text branch (fc_two, text encoder) on the side stream
         for (dUp, fc, E, dE, key, enc, Xn, X, w, dXn, q) in (
                 (dU2, gmu.fc_two, self.ET, self.dET, "t", te, self.XnT, self.T, self.dt, self.dXnT, st),
@@ -372,17 +400,8 @@ class MMIMDbEngine:
             # encoder (the BatchNorm1d input-feature gradient is skipped: nothing consumes it)
             linear_bwd(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, enc[1].weight.data_ptr(), g(enc[1].weight),
                        g(enc[1].bias), dXn.data_ptr(), w, q)
-            if not (_PAIRS and self.side is None):
-                self._bn_bwd(key, enc[0], dXn, X, w, None, q)
+            self._bn_bwd(key, enc[0], dXn, X, w, None, q)
         self._join()
-        if _PAIRS and self.side is None:  # both input BatchNorm1d backwards in one launch
-            bt, bi = te[0], ie[0]
-            (mt, it), (mi, ii) = self.stat["t"], self.stat["i"]
-            L.check(lib.tspm_bn1d_bwd_pair(n, self.dt, self.dXnT.data_ptr(), self.T.data_ptr(), mt.data_ptr(),
-                                           it.data_ptr(), bt.weight.data_ptr(), g(bt.weight), g(bt.bias), None,
-                                           self.di, self.dXn.data_ptr(), self.I.data_ptr(), mi.data_ptr(),
-                                           ii.data_ptr(), bi.weight.data_ptr(), g(bi.weight), g(bi.bias), None, sh),
-                    "bn1d_bwd_pair")
 
 
 # ------------------------------------------------------------------------------------------------
