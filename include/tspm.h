@@ -383,6 +383,12 @@ int tspm_gmu_bwd(int32_t n, int32_t d, const float* dz, int32_t lddz, const floa
  * y = max(a[:, :d], a[:, d:]) * (keep ? keep_scale : 0)  (keep NULL: no dropout). */
 int tspm_maxout_fwd(int32_t n, int32_t d, const float* a, int32_t lda, const uint8_t* keep, float keep_scale,
                     float* y, int32_t ldy, tspm_stream_t stream);
+/* tspm_maxout_fwd with the dropout mask drawn in-launch (ABI 11): keep[t] = the bit tspm_dropout_mask(
+ * count, p, seed, counter) writes at index index_offset + t (stored for the backward), y as tspm_maxout_fwd
+ * with that mask — one launch instead of mask + MaxOut. */
+int tspm_maxout_fwd_rng(int32_t n, int32_t d, const float* a, int32_t lda, float p, uint64_t seed,
+                        const uint64_t* counter, int64_t index_offset, uint8_t* keep, float keep_scale, float* y,
+                        int32_t ldy, tspm_stream_t stream);
 /* da[n,2d] from dy: the unit holding the max receives the (dropout-masked) gradient; ties split it in
  * half (ATen's derivative of torch.maximum). */
 int tspm_maxout_bwd(int32_t n, int32_t d, const float* dy, int32_t lddy, const float* a, int32_t lda,

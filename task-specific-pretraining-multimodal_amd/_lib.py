@@ -122,6 +122,8 @@ _SIGS = {
     "tspm_gmu_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _P, c_int32, _P]),
     "tspm_gmu_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, c_int32, _P, _P]),
     "tspm_maxout_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
+    "tspm_maxout_fwd_rng": (c_int32, [c_int32, c_int32, _P, c_int32, c_float, c_uint64, _P, c_int64, _P, c_float, _P,
+                                      c_int32, _P]),
     "tspm_maxout_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
     "tspm_bn1d_fwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P]),
     "tspm_bn1d_bwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -26,6 +26,19 @@ TSPM_DEV f32x16 mfma32(float a, float b, f32x16 c) {
 
 TSPM_DEV int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// Counter-based dropout RNG (splitmix64 finaliser over seed / device counter / element index), shared by
+// tspm_dropout_mask and the MMIMDb MaxOut forward that draws its mask in-launch (same keep bits).
+TSPM_DEV uint64_t tspm_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+TSPM_DEV uint64_t tspm_dropout_base(uint64_t seed, uint64_t c) { return tspm_mix64(seed ^ tspm_mix64(c + 0x9e3779b97f4a7c15ULL)); }
+TSPM_DEV bool tspm_dropout_keep(uint64_t base, long long i, float p) {
+  const uint64_t h = tspm_mix64(base + (uint64_t)i * 0x9e3779b97f4a7c15ULL);
+  return (float)(h >> 40) * (1.0f / 16777216.0f) >= p;
+}
+
 TSPM_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 TSPM_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 

@@ -279,22 +279,12 @@ __global__ __launch_bounds__(256) void k_act_bwd(int N, int COLS, float* __restr
   }
 }
 
-// counter-based RNG (splitmix64 finaliser over seed/counter/index)
-TSPM_DEV uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 31);
-}
-
+// counter-based RNG (tspm_dropout_* in common.h)
 __global__ __launch_bounds__(256) void k_dropout_mask(long long count, float p, uint64_t seed,
                                                       const uint64_t* __restrict__ ctr, uint8_t* __restrict__ keep) {
-  const uint64_t c = ctr ? *ctr : 0ULL;
-  const uint64_t base = mix64(seed ^ mix64(c + 0x9e3779b97f4a7c15ULL));
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < count; i += (long long)gridDim.x * 256) {
-    const uint64_t h = mix64(base + (uint64_t)i * 0x9e3779b97f4a7c15ULL);
-    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-    keep[i] = u >= p ? 1 : 0;
-  }
+  const uint64_t base = tspm_dropout_base(seed, ctr ? *ctr : 0ULL);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < count; i += (long long)gridDim.x * 256)
+    keep[i] = tspm_dropout_keep(base, i, p) ? 1 : 0;
 }
 
 // one workgroup; rows strided over threads; deterministic tree reduction in double

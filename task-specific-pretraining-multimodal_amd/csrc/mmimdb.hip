@@ -97,6 +97,25 @@ __global__ __launch_bounds__(256) void k_maxout_fwd(int n, int d, const float* _
   }
 }
 
+// MaxOut forward that draws its dropout mask in-launch (the bits tspm_dropout_mask would write for
+// elements index_offset + t) and stores it for the backward.
+__global__ __launch_bounds__(256) void k_maxout_fwd_rng(int n, int d, const float* __restrict__ a, int lda, float p,
+                                                        uint64_t seed, const uint64_t* __restrict__ ctr,
+                                                        long long index_offset, uint8_t* __restrict__ keep,
+                                                        float scale, float* __restrict__ y, int ldy) {
+  const uint64_t base = tspm_dropout_base(seed, ctr ? *ctr : 0ULL);
+  const long long total = (long long)n * d;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const long long r = t / d;
+    const int j = (int)(t - r * d);
+    const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
+    const bool k = tspm_dropout_keep(base, index_offset + t, p);
+    keep[t] = k ? 1 : 0;
+    const float v = a1 > a0 ? a1 : a0;
+    y[r * ldy + j] = v * (k ? scale : 0.f);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_maxout_bwd(int n, int d, const float* __restrict__ dy, int lddy,
                                                     const float* __restrict__ a, int lda,
                                                     const uint8_t* __restrict__ keep, float scale,
@@ -465,6 +484,18 @@ extern "C" int tspm_bn1d_bwd_pair(int32_t m, int32_t c0, const float* g0, const 
   const int nb0 = cdiv(c0, kBnCh);
   hipLaunchKernelGGL(k_bn1d_bwd2, dim3(nb0 + cdiv(c1, kBnCh)), dim3(kBnCh * kBnGroups), 0,
                      static_cast<hipStream_t>(stream), m, p0, p1, nb0);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_maxout_fwd_rng(int32_t n, int32_t d, const float* a, int32_t lda, float p, uint64_t seed,
+                                   const uint64_t* counter, int64_t index_offset, uint8_t* keep, float keep_scale,
+                                   float* y, int32_t ldy, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || lda < 2 * d || ldy < d || !a || !keep || !y || p < 0.f || p >= 1.f || index_offset < 0)
+    return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_maxout_fwd_rng, dim3(ew_grid((long long)n * d)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     n, d, a, lda, p, (unsigned long long)seed, counter, (long long)index_offset, keep, keep_scale, y,
+                     ldy);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

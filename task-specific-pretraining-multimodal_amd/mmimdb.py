@@ -312,18 +312,28 @@ class MMIMDbEngine:
                                  self.H.data_ptr(), 2 * d, self.gate.data_ptr(), self.Z.data_ptr(), d, sh), "gmu")
         # classifier (models/mmimdb.py:38-47)
         keep, k1, k2, scale = None, None, None, 1.0
+        # in-launch masks: each MaxOut forward draws its half of the mask tspm_dropout_mask would write
+        rng = train and self.p > 0 and self.keep_override is None and _PAIRS
         if train and self.p > 0:
             scale = 1.0 / (1.0 - self.p)
-            if self.keep_override is None:
+            if self.keep_override is None and not rng:
                 L.check(lib.tspm_dropout_mask(2 * n * h, self.p, self.model._rng_seed, self.rng_ctr_ptr,
                                               self.keep.data_ptr(), sh), "dropout_mask")
             k1, k2 = self.keep[0].data_ptr(), self.keep[1].data_ptr()
+
+        def maxout(A, k, Y, unit):
+            if rng:
+                L.check(lib.tspm_maxout_fwd_rng(n, h, A.data_ptr(), 2 * h, self.p, self.model._rng_seed,
+                                                self.rng_ctr_ptr, unit * n * h, k, scale, Y.data_ptr(), h, sh),
+                        "maxout+dropout")
+            else:
+                L.check(lib.tspm_maxout_fwd(n, h, A.data_ptr(), 2 * h, k, scale, Y.data_ptr(), h, sh), "maxout")
         bn("b0", net[0], self.Z, d, self.Zn)
         self._maxout_product(net[1], self.Zn, d, self.A1, sh)
-        L.check(lib.tspm_maxout_fwd(n, h, self.A1.data_ptr(), 2 * h, k1, scale, self.Y1.data_ptr(), h, sh), "maxout1")
+        maxout(self.A1, k1, self.Y1, 0)
         bn("b1", net[3], self.Y1, h, self.Y1n)
         self._maxout_product(net[4], self.Y1n, h, self.A2, sh)
-        L.check(lib.tspm_maxout_fwd(n, h, self.A2.data_ptr(), 2 * h, k2, scale, self.Y2.data_ptr(), h, sh), "maxout2")
+        maxout(self.A2, k2, self.Y2, 1)
         bn("b2", net[6], self.Y2, h, self.Y2n)
         L.check(lib.tspm_linear_fwd(n, h, c, self.Y2n.data_ptr(), h, net[7].weight.data_ptr(), net[7].bias.data_ptr(),
                                     0, None, 1.0, self.logits.data_ptr(), c, sh), "output fc")

@@ -424,3 +424,22 @@ def test_paired_launches_equal_separate(gpu, monkeypatch):
         res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]
                              + [ev.reshape(-1).cpu()]))
     assert torch.equal(res[0], res[1])
+
+
+def test_inlaunch_dropout_masks_equal_mask_kernel(gpu, monkeypatch):
+    """tspm_maxout_fwd_rng draws exactly the keep bits tspm_dropout_mask writes: the step with in-launch
+    masks equals bitwise the step with the separate mask launch (TSPM_MMIMDB_PAIRS=0 path)."""
+    n, res, masks = 64, [], []
+    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=16))
+    for pairs in (True, False):
+        monkeypatch.setattr(M, "_PAIRS", pairs)
+        ours, _, st, _, _ = _setup(gpu, n)
+        ours._rng_seed = 12345
+        for s in range(3):
+            st.step(I, T, y)
+            masks.append(st.eng.keep.clone())
+        torch.cuda.synchronize()
+        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
+    assert torch.equal(res[0], res[1])
+    for a, b in zip(masks[:3], masks[3:]):
+        assert torch.equal(a, b)
