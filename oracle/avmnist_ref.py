@@ -137,9 +137,46 @@ def _bump_tracked(bn: nn.BatchNorm2d, training: bool) -> None:
         bn.num_batches_tracked.add_(1)
 
 
-def block_forward(b: _OracleBlock, x: torch.Tensor, training: bool) -> torch.Tensor:
+class MaskTrace:
+    """Parity instrument (test infrastructure): every ReLU and max-pool of the forward goes through
+    here when a trace is passed.  Record mode keeps each site's input (pre-activation / pooled map)
+    and the pool's argmax; force mode additionally REPLACES the decision -- the ReLU becomes
+    ``x * mask`` and the pool a gather at the given flat indices -- so an fp64 run can follow the
+    exact threshold / argmax decisions an fp32 implementation took (a decision on an element whose
+    value is within rounding of the threshold or of a tie is not a property of the algorithm).
+    Sites: ``{prefix}stem``, ``{prefix}mp``, ``{prefix}blk{i}.a1``, ``{prefix}blk{i}.out`` (block i in
+    forward order), ``head.h1``, ``head.hh``."""
+
+    def __init__(self, force: Optional[Dict[str, torch.Tensor]] = None):
+        self.force = force
+        self.pre: Dict[str, torch.Tensor] = {}
+        self.idx: Dict[str, torch.Tensor] = {}
+
+    def relu(self, site: str, x: torch.Tensor) -> torch.Tensor:
+        self.pre[site] = x.detach()
+        if self.force is None or site not in self.force:
+            return F.relu(x)
+        return x * self.force[site].to(device=x.device, dtype=x.dtype)
+
+    def maxpool(self, site: str, x: torch.Tensor) -> torch.Tensor:
+        out, idx = F.max_pool2d(x, 3, 2, 1, return_indices=True)
+        self.pre[site] = x.detach()
+        self.idx[site] = idx
+        if self.force is None or site not in self.force:
+            return out
+        fi = self.force[site].to(x.device)
+        n, c, p, q = out.shape
+        return x.flatten(2).gather(2, fi.reshape(n, c, p * q)).view(n, c, p, q)
+
+
+def block_forward(b: _OracleBlock, x: torch.Tensor, training: bool, trace: Optional[MaskTrace] = None,
+                  site: str = "") -> torch.Tensor:
+    if trace is None:
+        relu = lambda t, k: F.relu(t)  # noqa: E731
+    else:
+        relu = lambda t, k: trace.relu(site + k, t)  # noqa: E731
     out = F.conv2d(x, b.conv1.weight, None, b.stride, 1)
-    out = F.relu(_bn(out, b.bn1, training)); _bump_tracked(b.bn1, training)
+    out = relu(_bn(out, b.bn1, training), ".a1"); _bump_tracked(b.bn1, training)
     out = F.conv2d(out, b.conv2.weight, None, 1, 1)
     out = _bn(out, b.bn2, training); _bump_tracked(b.bn2, training)
     if b.downsample is not None:
@@ -147,39 +184,46 @@ def block_forward(b: _OracleBlock, x: torch.Tensor, training: bool) -> torch.Ten
         identity = _bn(F.conv2d(x, c.weight, None, c.stride, 0), bn, training); _bump_tracked(bn, training)
     else:
         identity = x
-    return F.relu(out + identity)
+    return relu(out + identity, ".out")
 
 
-def encoder_forward(enc: OracleResNet, x: torch.Tensor, training: bool) -> torch.Tensor:
+def encoder_forward(enc: OracleResNet, x: torch.Tensor, training: bool, trace: Optional[MaskTrace] = None,
+                    prefix: str = "") -> torch.Tensor:
     if x.dim() == 3:  # resnet.py:201-203
         x = x.unsqueeze(1)
     x = F.conv2d(x, enc.conv1.weight, None, 2, 3)
-    x = F.relu(_bn(x, enc.bn1, training)); _bump_tracked(enc.bn1, training)
-    x = F.max_pool2d(x, 3, 2, 1)
+    x = _bn(x, enc.bn1, training)
+    x = F.relu(x) if trace is None else trace.relu(prefix + "stem", x)
+    _bump_tracked(enc.bn1, training)
+    x = F.max_pool2d(x, 3, 2, 1) if trace is None else trace.maxpool(prefix + "mp", x)
+    i = 0
     for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
         for blk in layer:
-            x = block_forward(blk, x, training)
+            x = block_forward(blk, x, training, trace, f"{prefix}blk{i}")
+            i += 1
     x = F.adaptive_avg_pool2d(x, (1, 1)).flatten(1)
     return F.linear(x, enc.fc.weight, enc.fc.bias)
 
 
 def head_forward(model: OracleAVMNIST, fused: torch.Tensor, training: bool,
-                 keep_mask: Optional[torch.Tensor]) -> torch.Tensor:
+                 keep_mask: Optional[torch.Tensor], trace: Optional[MaskTrace] = None) -> torch.Tensor:
     net = model.net
-    h = F.relu(F.linear(fused, net[0].weight, net[0].bias))
+    relu = (lambda t, k: F.relu(t)) if trace is None else (lambda t, k: trace.relu(k, t))  # noqa: E731
+    h = relu(F.linear(fused, net[0].weight, net[0].bias), "head.h1")
     if training and model.dropout_p > 0:
         if keep_mask is None:
             keep_mask = torch.bernoulli(torch.full_like(h, 1.0 - model.dropout_p))
         h = h * (keep_mask.to(h.dtype) / (1.0 - model.dropout_p))
-    h = F.relu(F.linear(h, net[3].weight, net[3].bias))
+    h = relu(F.linear(h, net[3].weight, net[3].bias), "head.hh")
     return F.linear(h, net[5].weight, net[5].bias)
 
 
 def avmnist_forward(model: OracleAVMNIST, audio: torch.Tensor, image: torch.Tensor, training: bool,
-                    keep_mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    ea = encoder_forward(model.audio_encoder, audio, training)
-    ei = encoder_forward(model.image_encoder, image, training)
-    logits = head_forward(model, torch.cat((ea, ei), dim=1), training, keep_mask)
+                    keep_mask: Optional[torch.Tensor] = None,
+                    trace: Optional[MaskTrace] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    ea = encoder_forward(model.audio_encoder, audio, training, trace, "audio.")
+    ei = encoder_forward(model.image_encoder, image, training, trace, "image.")
+    logits = head_forward(model, torch.cat((ea, ei), dim=1), training, keep_mask, trace)
     return logits, ea, ei
 
 
@@ -215,15 +259,18 @@ class OracleAdam:
             p.addcdiv_(m, denom, value=-step_size)
 
 
-def train_step(model: OracleAVMNIST, opt: OracleAdam, audio: torch.Tensor, image: torch.Tensor,
-               labels: torch.Tensor, keep_mask: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
-    """models/avmnist.py:269-310 restated: zero_grad → fwd → CE(mean)·1.0 → backward → Adam."""
+def train_step(model: OracleAVMNIST, opt: Optional[OracleAdam], audio: torch.Tensor, image: torch.Tensor,
+               labels: torch.Tensor, keep_mask: Optional[torch.Tensor] = None,
+               trace: Optional[MaskTrace] = None) -> Dict[str, torch.Tensor]:
+    """models/avmnist.py:269-310 restated: zero_grad → fwd → CE(mean)·1.0 → backward → Adam
+    (``opt=None``: stop before the optimizer step, gradients left in ``.grad``)."""
     for p in model.parameters():
         p.grad = None
-    logits, ea, ei = avmnist_forward(model, audio, image, True, keep_mask)
+    logits, ea, ei = avmnist_forward(model, audio, image, True, keep_mask, trace)
     loss = 0.0 + 1.0 * F.cross_entropy(logits, labels)  # loss.py:131-148 (defaultdict(float) + w·CE)
     loss.backward()
-    opt.step()
+    if opt is not None:
+        opt.step()
     preds = torch.softmax(logits.detach(), 1).argmax(1)
     return {"loss": loss.detach(), "logits": logits.detach(), "emb_audio": ea.detach(), "emb_image": ei.detach(),
             "preds": preds}

@@ -35,11 +35,31 @@ class OracleMaxOut(nn.Module):
         super().__init__()
         self.layers = nn.ModuleList([nn.Linear(i, o, bias=bias) for _ in range(units)])
 
-    def forward(self, x):
+    def forward(self, x, trace: Optional["MaxOutTrace"] = None, site: str = ""):
+        if trace is not None:
+            return trace.maxout(site, self.layers[0](x), self.layers[1](x))
         y = self.layers[0](x)
         for l in self.layers[1:]:
             y = torch.max(y, l(x))
         return y
+
+
+class MaxOutTrace:
+    """Parity instrument (test infrastructure): records both MaxOut units' outputs per site
+    (``mo1``, ``mo2``) and, in force mode, replaces the element-wise choice by a given one
+    (0 = unit 0, 1 = unit 1, 2 = tie: value and gradient split half/half, as torch.max's derivative
+    does for equal inputs) — the fp64 oracle then follows the fp32 implementation's decisions."""
+
+    def __init__(self, force: Optional[Dict[str, torch.Tensor]] = None):
+        self.force = force
+        self.units: Dict[str, tuple] = {}
+
+    def maxout(self, site: str, a0: torch.Tensor, a1: torch.Tensor) -> torch.Tensor:
+        self.units[site] = (a0.detach(), a1.detach())
+        if self.force is None or site not in self.force:
+            return torch.max(a0, a1)
+        c = self.force[site].to(a0.device)
+        return torch.where(c == 1, a1, torch.where(c == 0, a0, 0.5 * (a0 + a1)))
 
 
 class OracleEncoder(nn.Module):
@@ -71,11 +91,11 @@ class OracleClassifier(nn.Module):
         self.net = nn.Sequential(nn.BatchNorm1d(i), OracleMaxOut(i, h), nn.Dropout(0.5), nn.BatchNorm1d(h),
                                  OracleMaxOut(h, h), nn.Dropout(0.5), nn.BatchNorm1d(h), nn.Linear(h, o))
 
-    def forward(self, x, keep1=None, keep2=None):
+    def forward(self, x, keep1=None, keep2=None, trace=None):
         n = self.net
-        x = n[1](n[0](x))
+        x = n[1](n[0](x), trace, "mo1")
         x = _dropout(x, keep1, self.training)
-        x = n[4](n[3](x))
+        x = n[4](n[3](x), trace, "mo2")
         x = _dropout(x, keep2, self.training)
         return n[7](n[6](x))
 
@@ -96,8 +116,8 @@ class OracleMMIMDb(nn.Module):
         self.fusion_module = OracleGMU(embed, embed, embed, embed)
         self.mm_mlp = OracleClassifier(embed, genres, hidden)
 
-    def forward(self, I, T, keep1=None, keep2=None):
-        return self.mm_mlp(self.fusion_module(self.image_model(I), self.text_model(T)), keep1, keep2)
+    def forward(self, I, T, keep1=None, keep2=None, trace=None):
+        return self.mm_mlp(self.fusion_module(self.image_model(I), self.text_model(T)), keep1, keep2, trace)
 
 
 def build_oracle_mmimdb(seed: int = 0, **dims) -> OracleMMIMDb:
@@ -121,15 +141,18 @@ def bce_loss(logits, labels):
     return F.binary_cross_entropy_with_logits(logits, labels)
 
 
-def train_step(model: OracleMMIMDb, opt, image, text, labels, keep1=None, keep2=None) -> Dict[str, torch.Tensor]:
-    """models/mmimdb.py:203-245 (minus the host metric recorder): zero_grad, forward, BCE, backward, Adam."""
+def train_step(model: OracleMMIMDb, opt, image, text, labels, keep1=None, keep2=None,
+               trace: Optional[MaxOutTrace] = None) -> Dict[str, torch.Tensor]:
+    """models/mmimdb.py:203-245 (minus the host metric recorder): zero_grad, forward, BCE, backward, Adam
+    (``opt=None``: gradients only)."""
     model.train()
     for p in model.parameters():
         p.grad = None
-    logits = model(image, text, keep1, keep2)
+    logits = model(image, text, keep1, keep2, trace)
     loss = bce_loss(logits, labels)
     loss.backward()
-    opt.step()
+    if opt is not None:
+        opt.step()
     return {"loss": loss.detach(), "logits": logits.detach()}
 
 

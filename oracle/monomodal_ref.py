@@ -21,7 +21,7 @@ reference by tests/golden/make_golden.py); this module is pinned by tests/golden
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 import torch.nn as nn
@@ -51,20 +51,23 @@ def build_oracle_monomodal(modality: str = "audio", seed: int = 0) -> OracleMono
     return OracleMonomodal(enc, dim, NUM_CLASSES)
 
 
-def forward(model: OracleMonomodal, x: torch.Tensor, training: bool) -> torch.Tensor:
-    e = encoder_forward(model.encoder, x, training)
+def forward(model: OracleMonomodal, x: torch.Tensor, training: bool, trace=None) -> torch.Tensor:
+    """``trace``: an avmnist_ref.MaskTrace (parity instrument; sites prefixed ``enc.``)."""
+    e = encoder_forward(model.encoder, x, training, trace, "enc.")
     if e.dim() > 2:  # train_monomodal.py:83-86
         e = e.reshape(e.shape[0], -1)
     return F.linear(e, model.classifier.weight, model.classifier.bias)
 
 
-def train_step(model: OracleMonomodal, opt: OracleAdam, x: torch.Tensor, labels: torch.Tensor) -> Dict[str, torch.Tensor]:
+def train_step(model: OracleMonomodal, opt: Optional[OracleAdam], x: torch.Tensor, labels: torch.Tensor,
+               trace=None) -> Dict[str, torch.Tensor]:
     for p in model.parameters():
         p.grad = None
-    logits = forward(model, x, True)
+    logits = forward(model, x, True, trace)
     loss = 0.0 + 1.0 * F.cross_entropy(logits, labels)
     loss.backward()
-    opt.step()
+    if opt is not None:
+        opt.step()
     preds = torch.argmax(logits.detach(), dim=1)
     return {"loss": loss.detach(), "logits": logits.detach(), "preds": preds,
             "accuracy": (preds == labels).float().mean()}

@@ -204,12 +204,16 @@ __global__ __launch_bounds__(kLossThreads) void k_bce_logits(int n, int c, const
 // short and put c/32 workgroups on the chip (64 channels x 16 groups: 6.2-6.8 us per launch at c=512)
 constexpr int kBnCh = TSPM_BN1D_CH, kBnGroups = 1024 / TSPM_BN1D_CH;
 
-TSPM_DEV float bn_group_sum(float v, float* red) {
+// Per-channel sums of the row groups, in double and in fixed group order.  BatchNorm1d runs over as
+// few as 4 rows here, where the backward's projection (g - mean(g) - xhat * mean(g xhat)) cancels
+// most of g: the statistics and sums are formed in double (as ATen's CPU kernels accumulate) so the
+// cancellation does not amplify fp32 rounding.
+TSPM_DEV double bn_group_sum(double v, double* red) {
   const int ch = threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   __syncthreads();
   red[grp * kBnCh + ch] = v;
   __syncthreads();
-  float t = 0.f;
+  double t = 0.0;
 #pragma unroll
   for (int q = 0; q < kBnGroups; ++q) t += red[q * kBnCh + ch];
   return t;
@@ -228,24 +232,24 @@ struct Bn1dFwd {
   float* y;
 };
 
-TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, float* red);
+TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red);
 
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, Bn1dFwd p) {
-  __shared__ float red[kBnCh * kBnGroups];
+  __shared__ double red[kBnCh * kBnGroups];
   bn1d_fwd_body(m, p, blockIdx.x, red);
 }
 
 // Two independent BatchNorm1d layers over the same rows (the MMIMDb image and text encoders' input
 // BNs) in one launch: blocks [0, nb0) take p0.
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd2(int m, Bn1dFwd p0, Bn1dFwd p1, int nb0) {
-  __shared__ float red[kBnCh * kBnGroups];
+  __shared__ double red[kBnCh * kBnGroups];
   if ((int)blockIdx.x < nb0)
     bn1d_fwd_body(m, p0, blockIdx.x, red);
   else
     bn1d_fwd_body(m, p1, blockIdx.x - nb0, red);
 }
 
-TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, float* red) {
+TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red) {
   const int c = p.c;
   const float* __restrict__ x = p.x;
   const float momentum = p.momentum, eps = p.eps;
@@ -253,27 +257,27 @@ TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, float* red) {
   float* __restrict__ rvar = p.rvar;
   const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
-  float s = 0.f;
+  double s = 0.0;
   if (ok)
 #pragma unroll 4
-    for (int r = grp; r < m; r += kBnGroups) s += x[(long long)r * c + ch];
-  const float mean = bn_group_sum(s, red) / (float)m;
-  float q = 0.f;
+    for (int r = grp; r < m; r += kBnGroups) s += (double)x[(long long)r * c + ch];
+  const double meand = bn_group_sum(s, red) / (double)m;
+  double q = 0.0;
   if (ok)
 #pragma unroll 4
     for (int r = grp; r < m; r += kBnGroups) {
-      const float d = x[(long long)r * c + ch] - mean;
-      q = fmaf(d, d, q);
+      const double d = (double)x[(long long)r * c + ch] - meand;
+      q = fma(d, d, q);
     }
-  const float m2 = bn_group_sum(q, red);
-  const float var = m2 / (float)m;
-  const float invstd = 1.f / sqrtf(var + eps);
+  const double m2 = bn_group_sum(q, red);
+  const float mean = (float)meand;
+  const float invstd = (float)(1.0 / sqrt(m2 / (double)m + (double)eps));
   if (!ok) return;
   if (grp == 0) {
     p.smean[ch] = mean;
     p.sinvstd[ch] = invstd;
     if (rmean) rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * mean;
-    if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (m > 1 ? m2 / (float)(m - 1) : m2);
+    if (rvar) rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (float)(m > 1 ? m2 / (double)(m - 1) : m2);
   }
   const float ga = p.gamma[ch], be = p.beta[ch];
   for (int r = grp; r < m; r += kBnGroups) {
@@ -298,22 +302,22 @@ struct Bn1dBwd {
   float* mo_da;
 };
 
-TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, float* red);
+TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red);
 
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, Bn1dBwd p) {
-  __shared__ float red[kBnCh * kBnGroups];
+  __shared__ double red[kBnCh * kBnGroups];
   bn1d_bwd_body(m, p, blockIdx.x, red);
 }
 
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd2(int m, Bn1dBwd p0, Bn1dBwd p1, int nb0) {
-  __shared__ float red[kBnCh * kBnGroups];
+  __shared__ double red[kBnCh * kBnGroups];
   if ((int)blockIdx.x < nb0)
     bn1d_bwd_body(m, p0, blockIdx.x, red);
   else
     bn1d_bwd_body(m, p1, blockIdx.x - nb0, red);
 }
 
-TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, float* red) {
+TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   const int c = p.c;
   const float* __restrict__ g = p.g;
   const float* __restrict__ x = p.x;
@@ -330,27 +334,27 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, float* red) {
   const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
   const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
-  float sg = 0.f, sgx = 0.f;
+  double sg = 0.0, sgx = 0.0;
   if (ok)
 #pragma unroll 4
     for (int r = grp; r < m; r += kBnGroups) {
       const long long i = (long long)r * c + ch;
-      const float gv = g[i];
+      const double gv = (double)g[i];
       sg += gv;
-      sgx = fmaf(gv, (x[i] - mean) * invstd, sgx);
+      sgx = fma(gv, ((double)x[i] - (double)mean) * (double)invstd, sgx);
     }
-  const float tg = bn_group_sum(sg, red);
-  const float tgx = bn_group_sum(sgx, red);
+  const double tg = bn_group_sum(sg, red);
+  const double tgx = bn_group_sum(sgx, red);
   if (!ok) return;
   if (grp == 0) {
-    dgamma[ch] = tgx;
-    dbeta[ch] = tg;
+    dgamma[ch] = (float)tgx;
+    dbeta[ch] = (float)tg;
   }
   if (!dx && !mo_da) return;
-  const float k = gamma[ch] * invstd, mg = tg / (float)m, mgx = tgx / (float)m;
+  const double k = (double)gamma[ch] * (double)invstd, mg = tg / (double)m, mgx = tgx / (double)m;
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
-    const float v = k * (g[i] - mg - (x[i] - mean) * invstd * mgx);
+    const float v = (float)(k * ((double)g[i] - mg - ((double)x[i] - (double)mean) * (double)invstd * mgx));
     if (dx) dx[i] = v;
     if (mo_da) {  // x was MaxOut(2)+Dropout of a[m, 2c]: route v as k_maxout_bwd does
       const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;

@@ -97,3 +97,82 @@ def mono_flops_per_sample(layers=(2, 2, 2, 2), hw=(32, 94), hidden=64, classes=1
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+# ------------------------------------------------------------------------------------------------
+# Device-side kernel durations (measurement only; bench.py's roofline line)
+# ------------------------------------------------------------------------------------------------
+import re as _re
+
+CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|bwd_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
+                          r"conv_wgrad|conv_wgrad_t|reduce_slabs)\b")
+CONV_SECONDARY = _re.compile(r"\bk_reduce_slabs\b")  # second kernel of a split-K wgrad launch (variant 0)
+
+
+def device_kernels(run, replays: int):
+    """Run ``run()`` ``replays`` times under torch.profiler (kineto / rocprofiler on ROCm: the same
+    device timestamps rocprofv3 reports, including the kernels of replayed HIP graphs) and return the
+    GPU kernel records as dicts {name, stream, ts (us), dur (us)} sorted by start time."""
+    import json
+    import os
+    import tempfile
+
+    import torch
+    from torch.profiler import ProfilerActivity, profile
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(replays):
+            run()
+        torch.cuda.synchronize()
+    fd, path = tempfile.mkstemp(suffix=".json")
+    os.close(fd)
+    try:
+        prof.export_chrome_trace(path)
+        with open(path) as f:
+            trace = json.load(f)
+    finally:
+        os.remove(path)
+    ks = [{"name": e["name"], "stream": e.get("args", {}).get("stream"), "ts": float(e["ts"]), "dur": float(e["dur"])}
+          for e in trace.get("traceEvents", []) if e.get("cat") == "kernel"]
+    return sorted(ks, key=lambda k: k["ts"])
+
+
+class LaunchRecorder:
+    """engine.EncoderEngine.conv_timer hook that only records the (op, kind) of every conv launch in
+    issue order (kind: fwd / dgrad / wgrad / bwd = dgrad + wgrad in one launch)."""
+
+    def __init__(self):
+        self.launches = []
+
+    def begin(self, op, kind):
+        self.launches.append((op, kind))
+
+    def end(self):
+        pass
+
+
+def launch_flops(op, kind) -> int:
+    """Valid-tap FLOPs of one conv launch."""
+    s = op.shape
+    _, valid = conv_macs(s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad)
+    return 2 * valid * (2 if kind == "bwd" else 1)
+
+
+def attribute_conv_kernels(kernels, launches, replays: int):
+    """Map the conv-family kernels of ONE stream (``kernels``, start-ordered, ``replays`` step replays)
+    to that stream's conv launch sequence (``launches`` from a LaunchRecorder, one step).  A split-K
+    reduce kernel is charged to the launch before it.  Returns per-launch average durations (us), or
+    None when the kernel count does not match the launch sequence."""
+    main = [k for k in kernels if not CONV_SECONDARY.search(k["name"])]
+    if len(main) != replays * len(launches):
+        return None
+    per = [0.0] * len(launches)
+    li = -1
+    for k in kernels:
+        if CONV_SECONDARY.search(k["name"]):
+            if li >= 0:
+                per[li % len(launches)] += k["dur"]
+            continue
+        li += 1
+        per[li % len(launches)] += k["dur"]
+    return [d / replays for d in per]

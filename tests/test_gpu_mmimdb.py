@@ -1,11 +1,10 @@
 """MMIMDb late-fusion step (BASELINE configs[3]) on the HIP path against the CPU oracle
 (oracle/mmimdb_ref.py, pinned bit-exact to the real reference by tests/golden/make_mmimdb_golden.py).
-Criterion as tests/test_gpu_model.py: the oracle in fp64 is the truth; ours must stay within
-FACTOR (4x) the fp32 reference's own relative-L2 error plus a floor (2e-6 outputs, 2e-5 gradients),
-gradients may take the flip-tolerant bound (rel-L2 <= 2e-2 and cosine >= 0.9999: MaxOut argmax and
-threshold flips).  Logits additionally get the end-to-end floor of SURVEY §8c (rel-L2 <= 1e-4 against
-fp64 is the stated fp32 tolerance): the 4096-long encoder dot products summed in split-K order by the
-MFMA kernel and BatchNorm1d over as few as 4 rows put our error a few 1e-6 above the fp32 oracle's."""
+Criterion as tests/test_gpu_model.py (tests/parity.py): the oracle in fp64 with our MaxOut unit choices
+forced into it (oracle.mmimdb_ref.MaxOutTrace; every choice that differs from fp64's own must be a
+near-tie, and rare) is the truth; logits / loss rel-L2 <= 1e-4, every gradient rel-L2 <= 1e-3 and
+cosine >= 0.9999, each also within 4x the fp32 reference's error on the same choices; no relaxed
+branch.  Every step is checked from our own state (params, Adam moments, BN buffers)."""
 import copy
 
 import numpy as np
@@ -14,10 +13,7 @@ import torch
 
 import tspm_amd
 from oracle import mmimdb_ref as orc
-from oracle.avmnist_ref import OracleAdam
-from test_gpu_model import check, check_grad, rel_l2
-
-FLOOR_LOGITS = 5e-5  # end-to-end logits rel-L2 <= 1e-4 (fp32)
+from parity import GRAD_REL, MAX_FLIP_FRAC, NEAR, Tally, check_adam, check_grad, check_out, rel_l2, snapshot
 from test_mmimdb_cpu import dropin
 from tspm_amd import _lib as L
 from tspm_amd import mmimdb as M
@@ -40,7 +36,7 @@ def _keep(n, seed):
     return (torch.rand(2, n, 512, generator=g) >= 0.5).to(torch.uint8)
 
 
-def _sync_oracle(ours, opt, o, oopt):
+def _sync_oracle(ours, opt, o, oopt=None):
     """Restart the oracle from OUR state (params, Adam moments, BN buffers) so every step is checked
     on its own: at B=4 with BatchNorm1d, Adam's ~lr*sign(g) first steps turn near-zero gradient
     differences into 2*lr parameter differences, and trajectories diverge chaotically after step 1."""
@@ -48,70 +44,122 @@ def _sync_oracle(ours, opt, o, oopt):
     with torch.no_grad():
         for i, ((_, p), po) in enumerate(zip(ours.named_parameters(), o.parameters())):
             po.copy_(p.detach().cpu().to(dt))
-            oopt.m[i].copy_(opt.state[p]["exp_avg"].cpu().to(dt))
-            oopt.v[i].copy_(opt.state[p]["exp_avg_sq"].cpu().to(dt))
+            if oopt is not None:
+                oopt.m[i].copy_(opt.state[p]["exp_avg"].cpu().to(dt))
+                oopt.v[i].copy_(opt.state[p]["exp_avg_sq"].cpu().to(dt))
         sd = o.state_dict()
         for k, v in ours.state_dict().items():
             if "running" in k or "num_batches" in k:
                 sd[k].copy_(v.cpu().to(sd[k].dtype))
 
 
+def _decisions(st):
+    """Our MaxOut unit choices (0 / 1 / 2 = tie) from the step's saved unit outputs A1, A2 [n, 2h]."""
+    out = {}
+    for site, A in (("mo1", st.eng.A1), ("mo2", st.eng.A2)):
+        a = A.detach().cpu()
+        h = a.shape[1] // 2
+        a0, a1 = a[:, :h], a[:, h:]
+        out[site] = torch.where(a1 > a0, 1, torch.where(a1 == a0, 2, 0)).to(torch.int8)
+    return out
+
+
+def _flips(trace64, forced, keep):
+    """Every forced choice that differs from fp64's own is a near-tie; flips are rare."""
+    rep = {}
+    for k, site in enumerate(("mo1", "mo2")):
+        a0, a1 = trace64.units[site]
+        f = forced[site]
+        nat = (a1 > a0).to(torch.int8)
+        flip = (f != nat) & keep[k].bool()
+        d = (a1 - a0).abs()
+        rms = torch.cat([a0, a1]).pow(2).mean().sqrt().item() or 1.0
+        worst = (d[flip].max().item() / rms) if flip.any() else 0.0
+        assert worst <= NEAR, f"{site}: a flipped MaxOut choice is {worst:.2e} x rms from a tie"
+        assert int(flip.sum()) <= max(1, MAX_FLIP_FRAC * f.numel()), f"{site}: {int(flip.sum())} flips"
+        rep[site] = (int(flip.sum()), worst)
+    return rep
+
+
+def _check(name, ours, st, o32, o64, I, T, y, keep, out, tally, ref32_logits=None, ref32_loss=None, vs32=True):
+    """vs32=False: the §8(c) bounds only, without the within-4x-of-the-fp32-reference comparison — used
+    for the free-running n=4 case, where BatchNorm1d statistics over 4 rows with dropout put channels
+    at var ~ eps (invstd ~ 300): one element's GEMM rounding then dominates a gradient's error, in ours
+    and in ATen alike (scripts/diag_mmimdb_bn.py), so a single fp32 implementation is no yardstick."""
+    forced = _decisions(st)
+    t32, t64 = orc.MaxOutTrace(forced), orc.MaxOutTrace(forced)
+    r32 = orc.train_step(o32, None, I, T, y, keep[0], keep[1], t32)
+    r64 = orc.train_step(o64, None, I.double(), T.double(), y.double(), keep[0], keep[1], t64)
+    rep = _flips(t64, forced, keep)
+    check_out(f"logits {name}", out["logits"], r32["logits"] if ref32_logits is None else ref32_logits,
+              r64["logits"], tally)
+    check_out(f"loss {name}", out["loss"], r32["loss"] if ref32_loss is None else ref32_loss, r64["loss"], tally)
+    p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
+    for pname, p in ours.named_parameters():
+        check_grad(f"{pname} {name}", p.grad, p32[pname].grad if vs32 else None, p64[pname].grad, tally)
+    s32, s64 = o32.state_dict(), o64.state_dict()
+    for k, v in ours.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            check_out(f"{k} {name}", v, s32[k], s64[k], tally, bound=GRAD_REL)
+    return rep
+
+
 @pytest.mark.parametrize("n", [4, 64, 128, 256])
 def test_fused_step_vs_oracle(gpu, n):
     ours, opt, st, o32, o64 = _setup(gpu, n)
-    op32 = OracleAdam(list(o32.parameters()), lr=LR, weight_decay=WD)
-    op64 = OracleAdam(list(o64.parameters()), lr=LR, weight_decay=WD)
     I, T, y = orc.synthetic_batch(n, seed=77)
+    tally = Tally()
     for s in range(3):
         keep = _keep(n, 10 + s)
         if s > 0:
-            _sync_oracle(ours, opt, o32, op32)
-            _sync_oracle(ours, opt, o64, op64)
+            _sync_oracle(ours, opt, o32)
+            _sync_oracle(ours, opt, o64)
+        before = snapshot(ours, opt if s else None)
         st.keep_override = keep.to(gpu)
         out = st.step(I.to(gpu), T.to(gpu), y.to(gpu))
         torch.cuda.synchronize()
-        r32 = orc.train_step(o32, op32, I, T, y, keep[0], keep[1])
-        r64 = orc.train_step(o64, op64, I.double(), T.double(), y.double(), keep[0], keep[1])
-        check(f"logits s{s}", out["logits"], r32["logits"], r64["logits"], FLOOR_LOGITS)
-        check(f"loss s{s}", out["loss"], r32["loss"], r64["loss"], FLOOR_LOGITS)
-        if s == 0:
-            p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
-            for name, p in ours.named_parameters():
-                check_grad(name, p.grad, p32[name].grad, p64[name].grad)
+        rep = _check(f"s{s}", ours, st, o32, o64, I, T, y, keep, out, tally, vs32=n >= 32)
+        check_adam(ours, opt, *before, s + 1, lr=LR, wd=WD)
+        print(f"[n={n} step {s + 1}] maxout flips {rep}")
     for k, v in ours.state_dict().items():
-        if k.endswith("running_mean") or k.endswith("running_var"):
-            assert rel_l2(v, o64.state_dict()[k]) < 1e-4, k
         if k.endswith("num_batches_tracked"):
             assert int(v) == 3, k
+    print(tally)
 
 
 def test_fused_step_vs_golden_reference(gpu):
     """3 fused steps (eager, then captured graph) on the vectors the real MML_Suite MMIMDb.train_step
-    produced (B=4, seed-0 weights, the reference's dropout masks)."""
+    produced (B=4, seed-0 weights, the reference's dropout masks): step 1 against the golden fp32
+    reference and the forced fp64 oracle, later steps and the eval forward from our own state."""
     mg = dict(np.load("tests/golden/mmimdb_step_b4.npz", allow_pickle=False))
-    ours, opt, st, _, o64 = _setup(gpu, 4)
-    op64 = OracleAdam(list(o64.parameters()), lr=LR, weight_decay=WD)
+    ours, opt, st, o32, o64 = _setup(gpu, 4)
     I, T, y = (torch.from_numpy(mg[k]) for k in ("image", "text", "labels"))
+    tally = Tally()
     for s in range(3):
         k1, k2 = torch.from_numpy(mg["keep1"][s]), torch.from_numpy(mg["keep2"][s])
-        if s > 0:  # later steps: one-step error from our state (the golden logits pin step 1 only)
-            _sync_oracle(ours, opt, o64, op64)
+        if s > 0:
+            _sync_oracle(ours, opt, o32)
+            _sync_oracle(ours, opt, o64)
+        before = snapshot(ours, opt if s else None)
         st.keep_override = torch.stack([k1, k2]).to(gpu)
         out = st.step(I.to(gpu), T.to(gpu), y.to(gpu))
         torch.cuda.synchronize()
-        r64 = orc.train_step(o64, op64, I.double(), T.double(), y.double(), k1, k2)
+        keep = torch.stack([k1, k2])
         if s == 0:
-            check("logits s0", out["logits"], torch.from_numpy(mg["logits"][0]), r64["logits"], FLOOR_LOGITS)
-            assert abs(out["loss"].item() - float(mg["losses"][0])) <= 1e-5 * abs(float(mg["losses"][0]))
+            _check("s0", ours, st, o32, o64, I, T, y, keep, out, tally,
+                   torch.from_numpy(mg["logits"][0]), torch.tensor(float(mg["losses"][0])))
             gn = np.array([p.grad.double().norm().item() for p in ours.parameters()])
-            np.testing.assert_allclose(gn, mg["grad_norm_step1"], rtol=2e-3, atol=1e-9)
+            gn64 = np.array([q.grad.norm().item() for q in o64.parameters()])
+            check_out("grad norms s0", gn, mg["grad_norm_step1"], gn64, tally, bound=GRAD_REL)
         else:
-            assert rel_l2(out["logits"], r64["logits"]) <= 1e-4, f"logits s{s}"
-    _sync_oracle(ours, opt, o64, op64)
+            _check(f"s{s}", ours, st, o32, o64, I, T, y, keep, out, tally)
+        check_adam(ours, opt, *before, s + 1, lr=LR, wd=WD)
+    _sync_oracle(ours, opt, o64)
     ours.eval()
     ev = ours(I.to(gpu), T.to(gpu))
     ref_ev = orc.eval_forward(o64, I.double(), T.double())
-    assert rel_l2(ev, ref_ev) <= 1e-4
+    check_out("eval logits", ev, None, ref_ev, tally)
+    print(tally)
 
 
 def test_graph_replay_equals_eager(gpu):
