@@ -612,7 +612,7 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
-extern "C" int tspm_abi_version(void) { return 11; }
+extern "C" int tspm_abi_version(void) { return TSPM_ABI_VERSION; }
 
 extern "C" const char* tspm_status_string(int status) {
   switch (status) {

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void k_maxout_fwd(int n, int d, const float* _
     const long long r = t / d;
     const int j = (int)(t - r * d);
     const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
-    float v = a1 > a0 ? a1 : a0;
+    float v = (a1 > a0 || a1 != a1) ? a1 : a0;  // NaN in either unit propagates (torch.max)
     if (keep) v = v * (keep[t] ? scale : 0.f);
     y[r * ldy + j] = v;
   }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_maxout_fwd_rng(int n, int d, const floa
     const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
     const bool k = tspm_dropout_keep(base, index_offset + t, p);
     keep[t] = k ? 1 : 0;
-    const float v = a1 > a0 ? a1 : a0;
+    const float v = (a1 > a0 || a1 != a1) ? a1 : a0;  // NaN in either unit propagates (torch.max)
     y[r * ldy + j] = v * (k ? scale : 0.f);
   }
 }
@@ -128,8 +128,10 @@ __global__ __launch_bounds__(256) void k_maxout_bwd(int n, int d, const float* _
     if (keep) g = g * (keep[t] ? scale : 0.f);
     const float a0 = a[r * lda + j], a1 = a[r * lda + d + j];
     const float half = 0.5f * g;
-    da[r * ldda + j] = a0 > a1 ? g : (a0 == a1 ? half : 0.f);
-    da[r * ldda + d + j] = a1 > a0 ? g : (a0 == a1 ? half : 0.f);
+    // torch.maximum's derivative: where(a0 == a1, g/2, g) masked to 0 where the unit is the smaller one
+    // (so a NaN in either unit sends the full gradient to both, as ATen does)
+    da[r * ldda + j] = a0 == a1 ? half : (a0 < a1 ? 0.f : g);
+    da[r * ldda + d + j] = a0 == a1 ? half : (a1 < a0 ? 0.f : g);
   }
 }
 
@@ -360,8 +362,8 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
       const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;
       const float a0 = mo_a[(long long)r * 2 * c + ch], a1 = mo_a[(long long)r * 2 * c + c + ch];
       const float half = 0.5f * gv;
-      mo_da[(long long)r * 2 * c + ch] = a0 > a1 ? gv : (a0 == a1 ? half : 0.f);
-      mo_da[(long long)r * 2 * c + c + ch] = a1 > a0 ? gv : (a0 == a1 ? half : 0.f);
+      mo_da[(long long)r * 2 * c + ch] = a0 == a1 ? half : (a0 < a1 ? 0.f : gv);
+      mo_da[(long long)r * 2 * c + c + ch] = a0 == a1 ? half : (a1 < a0 ? 0.f : gv);
     }
   }
 }

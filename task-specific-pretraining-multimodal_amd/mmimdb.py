@@ -40,6 +40,9 @@ _FUSE_BN_MAXOUT = os.environ.get("TSPM_MMIMDB_FUSE", "0") == "1"
 # TSPM_MMIMDB_PAIRS=0: the independent image / text launches (input BatchNorm1d forward and backward, the
 # GMU projections) as separate launches instead of merged pairs (A/B; bitwise equal)
 _PAIRS = os.environ.get("TSPM_MMIMDB_PAIRS", "1") != "0"
+# TSPM_MMIMDB_RNG=0: draw the dropout masks with a separate tspm_dropout_mask launch instead of inside the
+# MaxOut forwards (tspm_maxout_fwd_rng; same bits — A/B switch for that fusion alone)
+_RNG_INLAUNCH = os.environ.get("TSPM_MMIMDB_RNG", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -313,7 +316,7 @@ class MMIMDbEngine:
         # classifier (models/mmimdb.py:38-47)
         keep, k1, k2, scale = None, None, None, 1.0
         # in-launch masks: each MaxOut forward draws its half of the mask tspm_dropout_mask would write
-        rng = train and self.p > 0 and self.keep_override is None and _PAIRS
+        rng = train and self.p > 0 and self.keep_override is None and _RNG_INLAUNCH
         if train and self.p > 0:
             scale = 1.0 / (1.0 - self.p)
             if self.keep_override is None and not rng:
@@ -652,9 +655,11 @@ class MMIMDbCorpus:
             m[pattern] = (torch.full((n,), ip, device=self.device), torch.full((n,), tp, device=self.device))
         return m[pattern]
 
-    def gather(self, index: torch.Tensor, I_out, T_out, Y_out, pattern: str = "it") -> None:
+    def gather(self, index: torch.Tensor, I_out, T_out, Y_out, pattern: str = "it", row_masks=None) -> None:
+        """Rows ``index`` into the step's buffers; the absent modality of ``pattern`` zeroed, or per row
+        with ``row_masks`` = (image presence [n], text presence [n]) float tensors."""
         lib, sh, n = L.lib(), L.stream_handle(), index.numel()
-        im, tm = self._mask(n, pattern)
+        im, tm = self._mask(n, pattern) if row_masks is None else row_masks
         for src, w, mask, out in ((self.image, self.image.shape[1], im, I_out), (self.text, self.text.shape[1], tm, T_out),
                                   (self.labels, self.labels.shape[1], None, Y_out)):
             L.check(lib.tspm_avmnist_gather(n, index.data_ptr(), self.n, src.data_ptr(), w, None, 0, None, None,
@@ -662,13 +667,13 @@ class MMIMDbCorpus:
 
 
 def _evaluate(model: MMIMDb, corpus: MMIMDbCorpus, batch: int, weight: float, pattern: str) -> Dict[str, float]:
+    """Metrics of one missing-data pattern over the whole validation corpus (eval mode: BatchNorm
+    running statistics, so a one-row last batch is valid, as in the reference)."""
     model.eval()
     sh = L.stream_handle()
     stats = None
     for s in range(0, corpus.n, batch):
         idx = torch.arange(s, min(s + batch, corpus.n), device=corpus.device)
-        if idx.numel() < 2:
-            break
         eng = model._engine(idx.numel(), corpus.device)
         if stats is None:
             stats = torch.zeros_like(eng.stats)
@@ -680,34 +685,91 @@ def _evaluate(model: MMIMDb, corpus: MMIMDbCorpus, batch: int, weight: float, pa
     return f1_metrics(stats, model.mm_mlp.output_size)
 
 
+def validation_loss(model: MMIMDb, corpus: MMIMDbCorpus, batch: int, weight: float, patterns=("it", "i", "t"),
+                    generator: Optional[torch.Generator] = None) -> float:
+    """The loss train_multimodal.py monitors (save_metric "loss", :494-541,750-758): the mean of the
+    per-batch losses over the validation loader, whose dataset holds every sample once per selected
+    pattern (len = N x #patterns, item k -> pattern k // N: data/base_dataset.py:89-92) and which
+    shuffles (mmimdb_baseline.yaml: shuffle true — the permutation here is seeded, not the reference's
+    RNG draws).  Batches mix patterns; the absent modality is zeroed per row."""
+    model.eval()
+    sh = L.stream_handle()
+    n, P = corpus.n, len(patterns)
+    order = torch.randperm(n * P, generator=generator) if generator is not None else torch.arange(n * P)
+    pres = torch.tensor([PATTERNS[p] for p in patterns], dtype=torch.float32)
+    losses = []
+    for s in range(0, n * P, batch):
+        ks = order[s:s + batch]
+        idx, pid = (ks % n).to(corpus.device), ks // n
+        im, tm = pres[pid, 0].to(corpus.device), pres[pid, 1].to(corpus.device)
+        eng = model._engine(ks.numel(), corpus.device)
+        corpus.gather(idx, eng.I, eng.T, eng.labels, row_masks=(im, tm))
+        eng.forward(sh, False)
+        eng.loss_fn(sh, weight, False, False)
+        losses.append(eng.loss.clone())
+    # one host read for the epoch; np.mean of the per-batch fp32 losses as the reference computes it
+    import numpy as np
+    return float(np.mean([float(v) for v in torch.cat(losses).cpu()]))
+
+
 def fit_mmimdb(model: MMIMDb, optimizer: FusedAdam, train: MMIMDbCorpus, val: MMIMDbCorpus, batch: int,
                epochs: int, loss_functions=None, patience: int = 25, seed: int = 0,
-               patterns=("it", "i", "t")) -> List[Dict[str, Any]]:
-    """The epoch loop of train_multimodal.py for the MMIMDb config (shuffled train batches, drop_last;
-    validation on each selected missing pattern with the absent modality zeroed; early stopping on
-    the full-pattern validation loss with the YAML's patience 25), every batch on the HIP path.
-    Returns one dict per epoch: train loss / f1s and ``val_{pattern}`` metrics."""
+               patterns=("it", "i", "t"), min_delta: float = 1e-3, checkpoint_dir=None,
+               scheduler=None) -> List[Dict[str, Any]]:
+    """The epoch loop of train_multimodal.py for the MMIMDb config, every batch on the HIP path:
+    shuffled train batches over every sample (the DataLoader's drop_last=False, config/data_config.py:121;
+    a last batch of one row is skipped — BatchNorm1d in training mode rejects it in the reference too),
+    the validation loss over all selected patterns together (``validation_loss``), per-pattern
+    validation metrics with the absent modality zeroed, early stopping on that loss with the
+    reference's check (harness.check_early_stopping: patience 25 from the YAML, min_delta 1e-3 =
+    TrainingConfig.early_stopping_min_delta), ``epoch_{n}.pth`` / ``best.pth`` through
+    harness.CheckpointManager on improvement, and ReduceLROnPlateau on the validation loss.
+    Returns one dict per epoch: train loss / f1s, ``val_loss`` and ``val_{pattern}`` metrics."""
+    from .harness import CheckpointManager, check_early_stopping
     weight = _bce_weight(loss_functions)
-    step = FusedMMIMDbStep(model, optimizer, loss_functions, batch)
-    step.log_stats = True
+    steps: Dict[int, FusedMMIMDbStep] = {}
+
+    def step_for(n):
+        st = steps.get(n)
+        if st is None:
+            st = FusedMMIMDbStep(model, optimizer, loss_functions, n)
+            st.log_stats = True
+            steps[n] = st
+        return st
+    main = step_for(batch)
     gen = torch.Generator(device="cpu").manual_seed(seed)
-    history, best, bad = [], float("inf"), 0
-    for ep in range(epochs):
+    vgen = torch.Generator(device="cpu").manual_seed(seed + 1)
+    ckpt = CheckpointManager(checkpoint_dir) if checkpoint_dir is not None else None
+    history, best, wait = [], None, 0
+    for ep in range(1, epochs + 1):
         model.train()
-        step.eng.stats.zero_()
+        for st in steps.values():
+            st.eng.stats.zero_()
         perm = torch.randperm(train.n, generator=gen).to(train.device)
-        for s in range(0, train.n - batch + 1, batch):
-            train.gather(perm[s:s + batch], step.eng.I, step.eng.T, step.eng.labels)
-            step.run()
-        rec = {"epoch": ep, "train": f1_metrics(step.eng.stats, model.mm_mlp.output_size)}
+        for s in range(0, train.n, batch):
+            rows = perm[s:s + batch]
+            if rows.numel() < 2:
+                break
+            st = step_for(rows.numel())
+            train.gather(rows, st.eng.I, st.eng.T, st.eng.labels)
+            st.run()
+        tot = main.eng.stats.clone()
+        for n, st in steps.items():
+            if n != batch:
+                tot += st.eng.stats
+        rec = {"epoch": ep, "train": f1_metrics(tot, model.mm_mlp.output_size),
+               "val_loss": validation_loss(model, val, batch, weight, patterns, vgen)}
         for p in patterns:
             rec[f"val_{p}"] = _evaluate(model, val, batch, weight, p)
         history.append(rec)
-        vl = rec[f"val_{patterns[0]}"]["loss"]
-        if vl < best - 1e-4:
-            best, bad = vl, 0
-        else:
-            bad += 1
-            if bad >= patience:
-                break
+        vm = {"loss": rec["val_loss"]}
+        is_best, cont, wait = check_early_stopping(vm, best, patience, min_delta, wait)
+        if is_best:
+            best = dict(vm)
+            if ckpt is not None:
+                ckpt.save_checkpoint(model, optimizer, scheduler, ep, vm, is_best=True)
+        if not cont:
+            break
+        if scheduler is not None:
+            scheduler.step(rec["val_loss"])
     return history

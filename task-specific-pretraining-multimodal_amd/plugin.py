@@ -12,6 +12,14 @@ The reference builds models through two seams:
 reference's ``config.resolvers`` module is importable in the process, wraps the resolvers so the
 names above return this package's classes (other names fall through to the originals).  After that,
 ``train_multimodal.py`` / ``train_monomodal.py`` and the YAML configs run unchanged on the HIP path.
+
+A third seam: with ``training.encoder_optimizer`` set and ``pretrained_encoders`` given (the
+pretrained late-fusion config, configs/avmnist/centralised/train_avmnist_resnet_pretrained.yaml:36),
+``setup_model_components`` bypasses ``resolve_optimizer`` and builds
+``getattr(torch.optim, config.training.optimizer.name)(param_groups)`` (train_multimodal.py:216-304).
+``register_script_optimizer`` makes that lookup return ``FusedAdam`` for "Adam" — inside the script
+module only (its global ``torch`` becomes a proxy whose ``optim.Adam`` is ``FusedAdam``; every other
+attribute is torch's own), so nothing else in the process is affected.
 """
 from __future__ import annotations
 
@@ -78,7 +86,10 @@ def register_resolvers(resolvers_module: Optional[object] = None, rebind_everywh
         setattr(mod, name, new)
         if rebind_everywhere:
             for m in list(sys.modules.values()):
-                if m is not None and m is not mod and getattr(m, name, None) is orig:
+                # the module's own namespace only: getattr would trigger lazy-import hooks
+                # (e.g. transformers' _LazyModule) in unrelated packages
+                d = getattr(m, "__dict__", None) if m is not None else None
+                if isinstance(d, dict) and m is not mod and d.get(name) is orig:
                     setattr(m, name, new)
     return True
 
@@ -99,9 +110,51 @@ def register_monomodal(module: Optional[object] = None) -> bool:
     return done
 
 
+class _OptimProxy:
+    """``torch.optim`` as the training script sees it: ``Adam`` is FusedAdam, the rest is torch's."""
+
+    def __init__(self, optim):
+        self._optim = optim
+
+    def __getattr__(self, name):
+        hit = OPTIMIZERS.get(name.lower())
+        return hit if hit is not None else getattr(self._optim, name)
+
+
+class _TorchProxy:
+    """The script module's global ``torch``: torch itself except for ``torch.optim`` (_OptimProxy)."""
+
+    def __init__(self, torch_mod):
+        self._torch = torch_mod
+        self.optim = _OptimProxy(torch_mod.optim)
+
+    def __getattr__(self, name):
+        return getattr(self._torch, name)
+
+
+def register_script_optimizer(module: Optional[object] = None) -> bool:
+    """Route ``getattr(torch.optim, "Adam")`` in ``train_multimodal`` (imported, or running as
+    ``__main__``) to FusedAdam: the script's own module global ``torch`` is replaced by a proxy."""
+    import torch
+    cands = [module] if module is not None else [sys.modules.get("train_multimodal"), sys.modules.get("__main__")]
+    done = False
+    for m in cands:
+        if m is None or not hasattr(m, "setup_model_components"):
+            continue
+        cur = getattr(m, "torch", None)
+        if isinstance(cur, _TorchProxy):
+            done = True
+            continue
+        if cur is torch:
+            m.torch = _TorchProxy(torch)
+            done = True
+    return done
+
+
 def register(loader=None, resolvers_module=None) -> None:
-    """Install the HIP implementations behind the reference's YAML tags, resolvers and the monomodal
-    script's model class."""
+    """Install the HIP implementations behind the reference's YAML tags, resolvers, the monomodal
+    script's model class and the multimodal script's param-group optimizer lookup."""
     register_yaml(loader)
     register_resolvers(resolvers_module)
     register_monomodal()
+    register_script_optimizer()

@@ -48,7 +48,7 @@ def _write_stubs(root: str) -> None:
                 def __str__(self):
                     return self.value
             def add_modality(name):
-                return Modality(name)
+                return Modality(str(name).lower())
             def create_missing_mask(n_modalities, batch, rates):
                 import torch
                 return torch.ones(batch, n_modalities)

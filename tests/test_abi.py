@@ -97,3 +97,16 @@ def test_workspace_queries():
     assert lib.tspm_conv_fwd_tile_rows(ctypes.byref(s), ctypes.byref(L.ConvAlgo(2, 1, 1, 1, 1, 1))) == 64
     assert lib.tspm_bn_stats_workspace(6272, 64) > 0
     assert lib.tspm_bn_bwd_workspace(6272, 64) >= lib.tspm_bn_stats_workspace(6272, 64)
+
+
+def test_abi_version_consistent_everywhere():
+    """include/tspm.h's TSPM_ABI_VERSION, the Python binding's expectation and the version the
+    INTEGRATION.md binding snippet asserts are the same number (the snippet must keep working)."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "include", "tspm.h")) as f:
+        hdr = int(re.search(r"#define TSPM_ABI_VERSION (\d+)", f.read()).group(1))
+    with open(os.path.join(root, "INTEGRATION.md")) as f:
+        doc = [int(v) for v in re.findall(r"tspm_abi_version\(\) == (\d+)", f.read())]
+    assert doc and all(v == hdr for v in doc)
+    assert L.ABI_VERSION == hdr

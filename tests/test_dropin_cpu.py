@@ -125,3 +125,44 @@ def test_roofline_accounting_matches_survey():
     nominal, valid = step_flops_per_sample()
     assert nominal == 1_049_740_032
     assert 0.6 < valid / nominal < 0.62
+
+
+def test_reference_config_resolution_fixture(golden):
+    """tests/golden/plugin_resolution.json was produced by the REAL reference (make_plugin_golden.py):
+    both AVMNIST configs — including the pretrained one, whose optimizer comes from
+    getattr(torch.optim, "Adam")(param_groups) at train_multimodal.py:216-304, not from
+    resolve_optimizer — resolve to this package's modules and FusedAdam once plugin.register() ran."""
+    import json
+    path = os.path.join(os.path.dirname(__file__), "golden", "plugin_resolution.json")
+    with open(path) as f:
+        fx = json.load(f)
+    assert fx["script_torch_is_proxy"] == "_TorchProxy"
+    cfgs = fx["configs"]
+    assert set(cfgs) == {"configs/avmnist/centralised/train_avmnist_resnet.yaml",
+                         "configs/avmnist/centralised/train_avmnist_resnet_pretrained.yaml"}
+    assert cfgs["configs/avmnist/centralised/train_avmnist_resnet_pretrained.yaml"]["optimizer_branch"].startswith(
+        "param_groups")
+    keys = list(golden["state_dict_keys"])
+    for name, d in cfgs.items():
+        assert d["model"] == "tspm_amd.modules.AVMNIST", name
+        assert d["audio_encoder"] == d["image_encoder"] == "tspm_amd.modules.ResNetEncoder", name
+        assert d["optimizer"] == "tspm_amd.optim.FusedAdam", name
+        assert d["state_dict_keys"] == keys, name
+        assert d["model_parameters"] == 178 and sum(g["params"] for g in d["param_groups"]) == 178, name
+        assert d["loss_terms"] == ["cross_entropy"], name
+        # one group over the whole model at the base optimizer's settings (the AVMNIST model has no
+        # image_model / audio_model attributes, so the encoder group of the pretrained branch is empty)
+        assert [(g["lr"], g["weight_decay"]) for g in d["param_groups"]] == [(5e-4, 1e-4)], name
+
+
+def test_script_optimizer_seam_is_scoped_to_the_script():
+    from tspm_amd import plugin
+    script = types.ModuleType("train_multimodal_fake")
+    script.torch = torch
+    script.setup_model_components = lambda *a: None
+    assert plugin.register_script_optimizer(script)
+    assert getattr(script.torch.optim, "Adam") is tspm_amd.FusedAdam
+    assert script.torch.optim.SGD is torch.optim.SGD and script.torch.nn is torch.nn
+    assert script.torch.no_grad is torch.no_grad
+    assert torch.optim.Adam is not tspm_amd.FusedAdam  # the real torch is untouched
+    assert plugin.register_script_optimizer(script)  # idempotent

@@ -212,9 +212,14 @@ def test_validation_step_and_metrics(gpu):
 
 
 def test_maxout_ties_split_gradient(gpu):
+    """Ties split the gradient and NaN propagates, both as torch.max(a0, a1) (models/maxout.py:40) and
+    its autograd derivative do (a NaN in either unit: NaN output, full gradient to both units)."""
     n, d = 8, 64
     a = torch.randn(n, 2 * d, device=gpu)
     a[:, d:d + 16] = a[:, :16]  # ties
+    a[0, 20] = float("nan")                                 # unit 0 NaN
+    a[1, d + 21] = float("nan")                             # unit 1 NaN
+    a[2, 22] = a[2, d + 22] = float("nan")                  # both
     dy = torch.randn(n, d, device=gpu)
     keep = (torch.rand(n, d, device=gpu) > 0.5).to(torch.uint8)
     y = torch.empty(n, d, device=gpu)
@@ -228,8 +233,11 @@ def test_maxout_ties_split_gradient(gpu):
     a1 = a[:, d:].cpu().requires_grad_(True)
     ref = torch.max(a0, a1) * (keep.cpu().float() * 2.0)
     ref.backward(dy.cpu())
-    assert torch.equal(y.cpu(), ref.detach())
-    assert torch.equal(da[:, :d].cpu(), a0.grad) and torch.equal(da[:, d:].cpu(), a1.grad)
+    same = lambda x, y_: torch.testing.assert_close(x, y_, rtol=0, atol=0, equal_nan=True)  # noqa: E731
+    same(y.cpu(), ref.detach())
+    assert torch.isnan(y[:3].cpu()).sum() == 3
+    same(da[:, :d].cpu(), a0.grad)
+    same(da[:, d:].cpu(), a1.grad)
 
 
 def test_gmu_kernels_vs_fp64(gpu):
@@ -269,15 +277,24 @@ def test_corpus_gather_and_patterns(gpu):
         assert torch.equal(Io.cpu(), I[ii] * ip) and torch.equal(To.cpu(), T[ii] * tp) and torch.equal(Yo.cpu(), y[ii])
 
 
-def test_fit_loop_metrics_match_oracle(gpu):
-    n_tr, n_va, B = 512, 200, 64
+def test_fit_loop_metrics_match_oracle(gpu, tmp_path):
+    """fit_mmimdb: every training sample is used (520 = 8 x 64 + a partial batch of 8, through a second
+    fused step), the validation corpus of 201 ends in a one-row eval batch, the monitored loss is the
+    mean of batch losses over the shuffled 3-pattern validation set, and best / epoch checkpoints are
+    written in the reference's format."""
+    n_tr, n_va, B = 520, 201, 64
     I, T, y = orc.synthetic_batch(n_tr, seed=41)
     Iv, Tv, yv = orc.synthetic_batch(n_va, seed=42)
     ours = dropin(2).to(gpu)
     opt = tspm_amd.FusedAdam(ours.parameters(), lr=1e-4, weight_decay=1e-3)
-    hist = M.fit_mmimdb(ours, opt, M.MMIMDbCorpus(I, T, y, gpu), M.MMIMDbCorpus(Iv, Tv, yv, gpu), B, epochs=3)
+    hist = M.fit_mmimdb(ours, opt, M.MMIMDbCorpus(I, T, y, gpu), M.MMIMDbCorpus(Iv, Tv, yv, gpu), B, epochs=3,
+                        checkpoint_dir=tmp_path)
     assert len(hist) == 3
     assert hist[-1]["train"]["loss"] < hist[0]["train"]["loss"]
+    assert (tmp_path / "best.pth").exists() and (tmp_path / "epoch_1.pth").exists()
+    ck = torch.load(tmp_path / "best.pth", weights_only=True)
+    assert set(ck) == {"model_state_dict", "optimizer_state_dict"}
+    assert list(ck["model_state_dict"]) == list(orc.build_oracle_mmimdb(0).state_dict())
     o = orc.build_oracle_mmimdb(2).double()
     sd = {k: v.detach().cpu().double() if v.is_floating_point() else v.cpu() for k, v in ours.state_dict().items()}
     o.load_state_dict(sd)
@@ -295,6 +312,19 @@ def test_fit_loop_metrics_match_oracle(gpu):
         assert abs(got["loss"] - ref["loss"]) <= 1e-4 * abs(ref["loss"]), pat
         for k in ("f1_samples", "f1_macro", "f1_weighted", "f1_micro"):
             assert abs(got[k] - ref[k]) <= 2e-2, (pat, k, got[k], ref[k])
+    # the monitored loss of the last epoch: mean of per-batch losses over the shuffled 3-pattern set
+    vgen = torch.Generator().manual_seed(1)
+    for _ in range(2):  # epochs 1 and 2 drew their permutations first
+        torch.randperm(3 * n_va, generator=vgen)
+    order = torch.randperm(3 * n_va, generator=vgen)
+    pres = torch.tensor([M.PATTERNS[p] for p in ("it", "i", "t")], dtype=torch.float64)
+    bl = []
+    for s in range(0, 3 * n_va, B):
+        ks = order[s:s + B]
+        idx, pid = ks % n_va, ks // n_va
+        lg = orc.eval_forward(o, Iv[idx].double() * pres[pid, :1], Tv[idx].double() * pres[pid, 1:])
+        bl.append(orc.bce_loss(lg, yv[idx].double()).item())
+    assert abs(hist[-1]["val_loss"] - float(np.mean(bl))) <= 1e-4 * abs(float(np.mean(bl)))
 
 
 @pytest.mark.parametrize("m,c", [(4, 300), (128, 4096), (256, 512), (1000, 68)])
@@ -476,11 +506,12 @@ def test_paired_launches_equal_separate(gpu, monkeypatch):
 
 def test_inlaunch_dropout_masks_equal_mask_kernel(gpu, monkeypatch):
     """tspm_maxout_fwd_rng draws exactly the keep bits tspm_dropout_mask writes: the step with in-launch
-    masks equals bitwise the step with the separate mask launch (TSPM_MMIMDB_PAIRS=0 path)."""
+    masks equals bitwise the step with the separate mask launch (TSPM_MMIMDB_RNG=0: only that fusion
+    differs between the two runs)."""
     n, res, masks = 64, [], []
     I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=16))
-    for pairs in (True, False):
-        monkeypatch.setattr(M, "_PAIRS", pairs)
+    for rng in (True, False):
+        monkeypatch.setattr(M, "_RNG_INLAUNCH", rng)
         ours, _, st, _, _ = _setup(gpu, n)
         ours._rng_seed = 12345
         for s in range(3):
@@ -491,3 +522,30 @@ def test_inlaunch_dropout_masks_equal_mask_kernel(gpu, monkeypatch):
     assert torch.equal(res[0], res[1])
     for a, b in zip(masks[:3], masks[3:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,h,ctr", [(37, 53, 5), (64, 512, 0), (3, 7, 123456789)])
+def test_maxout_fwd_rng_op_equals_mask_then_maxout(gpu, n, h, ctr):
+    """Op level: for each unit u, tspm_maxout_fwd_rng(index_offset = u*n*h) writes the keep bits of
+    tspm_dropout_mask's elements [u*n*h, (u+1)*n*h) and the output of tspm_maxout_fwd with them — odd
+    n and h (offsets and counts not multiples of 256) and nonzero step counters included."""
+    lib, sh = L.lib(), L.stream_handle()
+    g = torch.Generator().manual_seed(n * h)
+    a = torch.randn(2, n, 2 * h, generator=g).to(gpu)
+    counter = torch.tensor([ctr], dtype=torch.int64, device=gpu)
+    seed, p = 987654321, 0.5
+    keep_all = torch.empty(2 * n * h, dtype=torch.uint8, device=gpu)
+    L.check(lib.tspm_dropout_mask(2 * n * h, p, seed, counter.data_ptr(), keep_all.data_ptr(), sh), "mask")
+    for u in range(2):
+        k = torch.empty(n * h, dtype=torch.uint8, device=gpu)
+        y = torch.empty(n, h, device=gpu)
+        y_ref = torch.empty(n, h, device=gpu)
+        L.check(lib.tspm_maxout_fwd_rng(n, h, a[u].data_ptr(), 2 * h, p, seed, counter.data_ptr(), u * n * h,
+                                        k.data_ptr(), 2.0, y.data_ptr(), h, sh), "maxout rng")
+        ks = keep_all[u * n * h:(u + 1) * n * h].contiguous()
+        L.check(lib.tspm_maxout_fwd(n, h, a[u].data_ptr(), 2 * h, ks.data_ptr(), 2.0, y_ref.data_ptr(), h, sh), "mo")
+        torch.cuda.synchronize()
+        assert torch.equal(k, ks), u
+        assert torch.equal(y, y_ref), u
+    frac = keep_all.float().mean().item()
+    assert abs(frac - 0.5) < 0.05 or n * h < 64

@@ -311,3 +311,37 @@ def test_overlapped_adam_equals_plain_step(gpu):
         fg = opt.flat_groups()[0]
         results.append(torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).cpu())
     assert torch.equal(results[0], results[1]) and torch.equal(results[0], results[2])
+
+
+def test_pretrained_config_param_groups_run_fused_step(gpu, tmp_path):
+    """The pretrained late-fusion config (train_avmnist_resnet_pretrained.yaml) builds its optimizer as
+    getattr(torch.optim, "Adam")(param_groups) (train_multimodal.py:216-304): with the plugin that is
+    FusedAdam over ONE group holding every parameter at the base settings (the recorded resolution,
+    tests/golden/plugin_resolution.json).  The encoders' pretrained state_dicts load first
+    (:156-204), then train_step must run the fused HIP graph step, and match the same step built with
+    the keyword form of the optimizer bitwise."""
+    torch.manual_seed(5)
+    donor = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.0)
+    torch.save(donor.audio_encoder.state_dict(), tmp_path / "encoder_audio_best.pth")
+    torch.save(donor.image_encoder.state_dict(), tmp_path / "encoder_image_best.pth")
+    audio, image, labels, _ = orc.synthetic_batch(16, seed=21)
+    batch = {"audio": audio, "image": image, "labels": labels, "pattern_name": ["ai"] * 16}
+    res = []
+    for form in ("param_groups", "kwargs"):
+        torch.manual_seed(0)
+        m = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.0)
+        m.audio_encoder.load_state_dict(torch.load(tmp_path / "encoder_audio_best.pth", weights_only=True))
+        m.image_encoder.load_state_dict(torch.load(tmp_path / "encoder_image_best.pth", weights_only=True))
+        m.to(gpu)
+        if form == "param_groups":
+            opt = tspm_amd.plugin._OptimProxy(torch.optim).Adam([{"params": list(m.parameters()), "lr": 5e-4,
+                                                                   "weight_decay": 1e-4}])
+        else:
+            opt = tspm_amd.FusedAdam(m.parameters(), lr=5e-4, weight_decay=1e-4)
+        assert isinstance(opt, tspm_amd.FusedAdam)
+        for _ in range(3):
+            m.train_step(batch, opt, None, gpu, None)
+        assert m._fused_step is not None and m._fused_step.calls == 3
+        torch.cuda.synchronize()
+        res.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
+    assert torch.equal(res[0], res[1])

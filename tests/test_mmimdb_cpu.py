@@ -119,3 +119,20 @@ def test_bce_weight_checks_the_loss_group():
     assert M._bce_weight(Group(bce=Term(torch.nn.BCEWithLogitsLoss(), 2.0))) == 2.0
     with pytest.raises(tspm_amd.TspmError):
         M._bce_weight(Group(ce=Term(torch.nn.CrossEntropyLoss(), 1.0)))
+
+
+def test_early_stopping_epoch_pinned_on_a_loss_sequence():
+    """fit_mmimdb stops through harness.check_early_stopping with min_delta 1e-3
+    (TrainingConfig.early_stopping_min_delta, config/multimodal_training_config.py:48): improvements
+    smaller than 1e-3 count as no improvement (train_multimodal.py:329-377)."""
+    from tspm_amd.harness import check_early_stopping
+    losses = [0.50, 0.40, 0.3995, 0.3991, 0.3992, 0.3989, 0.30]
+    best, wait, stopped = None, 0, None
+    for ep, v in enumerate(losses, 1):
+        is_best, cont, wait = check_early_stopping({"loss": v}, best, 3, 1e-3, wait)
+        if is_best:
+            best = {"loss": v}
+        if not cont:
+            stopped = ep
+            break
+    assert stopped == 5 and best == {"loss": 0.40}
