@@ -1,0 +1,116 @@
+"""The data-parallel train step itself, two ranks on the one GPU of the test box.
+
+Two processes share cuda:0 and a gloo process group (gloo all-reduces device tensors through host
+copies; the driver's 8-GPU runs use RCCL with the same calls).  Each rank runs FusedTrainStep with
+``ddp.PhasedGradAllReduce`` — the overlapped exchange path bench.py uses at N > 1: per-phase HIP graphs,
+the phase-1 gradients all-reduced while phase 2 computes — on its half of a 64-sample batch, with
+FusedAdam(grad_scale = 1/2).  Checked:
+
+* the summed gradient buffer equals g_0 + g_1 bitwise, where g_r is rank r's gradient from a plain
+  (no exchange) fused step on the same half batch;
+* fp64 Adam applied to the averaged gradient (g_0 + g_1) / 2 reproduces every rank's update;
+* both ranks hold bitwise identical parameters and Adam moments after 1 and after 4 steps (eager
+  first step, then the captured phase graphs).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.dirname(here), here]
+        import torch.distributed as dist
+        import tspm_amd
+        from oracle import avmnist_ref as orc
+        from parity import adam_fp64
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        full_a, full_i, full_l, _ = orc.synthetic_batch(64, seed=2024)
+        half = slice(32 * rank, 32 * rank + 32)
+        keep_full = (torch.rand(64, 128, generator=torch.Generator().manual_seed(77)) > 0.5).to(torch.uint8)
+
+        def build():
+            torch.manual_seed(0)
+            m = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
+            return m
+        # plain fused step on this rank's half: the local gradient g_r
+        m_loc = build()
+        o_loc = tspm_amd.FusedAdam(m_loc.parameters(), lr=5e-4, weight_decay=1e-4)
+        s_loc = tspm_amd.FusedTrainStep(m_loc, o_loc, None, 32)
+        s_loc.keep_override = keep_full[half].to(dev)
+        s_loc.step(full_a[half].to(dev), full_i[half].to(dev), full_l[half].to(dev))
+        torch.cuda.synchronize()
+        g_loc = o_loc.flat_groups()[0].grad.clone()
+        # the DP step
+        m = build()
+        opt = tspm_amd.FusedAdam(m.parameters(), lr=5e-4, weight_decay=1e-4, grad_scale=1.0 / world)
+        st = tspm_amd.FusedTrainStep(m, opt, None, 32)
+        st.allreduce = st.phased_allreduce()
+        fg = opt.flat_groups()[0]
+        p0 = fg.param.detach().cpu().double().clone()
+        st.keep_override = keep_full[half].to(dev)
+        st.step(full_a[half].to(dev), full_i[half].to(dev), full_l[half].to(dev))
+        torch.cuda.synchronize()
+        gs = [torch.empty_like(g_loc) for _ in range(world)]
+        dist.all_gather(gs, g_loc)
+        ok_sum = bool(torch.equal(fg.grad, gs[0] + gs[1]))
+        exp, _, _ = adam_fp64(p0, (fg.grad.double().cpu()) / world, 1)
+        got = fg.param.detach().cpu().double()
+        ok_adam = bool(((got - exp).abs() <= 1e-6 * exp.abs() + 2e-9).all())
+        state1 = torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).clone()
+        for s in range(3):  # eager done; capture + replays of the phase graphs
+            a, i, lab, _ = orc.synthetic_batch(64, seed=3000 + s)
+            st.keep_override = keep_full[half].to(dev)
+            st.step(a[half].to(dev), i[half].to(dev), lab[half].to(dev))
+        torch.cuda.synchronize()
+        state4 = torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).clone()
+        same = []
+        for t in (state1, state4):
+            other = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(other, t)
+            same.append(bool(torch.equal(other[0], other[1])))
+        q.put((rank, ok_sum, ok_adam, same, st.graph is not None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
+
+
+def test_two_rank_phased_dp_step_on_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_sum, ok_adam, same, captured in res:
+        assert ok_sum is True, (rank, ok_sum)
+        assert ok_adam is True, rank
+        assert same == [True, True], (rank, same)
+        assert captured, rank
