@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 11
+#define TSPM_ABI_VERSION 12
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -316,6 +316,11 @@ int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream);
 /* One fused Adam update over `count` contiguous fp32 elements (the flat parameter buffer). */
 int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    const tspm_adam_hyper* hyper, tspm_stream_t stream);
+/* tspm_adam_step with the gradient also multiplied by the device scalar *clip_coef (ABI 12: the
+ * coefficient tspm_grad_clip_coef wrote — torch.nn.utils.clip_grad_norm_ before optimizer.step(),
+ * MML_Suite/models/msa/utt_fusion.py:188-190).  g' = (g * grad_scale) * clip_coef. */
+int tspm_adam_step_clip(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        const tspm_adam_hyper* hyper, const float* clip_coef, tspm_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Layout / data-stage helpers (collate → device, MML_Suite/data/avmnist.py:186-191,248-277)
@@ -429,6 +434,75 @@ int tspm_bn1d_bwd_pair(int32_t m, int32_t c0, const float* g0, const float* x0, 
  * (models/mmimdb.py:236-237). */
 int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float* targets, float* loss,
                     float* dlogits, float grad_scale, float threshold, float* stats, tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * MOSI UTT-Fusion (BASELINE configs[4]; ABI 12) — MML_Suite/models/msa/utt_fusion.py:25-200 with
+ * configs/mosi/centralised/utt_fusion_base_training.yaml.  Sequences are time-major on the device:
+ * row (t, b) of a [T][B][F] tensor.
+ * ----------------------------------------------------------------------------------------------*/
+/* nn.LSTM(input, hidden, batch_first=True), one layer, zero initial state, embd_method "last"
+ * (models/msa/networks/lstm.py:8-67; the reference runs the padded length, no packing).  xg = x W_ih^T
+ * + b_ih for all steps (a tspm_linear_fwd over the T*B rows); the recurrence adds h W_hh^T + b_hh.
+ * Saved for the backward: activated gates i,f,g,o [T][B][4H], c_t [T][B][H], h_t [T+1][B][H]
+ * (hs[0] = h0 = 0).  h_T goes to h_out (row stride ld_out).  hidden must be 64 and batch even. */
+typedef struct tspm_lstm_fwd_desc {
+  int32_t batch, steps, hidden, ld_out;
+  const float* xg;
+  const float* w_hh;
+  const float* b_hh; /* nullable */
+  float* gates;
+  float* cs;
+  float* hs;
+  float* h_out;
+} tspm_lstm_fwd_desc;
+/* 1 or 2 independent LSTMs (the audio and video encoders) in one launch. */
+int tspm_lstm_fwd(int32_t count, const tspm_lstm_fwd_desc* descs, tspm_stream_t stream);
+/* Backward through time from dh (the gradient of h_T, row stride ld_dh): writes the pre-activation
+ * gate gradients dgates [T][B][4H].  The weight gradients are then GEMMs over the T*B rows:
+ * dW_hh = dgates^T hs[0:T], dW_ih = dgates^T x, db_hh = db_ih = column sums of dgates. */
+typedef struct tspm_lstm_bwd_desc {
+  int32_t batch, steps, hidden, ld_dh;
+  const float* w_hh;
+  const float* gates;
+  const float* cs;
+  const float* dh;
+  float* dgates;
+} tspm_lstm_bwd_desc;
+int tspm_lstm_bwd(int32_t count, const tspm_lstm_bwd_desc* descs, tspm_stream_t stream);
+/* TextCNN pooling (models/msa/networks/textcnn.py:56-67): for conv i (kernel height heights[i], output
+ * conv_out[i] time-major [steps-heights[i]+1][batch][channels] without bias), bias[i] added, ReLU,
+ * max over time (first maximum, F.max_pool1d), concatenated over convs: pooled[b][i*C+c] and the
+ * argmax time index; out[b*ld_out + i*C+c] = pooled * (keep ? keep*keep_scale : 1) — the dropout before
+ * the embedding Linear (keep uint8 [batch][nconv*C], nullable).  nconv <= 4, steps <= 256. */
+int tspm_textcnn_pool_fwd(int32_t batch, int32_t steps, int32_t nconv, const int32_t* heights,
+                          int32_t channels, const float* const* conv_out, const float* const* bias,
+                          const uint8_t* keep, float keep_scale, float* pooled, uint8_t* argmax,
+                          float* out, int32_t ld_out, tspm_stream_t stream);
+/* TextCNN backward from dout (gradient of the embedding Linear's input, row stride ld_dout): through the
+ * dropout and the ReLU at the argmax; conv weight gradients dw[i] ([C][heights[i]][feat], the
+ * nn.Conv2d(1, C, (h, feat)) weight layout) and bias gradients db[i] (nullable) from the argmax rows
+ * only (the time-max passes gradient to one position per (b, c)): dw[c][dt][f] = sum_b g[b][c]
+ * x[arg[b][c] + dt][b][f].  x is the time-major text input [steps][batch][feat] (feat <= 1024,
+ * heights <= 5); g_work holds batch*nconv*channels floats. */
+int tspm_textcnn_bwd(int32_t batch, int32_t steps, int32_t feat, int32_t nconv, const int32_t* heights,
+                     int32_t channels, const float* x, const float* dout, int32_t ld_dout, const uint8_t* keep,
+                     float keep_scale, const float* pooled, const uint8_t* argmax, float* const* dw,
+                     float* const* db, float* g_work, tspm_stream_t stream);
+/* clip_grad_norm_(parameters, max_norm) coefficient (utt_fusion.py:189): total = ||grad * grad_scale||_2
+ * (squares summed in double, fixed order), *coef = min(1, max_norm / (total + 1e-6)) for
+ * tspm_adam_step_clip; *total_norm (nullable) = total.  workspace: tspm_grad_clip_workspace() bytes. */
+size_t tspm_grad_clip_workspace(void);
+int tspm_grad_clip_coef(int64_t count, const float* grad, float grad_scale, float max_norm, float* coef,
+                        float* total_norm, void* workspace, size_t workspace_bytes, tspm_stream_t stream);
+/* Padded batch assembly (data/mosi.py:202-232 pad_sequence + the step's .to(device)) from a ragged
+ * corpus data[rows][feat] (sample s = rows offsets[s] .. offsets[s]+lengths[s]-1): out[t*stride_t +
+ * b*stride_b + f] = sample index[b]'s row t (0 past its length) * row_mask[b] (nullable), for
+ * t < steps_pad; labels_out[b] = labels[index[b]] (both nullable).  Out-of-range indices write NaN
+ * rows and label -1. */
+int tspm_seq_gather(int32_t count, const int64_t* index, int64_t n_samples, const float* data,
+                    const int64_t* offsets, const int32_t* lengths, int32_t feat, int32_t steps_pad, float* out,
+                    int64_t stride_t, int64_t stride_b, const float* row_mask, const int64_t* labels,
+                    int64_t* labels_out, tspm_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,29 +1,29 @@
-"""Accuracy after equal epochs, reference vs the HIP path, on a REAL-data AVMNIST subset
+"""Accuracy after equal epochs, reference vs the HIP path, on REAL AVMNIST data
 (BASELINE.json north star: "final accuracy within ±0.2 pp of the reference after equal epochs").
 
 The reference's split CSVs are absent (``$EXP_PATH/DATA`` is gitignored), so this
 script defines its own pairing of the reference's sample files (MML_Suite/AVMNIST/dataset): for each
 digit d, the k-th spectrogram of d (``{d}_{speaker}_{rep}.pt`` sorted by speaker, repetition) is paired
-with the k-th MNIST image labelled d (``{idx}_{idx}_{d}.pt`` sorted by idx).  Train = the first
-TRAIN_PER_DIGIT pairs of every digit, test = the next TEST_PER_DIGIT.  Files are read with the
-weights-only unpickler only (data.load_sample_file).
+with the k-th MNIST image labelled d (``{idx}_{idx}_{d}.pt`` sorted by idx).  All 3000 spectrograms of
+every digit are used: train = the first 2400 pairs (speakers 0-47), test = the last 600 (speakers
+48-59, unseen voices): 24,000 / 6,000 samples.  Files are read with the weights-only unpickler only.
 
-Both sides train the late-fusion model (ResNet18 audio + ResNet34 image + MLP head, dropout 0.5) from
-the seed-0 weights, batch 128 over the same sample order (torch.randperm, generator seeded per epoch),
-Adam lr 5e-4 / wd 1e-4, E epochs, and measure test accuracy (eval mode, pattern "ai",
-argmax of the softmax) after every epoch:
+Paired design: run ``s`` of each side starts from the weights ``torch.manual_seed(s)`` gives, reads the
+same batch order (torch.randperm seeded per run and epoch) and applies the SAME dropout keep-masks
+(seeded per run, epoch and batch; ``keep_override`` on our step, the oracle's keep mask on the
+reference); batch 128 (last batch 64), Adam lr 5e-4 / wd 1e-4, dropout 0.5, E epochs; test accuracy
+(eval mode, pattern "ai", argmax of the softmax) after every epoch.  The two runs of a pair differ only
+in how each implementation rounds in fp32, so the per-run difference of final test accuracies is the
+effect of the implementation; its mean over runs, with a t confidence interval, is the result.
 
-  reference — oracle/avmnist_ref.py on the CPU, i.e. the reference's AVMNIST.train_step (bit-exact to it
-              on CPU, tests/test_oracle_golden.py); its dropout masks come from torch.bernoulli
-  ours      — tspm_amd.FusedTrainStep / FusedEvalStep on the MI355X; dropout masks from the device RNG
+  reference — oracle/avmnist_ref.py on the CPU of the build container, i.e. the reference's
+              AVMNIST.train_step (bit-exact to it on CPU, tests/test_oracle_golden.py)
+  ours      — tspm_amd.FusedTrainStep / FusedEvalStep on the MI355X
 
-Dropout masks (and fp32 summation order) differ between the sides, so the trajectories are two
-independent training runs of the same recipe on the same data; the comparison is of their accuracy.
-
-  python scripts/accuracy_parity.py prepare                  # here: reference files -> data_cache/
-  python scripts/accuracy_parity.py reference --epochs 6     # here, CPU
-  python scripts/accuracy_parity.py ours --epochs 6          # GPU box
-  python scripts/accuracy_parity.py compare                  # -> profiles/r1_v7_accuracy_parity.json
+  python scripts/accuracy_parity.py prepare                               # here: files -> data_cache/
+  python scripts/accuracy_parity.py reference --epochs 20 --seeds 0,1,... # here, CPU
+  python scripts/accuracy_parity.py ours --epochs 20 --seeds 0,1,...      # GPU box
+  python scripts/accuracy_parity.py compare --out profiles/r2_accuracy_parity.json
 """
 from __future__ import annotations
 
@@ -40,9 +40,9 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 DATASET = "/root/reference/MML_Suite/AVMNIST/dataset"
-CACHE = os.path.join(REPO, "data_cache", "avmnist_real_subset")
+CACHE = os.path.join(REPO, "data_cache", "avmnist_real_pairs")
 OUT = os.path.join(REPO, "gpurun_out")
-TRAIN_PER_DIGIT, TEST_PER_DIGIT = 400, 100
+TRAIN_PER_DIGIT, TEST_PER_DIGIT = 2400, 600  # all 3000 spectrograms of every digit: speakers 0-47 / 48-59
 BATCH = 128
 
 
@@ -82,14 +82,19 @@ def _lut() -> np.ndarray:
     return default_lut()
 
 
-def _order(n: int, epoch: int) -> torch.Tensor:
-    return torch.randperm(n, generator=torch.Generator().manual_seed(1000 + epoch))
+def _order(n: int, epoch: int, seed: int = 0) -> torch.Tensor:
+    return torch.randperm(n, generator=torch.Generator().manual_seed(1000 * (seed + 1) + epoch))
+
+
+def _keep(seed: int, epoch: int, b: int, n: int) -> torch.Tensor:
+    """The dropout keep-mask of batch b of epoch `epoch` in run `seed` — the SAME on both sides."""
+    g = torch.Generator().manual_seed(((seed * 1000 + epoch) * 100003 + b) & 0x7FFFFFFF)
+    return (torch.rand(n, 128, generator=g) >= 0.5).to(torch.uint8)
 
 
 def reference(epochs: int, seed: int) -> None:
     from oracle import avmnist_eval_ref as eref
     from oracle import avmnist_ref as orc
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
     tr, te = _load()
     lut = torch.from_numpy(_lut().astype(np.int64))
 
@@ -97,18 +102,18 @@ def reference(epochs: int, seed: int) -> None:
         a = torch.from_numpy(np.asarray(c.audio[rows]))
         i = (lut[torch.from_numpy(np.asarray(c.image[rows])).long()].float() * (1.0 / 255.0)).unsqueeze(1)
         return a, i, torch.from_numpy(np.asarray(c.labels[rows]))
-    model = orc.build_oracle_avmnist(0)
+    model = orc.build_oracle_avmnist(seed)
     opt = orc.OracleAdam(list(model.parameters()), lr=5e-4, weight_decay=1e-4)
-    torch.manual_seed(seed)  # the dropout masks' RNG (weights stay the seed-0 ones)
     curve = []
     for ep in range(epochs):
         t0 = time.time()
-        order = _order(len(tr), ep).numpy()
+        order = _order(len(tr), ep, seed).numpy()
         losses = []
         model.train()
         for b in range(0, len(order), BATCH):
             a, i, lab = tensors(tr, order[b:b + BATCH])
-            losses.append(orc.train_step(model, opt, a, i, lab)["loss"].item())
+            keep = _keep(seed, ep, b // BATCH, lab.numel())
+            losses.append(orc.train_step(model, opt, a, i, lab, keep)["loss"].item())
         model.eval()
         correct = 0
         for b in range(0, len(te), BATCH):
@@ -120,7 +125,8 @@ def reference(epochs: int, seed: int) -> None:
         print(json.dumps(curve[-1]), flush=True)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, f"accuracy_reference_s{seed}.json"), "w") as f:
-        json.dump({"side": "reference (oracle on CPU)", "dropout_seed": seed, "curve": curve}, f, indent=1)
+        json.dump({"side": "reference (oracle on CPU)", "seed": seed, "threads": torch.get_num_threads(),
+                   "curve": curve}, f, indent=1)
 
 
 def ours(epochs: int, seed: int) -> None:
@@ -130,21 +136,21 @@ def ours(epochs: int, seed: int) -> None:
     dev = torch.device("cuda", 0)
     tr, te = _load()
     dtr, dte = DeviceCorpus(tr, dev), DeviceCorpus(te, dev)
-    torch.manual_seed(0)
+    torch.manual_seed(seed)  # the same initial weights as the reference side's run `seed`
     model = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
     opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
-    model._rng_seed = 7919 * (seed + 1)  # the device dropout RNG's key (weights stay the seed-0 ones)
     steps, evals = {}, {}
     curve = []
     for ep in range(epochs):
         t0 = time.time()
-        order = _order(len(tr), ep).to(dev)
+        order = _order(len(tr), ep, seed).to(dev)
         losses = []
         for b in range(0, len(tr), BATCH):
             idx = order[b:b + BATCH].contiguous()
             n = idx.numel()
             st = steps.get(n) or steps.setdefault(n, tspm_amd.FusedTrainStep(model, opt, None, n))
             dtr.gather(idx, out=(st.A, st.I, st.labels))
+            st.keep_override = _keep(seed, ep, b // BATCH, n).to(dev, non_blocking=True)
             st.run()
             losses.append(st.loss.clone())
         correct = torch.zeros((), dtype=torch.int64, device=dev)
@@ -161,54 +167,60 @@ def ours(epochs: int, seed: int) -> None:
         print(json.dumps(curve[-1]), flush=True)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, f"accuracy_ours_s{seed}.json"), "w") as f:
-        json.dump({"side": "ours (HIP path, MI355X)", "dropout_seed": seed, "curve": curve}, f, indent=1)
+        json.dump({"side": "ours (HIP path, MI355X)", "seed": seed, "curve": curve}, f, indent=1)
 
 
 def compare(out_path: str) -> None:
+    from scipy import stats
+
     def runs(side):
         out = {}
         for p in sorted(glob.glob(os.path.join(OUT, f"accuracy_{side}_s*.json"))):
             d = json.load(open(p))
-            out[d["dropout_seed"]] = d["curve"]
+            out[d["seed"]] = d["curve"]
         return out
     ref, our = runs("reference"), runs("ours")
-    n = min(min(len(c) for c in ref.values()), min(len(c) for c in our.values()))
+    seeds = sorted(set(ref) & set(our))
+    n = min(min(len(ref[s]) for s in seeds), min(len(our[s]) for s in seeds))
     rows = []
     for k in range(n):
-        ra = [c[k]["test_accuracy"] for c in ref.values()]
-        oa = [c[k]["test_accuracy"] for c in our.values()]
-        rows.append({"epoch": k + 1, "reference_test_accuracy": ra, "ours_test_accuracy": oa,
-                     "reference_mean": round(float(np.mean(ra)), 5), "ours_mean": round(float(np.mean(oa)), 5),
-                     "delta_mean_pp": round(100 * (float(np.mean(oa)) - float(np.mean(ra))), 2),
-                     "reference_train_loss": [round(c[k]["train_loss"], 5) for c in ref.values()],
-                     "ours_train_loss": [round(c[k]["train_loss"], 5) for c in our.values()]})
+        ra = np.array([ref[s][k]["test_accuracy"] for s in seeds])
+        oa = np.array([our[s][k]["test_accuracy"] for s in seeds])
+        rows.append({"epoch": k + 1, "reference_test_accuracy": ra.tolist(), "ours_test_accuracy": oa.tolist(),
+                     "reference_mean": round(float(ra.mean()), 5), "ours_mean": round(float(oa.mean()), 5),
+                     "delta_mean_pp": round(100 * float((oa - ra).mean()), 3),
+                     "reference_train_loss": [round(ref[s][k]["train_loss"], 5) for s in seeds],
+                     "ours_train_loss": [round(our[s][k]["train_loss"], 5) for s in seeds]})
+
+    def paired(a, b):
+        d = 100 * (np.asarray(a) - np.asarray(b))
+        m, se = float(d.mean()), float(d.std(ddof=1) / np.sqrt(len(d))) if len(d) > 1 else float("nan")
+        t = float(stats.t.ppf(0.975, len(d) - 1)) if len(d) > 1 else float("nan")
+        return {"delta_pp": round(m, 3), "stderr_pp": round(se, 3), "ci95_pp": [round(m - t * se, 3), round(m + t * se, 3)],
+                "within_0.2pp": bool(m - t * se >= -0.2 and m + t * se <= 0.2)}
     last = rows[-1]
-    doc = {"what": "late-fusion AVMNIST, real-data subset of the reference's sample files "
-                   f"({TRAIN_PER_DIGIT * 10} train / {TEST_PER_DIGIT * 10} test pairs, own pairing: the "
-                   "reference's split CSVs are absent), seed-0 weights, same batch order, batch 128, Adam "
-                   "5e-4 / 1e-4, dropout 0.5; one run per dropout seed and side (masks drawn independently)",
-           "reference_seeds": sorted(ref), "ours_seeds": sorted(our),
-           "test_samples": TEST_PER_DIGIT * 10, "one_sample_pp": round(100 / (TEST_PER_DIGIT * 10), 3),
+    fin_o, fin_r = last["ours_test_accuracy"], last["reference_test_accuracy"]
+    t3 = lambda c, s: float(np.mean([c[s][k]["test_accuracy"] for k in range(n - 3, n)]))  # noqa: E731
+    doc = {"what": "late-fusion AVMNIST on the reference's own sample files (24,000 train / 6,000 test pairs, "
+                   "speaker-disjoint test; own pairing — the reference's split CSVs are absent); paired runs: "
+                   "same initial weights (seed s), batch order and dropout masks on both sides; batch 128, "
+                   "Adam 5e-4 / 1e-4, dropout 0.5",
+           "seeds": seeds, "epochs_compared": n, "test_samples": TEST_PER_DIGIT * 10,
+           "one_sample_pp": round(100 / (TEST_PER_DIGIT * 10), 4),
+           "reference_published": {"test_accuracy_scratch_20ep": 0.9870, "source": "README.md:26-29 / "
+                                   "plots/avmnist/comparison/resnet/test_accuracy.png (their split, unknown hardware)"},
            "final": {"epoch": last["epoch"], "reference_mean": last["reference_mean"], "ours_mean": last["ours_mean"],
-                     "delta_mean_pp": last["delta_mean_pp"],
-                     "reference_seed_spread_pp": round(100 * (max(last["reference_test_accuracy"]) -
-                                                              min(last["reference_test_accuracy"])), 2),
-                     "ours_seed_spread_pp": round(100 * (max(last["ours_test_accuracy"]) -
-                                                         min(last["ours_test_accuracy"])), 2)},
+                     "reference_std_pp": round(100 * float(np.std(fin_r, ddof=1)), 3) if len(seeds) > 1 else None,
+                     "ours_std_pp": round(100 * float(np.std(fin_o, ddof=1)), 3) if len(seeds) > 1 else None,
+                     "paired": paired(fin_o, fin_r)},
+           "last3_epochs_mean": {"reference_mean": round(float(np.mean([t3(ref, s) for s in seeds])), 5),
+                                 "ours_mean": round(float(np.mean([t3(our, s) for s in seeds])), 5),
+                                 "paired": paired([t3(our, s) for s in seeds], [t3(ref, s) for s in seeds])},
            "epochs": rows}
-    # less noisy summary: per run, the mean test accuracy of the last 3 epochs; then mean and standard
-    # error over the runs of each side
-    def tail3(curves):
-        v = np.array([np.mean([c[k]["test_accuracy"] for k in range(n - 3, n)]) for c in curves.values()])
-        return float(v.mean()), float(v.std(ddof=1) / np.sqrt(len(v))) if len(v) > 1 else float("nan")
-    (rm, rse), (om, ose) = tail3(ref), tail3(our)
-    doc["last3_epochs"] = {"reference_mean": round(rm, 5), "reference_stderr": round(rse, 5), "ours_mean": round(om, 5),
-                           "ours_stderr": round(ose, 5), "delta_pp": round(100 * (om - rm), 2),
-                           "delta_stderr_pp": round(100 * float(np.hypot(rse, ose)), 2)}
     with open(out_path, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc["final"], indent=1))
-    print(json.dumps(doc["last3_epochs"], indent=1))
+    print(json.dumps(doc["last3_epochs_mean"], indent=1))
 
 
 def main() -> None:
@@ -216,11 +228,14 @@ def main() -> None:
     ap.add_argument("what", choices=["prepare", "reference", "ours", "compare"])
     ap.add_argument("--epochs", type=int, default=6)
     ap.add_argument("--seeds", default="0", help="comma-separated dropout seeds (one run each)")
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r1_v7_accuracy_parity.json"))
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r2_accuracy_parity.json"))
+    ap.add_argument("--threads", type=int, default=0, help="reference side: torch threads (0 = all)")
     a = ap.parse_args()
     if a.what == "prepare":
         prepare()
     elif a.what == "reference":
+        if a.threads:
+            torch.set_num_threads(a.threads)
         for sd in a.seeds.split(","):
             reference(a.epochs, int(sd))
     elif a.what == "ours":

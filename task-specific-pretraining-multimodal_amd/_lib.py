@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -66,6 +66,18 @@ class LinearBwdDesc(Structure):
 
 # name -> (restype, argtypes)
 _P = c_void_p
+class LstmFwdDesc(Structure):
+    """tspm_lstm_fwd_desc (ABI 12)."""
+    _fields_ = [(n, c_int32) for n in ("batch", "steps", "hidden", "ld_out")] + \
+        [(n, c_void_p) for n in ("xg", "w_hh", "b_hh", "gates", "cs", "hs", "h_out")]
+
+
+class LstmBwdDesc(Structure):
+    """tspm_lstm_bwd_desc (ABI 12)."""
+    _fields_ = [(n, c_int32) for n in ("batch", "steps", "hidden", "ld_dh")] + \
+        [(n, c_void_p) for n in ("w_hh", "gates", "cs", "dh", "dgates")]
+
+
 _SIGS = {
     "tspm_abi_version": (c_int32, []),
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
@@ -133,6 +145,18 @@ _SIGS = {
     "tspm_bn1d_bwd_pair": (c_int32, [c_int32] + ([c_int32] + [_P] * 8) * 2 + [_P]),
     "tspm_linear_fwd_pair": (c_int32, [c_int32, c_int32, c_int32] + [_P, c_int32, _P, _P, c_int32] * 2 + [_P]),
     "tspm_bce_logits": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, c_float, _P, _P]),
+    # ABI 12: MOSI UTT-Fusion
+    "tspm_adam_step_clip": (c_int32, [c_int64, _P, _P, _P, _P, _P, _P, _P]),
+    "tspm_lstm_fwd": (c_int32, [c_int32, POINTER(LstmFwdDesc), _P]),
+    "tspm_lstm_bwd": (c_int32, [c_int32, POINTER(LstmBwdDesc), _P]),
+    "tspm_textcnn_pool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, _P, c_float, _P, _P, _P,
+                                        c_int32, _P]),
+    "tspm_textcnn_bwd": (c_int32, [c_int32, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, c_float, _P,
+                                   _P, _P, _P, _P, _P]),
+    "tspm_grad_clip_workspace": (c_size_t, []),
+    "tspm_grad_clip_coef": (c_int32, [c_int64, _P, c_float, c_float, _P, _P, _P, c_size_t, _P]),
+    "tspm_seq_gather": (c_int32, [c_int32, _P, c_int64, _P, _P, _P, c_int32, c_int32, _P, c_int64, c_int64, _P, _P, _P,
+                                  _P]),
 }
 
 EXPORTED = tuple(_SIGS)

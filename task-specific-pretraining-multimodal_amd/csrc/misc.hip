@@ -341,7 +341,8 @@ __global__ void k_adam_begin(tspm_adam_hyper* h) { h->step += 1; }
 
 __global__ __launch_bounds__(256) void k_adam(long long count, float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
-                                              const tspm_adam_hyper* __restrict__ hp) {
+                                              const tspm_adam_hyper* __restrict__ hp,
+                                              const float* __restrict__ clip) {
   __shared__ float sh[8];
   if (threadIdx.x == 0) {
     const tspm_adam_hyper h = *hp;
@@ -359,8 +360,10 @@ __global__ __launch_bounds__(256) void k_adam(long long count, float* __restrict
   __syncthreads();
   const float step_size = sh[0], bc2s = sh[1], w1 = sh[2], b2 = sh[3], omb2 = sh[4], eps = sh[5], wd = sh[6],
               gs = sh[7];
+  const float cc = clip ? clip[0] : 1.f;
   auto upd = [&](float& pp, float gg, float& mm, float& vv) {
     gg = gg * gs;
+    if (clip) gg = gg * cc;
     if (wd != 0.f) gg = gg + wd * pp;
     mm = mm + w1 * (gg - mm);
     vv = vv * b2;
@@ -598,7 +601,20 @@ extern "C" int tspm_adam_step(int64_t count, float* param, const float* grad, fl
   long long blocks = cdiv64(count / 4 + 1, 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(k_adam, dim3((int)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)count, param,
-                     grad, exp_avg, exp_avg_sq, hyper);
+                     grad, exp_avg, exp_avg_sq, hyper, nullptr);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_adam_step_clip(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                                   const tspm_adam_hyper* hyper, const float* clip_coef, tspm_stream_t stream) {
+  if (count < 0 || !param || !grad || !exp_avg || !exp_avg_sq || !hyper || !clip_coef) return TSPM_ERR_INVALID;
+  if (!aligned16(param) || !aligned16(grad) || !aligned16(exp_avg) || !aligned16(exp_avg_sq)) return TSPM_ERR_INVALID;
+  if (count == 0) return TSPM_OK;
+  long long blocks = cdiv64(count / 4 + 1, 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_adam, dim3((int)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)count, param,
+                     grad, exp_avg, exp_avg_sq, hyper, clip_coef);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

@@ -13,7 +13,7 @@ format (``step`` / ``exp_avg`` / ``exp_avg_sq`` per parameter).
 from __future__ import annotations
 
 import ctypes
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 import torch
 
@@ -77,6 +77,9 @@ class FusedAdam(torch.optim.Optimizer):
                         foreach=None, capturable=False, differentiable=False, fused=None)
         super().__init__(params, defaults)
         self.grad_scale = float(grad_scale)
+        # device scalar multiplying every gradient in the update (the clip_grad_norm_ coefficient written
+        # by tspm_grad_clip_coef; None = no clip) — set by the MOSI step (utt_fusion.py:188-190)
+        self.clip_coef: Optional[torch.Tensor] = None
         self._flat: List[_FlatGroup] = []
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.requires_grad]
@@ -121,6 +124,11 @@ class FusedAdam(torch.optim.Optimizer):
         lib = L.lib()
         for fg in self.flat_groups():
             L.check(lib.tspm_adam_begin(fg.hyper.data_ptr(), stream_handle), "adam_begin")
+            if self.clip_coef is not None:
+                L.check(lib.tspm_adam_step_clip(fg.numel, fg.param.data_ptr(), fg.grad.data_ptr(), fg.exp_avg.data_ptr(),
+                                                fg.exp_avg_sq.data_ptr(), fg.hyper.data_ptr(),
+                                                self.clip_coef.data_ptr(), stream_handle), "adam_step_clip")
+                continue
             L.check(lib.tspm_adam_step(fg.numel, fg.param.data_ptr(), fg.grad.data_ptr(), fg.exp_avg.data_ptr(),
                                        fg.exp_avg_sq.data_ptr(), fg.hyper.data_ptr(), stream_handle), "adam_step")
 

@@ -30,14 +30,19 @@ from . import data
 from .modules import AVMNIST, ResNet18, ResNet34, ResNetEncoder
 from .optim import FusedAdam
 from . import mmimdb as _mm
+from . import mosi as _mosi
 
 TAGS = {"!ResNet18": ResNet18, "!ResNet34": ResNet34, "!ResNetEncoder": ResNetEncoder,
         # MMIMDb late-fusion path (config/yaml_constructors.py:126-142)
         "!MMIMDbModalityEncoder": _mm.MMIMDbModalityEncoder, "!MaxOut": _mm.MaxOut,
         "!GatedBiModalNetwork": _mm.GatedBiModalNetwork, "!MMIMDb": _mm.MMIMDb,
-        "!MLPGenreClassifier": _mm.MLPGenreClassifier}
-MODELS = {"avmnist": AVMNIST, "mmimdb": _mm.MMIMDb, "mmimdbmodalityencoder": _mm.MMIMDbModalityEncoder}
-ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder}
+        "!MLPGenreClassifier": _mm.MLPGenreClassifier,
+        # MOSI UTT-Fusion path (config/yaml_constructors.py:99-110)
+        "!LSTMEncoder": _mosi.LSTMEncoder, "!TextCNN": _mosi.TextCNN, "!FcClassifier": _mosi.FcClassifier}
+MODELS = {"avmnist": AVMNIST, "mmimdb": _mm.MMIMDb, "mmimdbmodalityencoder": _mm.MMIMDbModalityEncoder,
+          "utt-fusion": _mosi.UttFusionModel}  # config/resolvers.py:28-31
+ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder,
+            "lstmencoder": _mosi.LSTMEncoder, "textcnn": _mosi.TextCNN}
 OPTIMIZERS = {"adam": FusedAdam}
 DATASETS = {"avmnist": data.AVMNIST}
 

@@ -185,13 +185,28 @@ def adam_fp64(p0, g, step, lr=5e-4, wd=1e-4, b1=0.9, b2=0.999, eps=1e-8, m=None,
     return p0 - (lr / bc1) * m / (v.sqrt() / bc2 ** 0.5 + eps), m, v
 
 
-def check_adam(model, opt, p_before, m_before, v_before, step, lr=5e-4, wd=1e-4):
-    """The optimizer exactly: fp64 Adam applied to OUR gradient and OUR moments reproduces OUR update."""
+def adam_tolerance(p0, g, step, exp_v, lr, wd, b1=0.9, b2=0.999, eps=1e-8):
+    """Per-element bound for an fp32 Adam update against fp64: 1e-6 relative + 2e-9, plus the first-order
+    effect of rounding g' = g + wd*p in fp32 (4 ulps of |g| + |wd*p|) through the update
+    lr/bc1 * (1-b1) * dg' / (sqrt(v)/sqrt(bc2) + eps) — large only where g and wd*p nearly cancel, which
+    torch's fp32 Adam computes the same way (the value is ill-conditioned, not a kernel error)."""
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    dg = 4 * 2.0 ** -23 * (g.abs() + wd * p0.abs())
+    denom = exp_v.sqrt() / bc2 ** 0.5 + eps
+    return 2e-9 + lr / bc1 * (1 - b1) * dg / denom
+
+
+def check_adam(model, opt, p_before, m_before, v_before, step, lr=5e-4, wd=1e-4, coef=1.0):
+    """The optimizer exactly: fp64 Adam applied to OUR gradient (times the clip coefficient) and OUR
+    moments reproduces OUR update (adam_tolerance)."""
     for n, p in model.named_parameters():
-        exp, _, _ = adam_fp64(p_before[n], p.grad.detach().cpu(), step, lr=lr, wd=wd,
+        g = p.grad.detach().cpu().double() * coef
+        exp, _, v = adam_fp64(p_before[n], g, step, lr=lr, wd=wd,
                               m=None if m_before is None else m_before[n], v=None if v_before is None else v_before[n])
         got = p.detach().cpu().double()
-        assert ((got - exp).abs() <= 1e-6 * exp.abs() + 2e-9).all(), n
+        tol = 1e-6 * exp.abs() + adam_tolerance(p_before[n], g, step, v, lr, wd)
+        bad = (got - exp).abs() > tol
+        assert not bad.any(), (n, step, int(bad.sum()), ((got - exp).abs() / tol).max().item())
 
 
 def snapshot(model, opt=None):

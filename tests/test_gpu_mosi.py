@@ -1,0 +1,271 @@
+"""MOSI UTT-Fusion step (BASELINE configs[4]) on the HIP path against the CPU oracle (oracle/mosi_ref.py,
+pinned bit-exact to the real reference by tests/golden/make_mosi_golden.py / tests/test_mosi_cpu.py).
+
+Criterion as tests/test_gpu_model.py (tests/parity.py): the oracle in fp64 with our decisions forced
+into it — the TextCNN time-max argmax and the ReLU at it, the embedding and classifier ReLU masks, the
+dropout masks — is the truth; every forced decision that differs from fp64's own must be a near-tie
+(and rare); logits / loss rel-L2 <= 1e-4, every gradient rel-L2 <= 1e-3 and cosine >= 0.9999 and within
+4x the fp32 reference's error on the same decisions; no relaxed branch.  The clip coefficient
+(clip_grad_norm_ total) is checked against the fp64 gradients; Adam exactly (fp64 Adam applied to our
+clipped gradient and moments).  Every step is checked from our own state.
+"""
+import numpy as np
+import pytest
+import torch
+
+import tspm_amd
+from oracle import mosi_ref as orc
+from parity import (MAX_FLIP_FRAC, NEAR, Tally, check_adam, check_grad, check_out, pair_from, rel_l2, snapshot)
+from test_mosi_cpu import _dropin
+from tspm_amd import _lib as L
+from tspm_amd import mosi as M
+
+pytestmark = pytest.mark.gpu
+LR, WD = 1e-3, 1e-3
+
+
+def _decisions(eng):
+    C, d = eng.C, {}
+    for i in range(3):
+        d[f"text.pool{i}"] = eng.argmax[:, i * C:(i + 1) * C].long().cpu()
+        d[f"text.relu{i}"] = (eng.pooled[:, i * C:(i + 1) * C] > 0).cpu()
+    col = eng.m.netA.hidden_size + eng.m.netV.hidden_size
+    d["text.embd"] = (eng.fused[:, col:] > 0).cpu()
+    for j, h in enumerate(eng.h):
+        d[f"cls.relu{j}"] = (h > 0).cpu()
+    return d
+
+
+def _flips(t64, forced, keeps):
+    rep = {}
+    for site, f in forced.items():
+        if site.startswith("text.pool"):
+            conv = t64.pre[site].double().relu()
+            nat = t64.idx[site]
+            flip = f != nat
+            dist = (conv.gather(2, f.unsqueeze(2)) - conv.gather(2, nat.unsqueeze(2))).squeeze(2).abs()[flip]
+            x = conv
+        else:
+            x = t64.pre[site].double()
+            flip = f != (x > 0)
+            if site.startswith("cls.relu"):
+                flip &= keeps[f"cls{site[-1]}"].bool()
+            dist = x.abs()[flip]
+        rms = x.pow(2).mean().sqrt().item() or 1.0
+        nf = int(flip.sum())
+        worst = dist.max().item() / rms if nf else 0.0
+        assert worst <= NEAR, f"{site}: a flipped decision is {worst:.2e} x rms from its threshold / tie"
+        assert nf <= max(1, MAX_FLIP_FRAC * f.numel()), f"{site}: {nf} of {f.numel()} decisions flipped"
+        rep[site] = nf
+    return {k: v for k, v in rep.items() if v}
+
+
+def _forced(o32, o64, A, V, T, y, keeps, forced):
+    o32.clip = o64.clip = None  # raw gradients; the clip is checked through the total norm
+    t32, t64 = orc.MosiTrace(forced), orc.MosiTrace(forced)
+    r32 = orc.train_step(o32, None, A, V, T, y, keeps, t32)
+    r64 = orc.train_step(o64, None, A.double(), V.double(), T.double(), y, keeps, t64)
+    return r32, r64, t64
+
+
+def _check_step(ours, st, o32, o64, A, V, T, y, keeps, out, tally, ref32_logits=None, ref32_loss=None):
+    eng = st.eng
+    forced = _decisions(eng)
+    r32, r64, t64 = _forced(o32, o64, A, V, T, y, keeps, forced)
+    rep = _flips(t64, forced, keeps)
+    check_out("logits", out["logits"], r32["logits"] if ref32_logits is None else ref32_logits, r64["logits"], tally)
+    check_out("loss", out["loss"], (r32["loss"] if ref32_loss is None else ref32_loss).reshape(1),
+              r64["loss"].reshape(1), tally)
+    p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
+    for n, p in ours.named_parameters():
+        check_grad(f"grad {n}", p.grad, p32[n].grad, p64[n].grad, tally)
+    norm64 = torch.sqrt(sum((q.grad.double() ** 2).sum() for q in o64.parameters()))
+    norm32 = torch.sqrt(sum((q.grad.double() ** 2).sum() for q in o32.parameters()))
+    check_out("total grad norm", eng.total_norm, norm32.reshape(1), norm64.reshape(1), tally)
+    return rep
+
+
+def _check_adam(ours, opt, before, step, coef):
+    check_adam(ours, opt, *before, step, lr=LR, wd=WD, coef=coef)
+
+
+def _run_steps(gpu, batch, steps, clip, n_steps=3, seed=3, lengths=None, golden=None):
+    ours = _dropin(seed, clip=clip).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    if golden is not None:
+        A, V, T, y = (torch.from_numpy(golden[k]) for k in ("audio", "video", "text", "labels"))
+    else:
+        A, V, T, y = orc.synthetic_batch(batch, steps, seed=1234 + batch, lengths=lengths)
+    st = M.FusedMosiStep(ours, opt, None, batch, steps)
+    tally, coefs = Tally(), []
+    for s in range(n_steps):
+        if golden is not None:
+            keeps = {k: torch.from_numpy(golden[f"keep_{k}"][s]) for k in ("text", "cls0", "cls1", "cls2")}
+        else:
+            keeps = orc.keep_masks(batch, 50 + s)
+        o32, o64 = pair_from(ours, lambda: orc.build_oracle_utt(seed))
+        before = snapshot(ours, opt if s else None)
+        st.keep_override = {k: v.to(gpu) for k, v in keeps.items()}
+        out = st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        if golden is not None and s == 0:
+            rep = _check_step(ours, st, o32, o64, A, V, T, y, keeps, out, tally,
+                              torch.from_numpy(golden["logits"][0]), torch.tensor(float(golden["losses"][0])))
+            # the reference's clip total (its own fp32 gradients, un-forced decisions)
+            assert abs(st.eng.total_norm.item() - golden["total_norms"][0]) <= 1e-4 * golden["total_norms"][0]
+        else:
+            rep = _check_step(ours, st, o32, o64, A, V, T, y, keeps, out, tally)
+        coef = float(st.eng.clip_coef.item())
+        if clip is not None:
+            exp = min(1.0, clip / (st.eng.total_norm.item() + 1e-6))
+            assert abs(coef - exp) <= 1e-6 * exp
+        coefs.append(coef)
+        _check_adam(ours, opt, before, s + 1, coef if clip is not None else 1.0)
+        print(f"[B={batch} T={steps} step {s + 1}] flips {rep} clip coef {coef:.4f}")
+    print(tally)
+    return ours, st, coefs
+
+
+def test_fused_step_vs_golden_reference(gpu):
+    """Steps on the B=4 batch the real UttFusionModel.train_step ran (20 steps, two samples zero-padded
+    past their length, the reference's dropout masks), clip 1.0 as in the YAML."""
+    import os
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "mosi_step_b4.npz"), allow_pickle=False))
+    _run_steps(gpu, 4, 20, 1.0, seed=0, golden=g)
+
+
+@pytest.mark.parametrize("batch,steps,clip", [(32, 50, 1.0), (128, 50, 1.0), (64, 37, 0.05)])
+def test_fused_step_vs_oracle(gpu, batch, steps, clip):
+    """Full-size steps (aligned_50 length; an odd length; clip 0.05 so the coefficient is < 1 and the clip
+    acts), variable lengths zero-padded to the batch length as pad_sequence does."""
+    lengths = [steps - (i * 7) % (steps // 2) for i in range(batch)]
+    _, _, coefs = _run_steps(gpu, batch, steps, clip, lengths=lengths)
+    if clip == 0.05:
+        assert max(coefs) < 1.0
+
+
+def test_graph_replay_equals_eager(gpu):
+    res = []
+    for use_graph in (False, True):
+        ours = _dropin(7).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+        st = M.FusedMosiStep(ours, opt, None, 64, 50, use_graph=use_graph)
+        A, V, T, y = orc.synthetic_batch(64, 50, seed=5)
+        for s in range(4):
+            st.keep_override = {k: v.to(gpu) for k, v in orc.keep_masks(64, 90 + s).items()}
+            st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        res.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()]).cpu())
+    assert torch.equal(res[0], res[1])
+
+
+def test_lstm_bias_gradients_identical(gpu):
+    """b_ih.grad and b_hh.grad are the same column sums of the gate gradients (as in ATen): bitwise."""
+    ours = _dropin(1).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    st = M.FusedMosiStep(ours, opt, None, 32, 50)
+    A, V, T, y = orc.synthetic_batch(32, 50, seed=9)
+    st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
+    torch.cuda.synchronize()
+    for enc in (ours.netA, ours.netV):
+        assert torch.equal(enc.rnn.bias_ih_l0.grad, enc.rnn.bias_hh_l0.grad)
+
+
+def test_device_dropout_masks(gpu):
+    """Without keep_override the step draws fresh masks on the device every step (rate ~0.5)."""
+    ours = _dropin(2).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    st = M.FusedMosiStep(ours, opt, None, 64, 20)
+    A, V, T, y = orc.synthetic_batch(64, 20, seed=11)
+    masks = []
+    for _ in range(3):
+        st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
+        masks.append(st.eng.keep_all.clone())
+    torch.cuda.synchronize()
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    for m in masks:
+        assert abs(m.float().mean().item() - 0.5) < 0.02
+
+
+def test_train_step_api_fused_and_autograd(gpu):
+    """UttFusionModel.train_step with the reference's call signature: FusedAdam → the fused step; the
+    reference's own torch.optim.Adam + LossFunctionGroup → forward / backward / clip_grad_norm_ / step
+    through the autograd node (dropout off for a deterministic comparison of the two)."""
+    from types import SimpleNamespace
+
+    class Group(dict):
+        def __call__(self, x, y):
+            return {"total_loss": 0.0 + 1.0 * torch.nn.functional.cross_entropy(x, y)}
+
+    A, V, T, y = orc.synthetic_batch(16, 30, seed=21)
+    batch = {"audio": A, "video": V, "text": T, "label": y, "pattern_name": ["atv"] * 16}
+    res = {}
+    for kind in ("fused", "autograd"):
+        ours = _dropin(4).to(gpu)
+        ours.netT.dropout.p = 0.0
+        for mm in ours.netC.module:
+            if isinstance(mm, torch.nn.Dropout):
+                mm.p = 0.0
+        ours.netC.dropout_p = 0.0
+        opt = (tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD) if kind == "fused"
+               else torch.optim.Adam(ours.parameters(), lr=LR, weight_decay=WD))
+        r = ours.train_step(batch, opt, None if kind == "fused" else Group(), gpu, None)
+        assert set(r) == {"loss"}
+        assert (kind == "fused") == bool(ours._steps)
+        torch.cuda.synchronize()
+        res[kind] = (r["loss"], torch.cat([p.detach().reshape(-1) for p in ours.parameters()]).cpu())
+    assert abs(res["fused"][0] - res["autograd"][0]) <= 1e-6 * abs(res["fused"][0])
+    assert rel_l2(res["fused"][1], res["autograd"][1]) < 1e-6
+    o = orc.build_oracle_utt(4)
+    o.netT.p = 0.0
+    o.netC.p = 0.0
+    ro = orc.train_step(o, orc.OracleAdam(list(o.parameters()), lr=LR, weight_decay=WD), A, V, T, y)
+    assert abs(res["fused"][0] - ro["loss"].item()) <= 1e-4 * abs(ro["loss"].item())
+    _ = SimpleNamespace
+
+
+def test_validation_step_and_embeddings(gpu):
+    ours = _dropin(6).to(gpu)
+    o = orc.build_oracle_utt(6)
+    A, V, T, y = orc.synthetic_batch(48, 50, seed=31)
+    batch = {"audio": A, "video": V, "text": T, "label": y, "pattern_name": ["atv"] * 48}
+
+    class Rec:
+        calls = []
+
+        def update_group_all(self, group, predictions, targets, m_types):
+            self.calls.append((group, predictions, targets, m_types))
+    rec = Rec()
+    v = ours.validation_step(batch, None, gpu, rec, return_test_info=True)
+    r = orc.validation_step(o, A, V, T, y)
+    assert abs(v["loss"] - r["loss"].item()) <= 1e-4 * abs(r["loss"].item())
+    eng = ours._engine(48, 50, gpu)
+    check_out("eval logits", eng.logits, None, orc.validation_step(o.double(), A.double(), V.double(), T.double(),
+                                                                   y)["logits"])
+    assert rec.calls and rec.calls[0][0] == "classification"
+    emb = ours.netA(A.to(gpu))  # the standalone encoder embedding equals the model's audio columns
+    assert rel_l2(emb, eng.fused[:, :64]) < 1e-6
+
+
+def test_seq_gather_pads_like_pad_sequence(gpu):
+    """tspm_seq_gather: ragged corpus rows → a zero-padded time-major batch, masks and labels —
+    pad_sequence(batch_first) semantics (data/mosi.py:225-230), transposed."""
+    rng = np.random.default_rng(0)
+    lens = rng.integers(3, 25, size=40).astype(np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    data = rng.standard_normal((int(lens.sum()), 7)).astype(np.float32)
+    labels = rng.integers(0, 3, size=40).astype(np.int64)
+    idx = torch.tensor([5, 0, 39, 17, 5, 22], dtype=torch.int64)
+    tpad = int(lens[idx.numpy()].max())
+    mask = torch.tensor([1, 0, 1, 1, 0, 1], dtype=torch.float32)
+    dd = [torch.from_numpy(a).to(gpu) for a in (idx.numpy(), data, offs, lens, mask.numpy(), labels)]  # kept alive
+    out = torch.empty(tpad, 6, 7, device=gpu)
+    lab = torch.empty(6, dtype=torch.int64, device=gpu)
+    L.check(L.lib().tspm_seq_gather(6, dd[0].data_ptr(), 40, dd[1].data_ptr(), dd[2].data_ptr(), dd[3].data_ptr(), 7,
+                                    tpad, out.data_ptr(), 6 * 7, 7, dd[4].data_ptr(), dd[5].data_ptr(), lab.data_ptr(),
+                                    L.stream_handle()), "seq_gather")
+    seqs = [torch.from_numpy(data[offs[i]:offs[i] + lens[i]]) for i in idx.numpy()]
+    ref = torch.nn.utils.rnn.pad_sequence(seqs, batch_first=True) * mask[:, None, None]
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu().transpose(0, 1), ref)
+    assert torch.equal(lab.cpu(), torch.from_numpy(labels[idx.numpy()]))

@@ -1,0 +1,100 @@
+"""MOSI UTT-Fusion (BASELINE configs[4]) checks that need no GPU: the CPU oracle against the vectors
+captured from the REAL reference (tests/golden/make_mosi_golden.py → mosi_step_b4.npz, bit-exact),
+and the drop-in modules' constructor signatures, seeded initialisation and state_dict layout."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import tspm_amd
+from oracle import mosi_ref as orc
+from tspm_amd import mosi as M
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "mosi_step_b4.npz")
+
+
+@pytest.fixture(scope="module")
+def mg():
+    return dict(np.load(GOLDEN, allow_pickle=False))
+
+
+def _dropin(seed=0, clip=1.0):
+    torch.manual_seed(seed)
+    a = M.LSTMEncoder(input_size=5, hidden_size=64, embd_method="last")
+    v = M.LSTMEncoder(input_size=20, hidden_size=64, embd_method="last")
+    t = M.TextCNN(input_size=768, embd_size=64, dropout=0.5, in_channels=1, out_channels=128, kernel_heights=[3, 4, 5])
+    c = M.FcClassifier(input_dim=192, layers=[192, 64, 32], output_dim=3, dropout=0.5)
+    return M.UttFusionModel(a, v, t, c, clip=clip)
+
+
+def test_oracle_reproduces_reference_train_steps_bitwise(mg):
+    """3 train steps of oracle/mosi_ref.py equal the real UttFusionModel.train_step bit for bit (same
+    seed-0 weights, inputs with zero padding, the reference's own dropout masks): logits, losses, the
+    clip_grad_norm_ totals, step-1 gradients (after the clip) and the parameters after every step.
+    (4 intra-op threads, as when the vectors were made: ATen's CPU reductions depend on the split.)"""
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    try:
+        _replay(mg)
+    finally:
+        torch.set_num_threads(nt)
+
+
+def _replay(mg):
+    model = orc.build_oracle_utt(0)
+    assert list(model.state_dict()) == list(mg["state_dict_keys"])
+    opt = orc.OracleAdam(list(model.parameters()), lr=1e-3, weight_decay=1e-3)
+    A, V, T, y = (torch.from_numpy(mg[k]) for k in ("audio", "video", "text", "labels"))
+    for s in range(3):
+        keeps = {k: torch.from_numpy(mg[f"keep_{k}"][s]) for k in ("text", "cls0", "cls1", "cls2")}
+        r = orc.train_step(model, opt, A, V, T, y, keeps)
+        assert torch.equal(r["logits"], torch.from_numpy(mg["logits"][s])), s
+        assert r["loss"].item() == mg["losses"][s], s
+        assert float(r["total_norm"]) == mg["total_norms"][s], s
+        if s == 0:
+            gn = np.array([p.grad.double().norm().item() for p in model.parameters()])
+            np.testing.assert_array_equal(gn, mg["grad_norm_step1"])
+        ps = np.array([p.detach().double().sum().item() for p in model.parameters()])
+        np.testing.assert_array_equal(ps, mg["param_sums"][s])
+    model.eval()
+    with torch.no_grad():
+        ev = orc.forward(model, A, V, T, False)
+    assert torch.equal(ev, torch.from_numpy(mg["eval_logits"]))
+
+
+def test_dropin_state_dict_and_seeded_init_equal_reference(mg):
+    ours, ref = _dropin(0), orc.build_oracle_utt(0)
+    sd, rsd = ours.state_dict(), ref.state_dict()
+    assert list(sd) == list(rsd) == list(mg["state_dict_keys"])
+    for k in sd:
+        assert torch.equal(sd[k], rsd[k]), k
+    assert [n for n, _ in ours.named_parameters()] == list(mg["param_names"])
+
+
+def test_dropin_api_surface():
+    m = _dropin(0)
+    assert m.get_encoder("audio") is m.netA and m.get_encoder("video") is m.netV and m.get_encoder("text") is m.netT
+    assert m.netA.hidden_size == 64 and m.netT.hidden_size == 64 and m.clip == 1.0
+    with pytest.raises(NotImplementedError):
+        M.LSTMEncoder(5, 64, embd_method="attention")
+    with pytest.raises(NotImplementedError):
+        M.FcClassifier(192, [64], 3, use_bn=True)
+    m.flatten_parameters()
+    with pytest.raises(tspm_amd._lib.TspmError):  # no CPU fallback
+        m.eval()
+        m(torch.zeros(2, 8, 5), torch.zeros(2, 8, 20), torch.zeros(2, 8, 768))
+
+
+def test_yaml_tags_build_dropins():
+    import yaml
+    tspm_amd.plugin.register_yaml()
+    doc = yaml.safe_load("""
+netA: !LSTMEncoder {input_size: 5, hidden_size: 64, embd_method: "last"}
+netT: !TextCNN {input_size: 768, embd_size: 64, dropout: 0.5, in_channels: 1, out_channels: 128,
+                kernel_heights: [3, 4, 5]}
+netC: !FcClassifier {input_dim: 192, layers: [192, 64, 32], output_dim: 3, dropout: 0.5}
+""")
+    assert isinstance(doc["netA"], M.LSTMEncoder) and isinstance(doc["netT"], M.TextCNN)
+    assert isinstance(doc["netC"], M.FcClassifier)
+    assert tspm_amd.plugin.MODELS["utt-fusion"] is M.UttFusionModel
