@@ -9,9 +9,9 @@ all in fp32 on the libtspm HIP kernels (graph-replayed).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including:
   roofline     — the conv implicit-GEMM kernel family (dominant: ~90 % of step FLOPs): valid-tap
-                 FLOPs of every conv launch of one step ÷ the summed device time of those launches,
-                 timed with HIP events in an instrumented eager step run right after the timed
-                 region with every launch on one stream (no concurrent kernels inside a bracket); peak = fp32 MFMA 157.3 TF/s.
+                 FLOPs of every conv launch of one step ÷ the summed DEVICE duration of those kernels
+                 (torch.profiler = rocprofiler timestamps) over replays of the step re-captured on one
+                 stream after the timed region; peak = fp32 MFMA 157.3 TF/s.
   cpu_baseline — the oracle (CPU fp32 restatement of the reference train step, bit-identical to it
                  on CPU) timed on this host at batch 128, rank 0 / N=1 only.
 """
@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -574,9 +575,16 @@ def mono_bench(args) -> None:
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     value = args.steps * B / el
-    # roofline: device kernel durations of further graph replays (outside the timed region)
-    roof = conv_roofline([("audio", op, kind) for op, kind in rec.launches], lambda: (next(f), st.run()),
-                         args.profile_steps) if args.profile_steps > 0 else None
+    # roofline: device kernel durations of further graph replays (outside the timed region); the graph
+    # is re-captured once with a recorder on the engine so every conv launch maps to its shape
+    roof = None
+    if args.profile_steps > 0:
+        seq = []
+        st.graph, st.eng.conv_timer = None, _EngineRecorder("audio", seq)
+        next(f)
+        st.run()
+        st.eng.conv_timer = None
+        roof = conv_roofline(seq, lambda: (next(f), st.run()), args.profile_steps)
     achieved = roof["achieved"] if roof else float("nan")
     conv_ms = roof["conv_kernel_ms_per_step"] if roof else float("nan")
     conv_flops = roof["valid_tap_flop_per_step"] if roof else None
@@ -619,6 +627,145 @@ def mono_bench(args) -> None:
     print(json.dumps(res), flush=True)
 
 
+def _mosi_family(name: str) -> str:
+    from tspm_amd.roofline import CONV_KERNEL
+    for key, fam in (("k_lstm_fwd", "lstm_fwd"), ("k_lstm_bwd", "lstm_bwd"), ("k_textcnn", "textcnn_pool_wgrad"),
+                     ("k_seq_gather", "seq_gather"), ("k_adam", "adam"), ("k_sumsq", "clip"), ("k_clip", "clip")):
+        if key in name:
+            return fam
+    if CONV_KERNEL.search(name):
+        return "textcnn_conv"
+    return "gemm_other"
+
+
+def mosi_bench(args) -> None:
+    """--mosi: BASELINE.json configs[4] — the MOSI UTT-Fusion train step (models/msa/utt_fusion.py:151-200 with
+    configs/mosi/centralised/utt_fusion_base_training.yaml: LSTM audio 5→64 and video 20→64, TextCNN over
+    768-d text, FcClassifier 192→192/64/32→3, CE, clip_grad_norm_ 1.0, Adam) at per-rank batch --mosi-batch
+    as one FusedMosiStep graph replay per step.  Input stage in the step: a ragged synthetic MOSI corpus
+    (lengths uniform in [20, 50]) resident in HBM, each batch padded to the aligned length 50 and gathered
+    time-major straight into the step's inputs (3 tspm_seq_gather launches; 'atv' training pattern).
+    Roofline: the TextCNN convolution (the step's FLOP-dominant kernel, implicit GEMM on MFMA) from device
+    kernel durations of graph replays after the timed region; the LSTM recurrences are latency-bound
+    (T=50 dependent steps) and reported by time."""
+    import tspm_amd
+    from tspm_amd import ddp
+    from tspm_amd import mosi as M
+    from tspm_amd.mosi_data import MOSI, synthetic_mosi_corpus
+    from tspm_amd.roofline import CONV_KERNEL, FP32_MFMA_PEAK_TFLOPS, device_kernels
+    rank, world, local = ddp.init_from_env("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, T = args.mosi_batch, 50
+    torch.manual_seed(0)
+    netA = M.LSTMEncoder(input_size=5, hidden_size=64, embd_method="last")
+    netV = M.LSTMEncoder(input_size=20, hidden_size=64, embd_method="last")
+    netT = M.TextCNN(input_size=768, embd_size=64, dropout=0.5, in_channels=1, out_channels=128, kernel_heights=[3, 4, 5])
+    netC = M.FcClassifier(input_dim=192, layers=[192, 64, 32], output_dim=3, dropout=0.5)
+    model = M.UttFusionModel(netA, netV, netT, netC, clip=1.0).to(dev)
+    opt = tspm_amd.FusedAdam(model.parameters(), lr=1e-3, weight_decay=1e-3, grad_scale=1.0 / world)
+    st = model.fused_step(opt, None, B, T)  # None: the config's single cross-entropy term, weight 1.0
+    if world > 1:  # data parallel: one RCCL all-reduce of the flat gradient buffer per step, then clip + Adam
+        for fg in opt.flat_groups():
+            dist.broadcast(fg.param, src=0)
+        st.allreduce = ddp.GradAllReduce([fg.grad for fg in opt.flat_groups()])
+    ds = MOSI(split="train", corpus=synthetic_mosi_corpus(args.mosi_corpus, 1234 + rank, T, min_len=20),
+              selected_patterns=["atv"], device=dev, seed=rank)
+    ds.device_corpus  # upload once, outside the timed region
+    gen = torch.Generator().manual_seed(1234 + rank)
+
+    def feed():
+        while True:
+            yield from ds.device_loader(B, shuffle=True, drop_last=True, generator=gen,
+                                        step_for=lambda b, t: st, pad_to=T)
+    f = feed()
+
+    def one():
+        next(f)
+        st.run()
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    value = args.steps * B * world / el
+    heights, C, Ft = netT.heights, netT.out_channels, netT.input_size
+    conv_flops = sum(2 * B * (T - h + 1) * h * Ft * C for h in heights)  # valid MACs x 2, one launch per height
+    roof = {"bound": "mfma", "kernel": "TextCNN convolutions: (h x 768) kernels over [B, T, 768] as implicit GEMM "
+                                       "(LDS-staged MFMA 32x32x2 fp32), 3 launches per step",
+            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
+            "flop_per_step": conv_flops, "achieved": None, "frac": None}
+    if args.profile_steps > 0 and world == 1:
+        R = args.profile_steps
+        ks = device_kernels(one, R)
+        fams, names = {}, {}
+        for k in ks:
+            fam = _mosi_family(k["name"])
+            fams[fam] = fams.get(fam, 0.0) + k["dur"] / R / 1e3
+            mt = re.search(r"\b(k_\w+|at::native::\w+|\w*[Kk]ernel\w*)", k["name"])
+            nm = mt.group(1) if mt else k["name"][:60]
+            cnt, ms = names.get(nm, (0, 0.0))
+            names[nm] = (cnt + 1, ms + k["dur"] / R / 1e3)
+        conv = [k for k in ks if CONV_KERNEL.search(k["name"]) and "k_textcnn" not in k["name"]]
+        conv_us = sum(k["dur"] for k in conv) / R
+        ach = conv_flops / (conv_us * 1e-6) / 1e12 if conv_us else None
+        roof.update({"achieved": round(ach, 3) if ach else None,
+                     "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4) if ach else None,
+                     "conv_ms_per_step": round(conv_us / 1e3, 4), "conv_launches_per_step": len(conv) / R,
+                     "kernels_per_step": len(ks) / R, "kernel_ms_per_step": round(sum(k["dur"] for k in ks) / R / 1e3, 4),
+                     "kernel_ms_per_step_by_family": {k: round(v, 4) for k, v in sorted(fams.items())},
+                     "kernels_by_name": {k: [round(v[0] / R, 2), round(v[1], 4)] for k, v in
+                                         sorted(names.items(), key=lambda kv: -kv[1][1])},
+                     "timing": f"device kernel durations (torch.profiler = rocprofiler timestamps) of {R} graph "
+                               "replays after the timed region (one stream)"})
+    res = {"metric": "samples/sec MOSI UTT-Fusion (LSTM audio/video + TextCNN text + FcClassifier) train step "
+                     "(BASELINE.json configs[4])",
+           "value": round(value, 2), "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32",
+           "data": f"synthetic MOSI-shaped ragged corpus of {args.mosi_corpus} samples (audio 5-d, video 20-d, text "
+                   "768-d, lengths U[20,50]) resident in HBM, padded to 50 and gathered on device each step; random-"
+                   "init weights (seed 0)",
+           "config": {"workload": "mosi_utt_fusion_train_step(lstm x2, textcnn, fc classifier, CE, clip 1.0, Adam)",
+                      "per_rank_batch": B, "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                      "params": sum(p.numel() for p in model.parameters())},
+           "roofline": roof, "final_loss": round(st.eng.loss.item(), 5)}
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
+        from oracle import mosi_ref as mref
+        from oracle.avmnist_ref import OracleAdam
+        threads, hcpu = cpu_threads()
+        torch.set_num_threads(threads)
+        ref = mref.build_oracle_utt(0)
+        ropt = OracleAdam(list(ref.parameters()), lr=1e-3, weight_decay=1e-3)
+        A, V, X, y = mref.synthetic_batch(B, T, seed=1234)
+        mref.train_step(ref, ropt, A, V, X, y)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_budget and n < 500:
+            mref.train_step(ref, ropt, A, V, X, y)
+            n += 1
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n * B / el, 1), "unit": "samples/sec", "cores": threads,
+                               "cpu_model": hcpu["model"], "host_cpus": hcpu, "kind": "port",
+                               "sample": f"{n} oracle UTT-Fusion train steps (fwd+CE+bwd+clip+Adam, fp32; bit-identical "
+                                         f"to the reference on CPU) at batch {B}, T={T}, {el:.1f}s, "
+                                         f"torch.set_num_threads({threads})"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -641,6 +788,9 @@ def main() -> None:
     ap.add_argument("--mono-batch", type=int, default=256)
     ap.add_argument("--mmimdb", action="store_true", help="BASELINE configs[3]: MMIMDb late-fusion step (one JSON line)")
     ap.add_argument("--mmimdb-batch", type=int, default=256)
+    ap.add_argument("--mosi", action="store_true", help="BASELINE configs[4]: MOSI UTT-Fusion step (one JSON line)")
+    ap.add_argument("--mosi-batch", type=int, default=128)
+    ap.add_argument("--mosi-corpus", type=int, default=4096, help="samples in the HBM-resident MOSI corpus")
     ap.add_argument("--profile-steps", type=int, default=10,
                     help="step replays profiled after the timed region for the roofline (0: skip)")
     ap.add_argument("--pcie-steps", type=int, default=20,
@@ -655,6 +805,9 @@ def main() -> None:
         return
     if args.mmimdb:
         mmimdb_bench(args)
+        return
+    if args.mosi:
+        mosi_bench(args)
         return
     if args.eval:
         eval_bench(args)

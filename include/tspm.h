@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 12
+#define TSPM_ABI_VERSION 13
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -262,6 +262,16 @@ int tspm_linear_bwd_data(int32_t n, int32_t in, int32_t out, const float* dy, in
 /* dw = dy^T @ x, db = sum_n dy (both overwritten). */
 int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx,
                            const float* dy, int32_t ldy, float* dw, float* db, tspm_stream_t stream);
+/* tspm_linear_bwd_weight with the reduction over the n rows split into `splits` workgroup slices
+ * (ABI 13): for very long reductions with few output tiles (the LSTM weight gradients of the MOSI
+ * step, n = T*B = 6400 rows into 256 x 64 / 256 x 5 / 256 x 20 outputs).  Per-slice partial products
+ * and row sums go to the workspace (tspm_linear_bwd_weight_splitk_workspace bytes; 0 = no split), a
+ * second launch sums the slices in order.  Same results as tspm_linear_bwd_weight up to summation
+ * order; dw and db from the same call share one split (an LSTM's db_ih / db_hh stay bitwise equal). */
+int tspm_linear_bwd_weight_splitk(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx, const float* dy,
+                                  int32_t ldy, float* dw, float* db, int32_t splits, void* workspace,
+                                  size_t workspace_bytes, tspm_stream_t stream);
+size_t tspm_linear_bwd_weight_splitk_workspace(int32_t n, int32_t in, int32_t out, int32_t splits);
 /* Both backward products of one nn.Linear in ONE launch (ABI 11): dw = dy^T @ x, db = sum_n dy
  * (db nullable), and, if dx != NULL, dx = dy @ w (row stride lddx) — bitwise the results of
  * tspm_linear_bwd_weight + tspm_linear_bwd_data (same per-product reduction split). */

@@ -1,0 +1,107 @@
+"""Tile search for the MOSI TextCNN convolutions (the (h x 768) kernels over [B, T, 768], as 1-D convs with
+768 input channels on the LDS-staged implicit-GEMM kernel): every supported variant-1 configuration
+including split-K, checked against the default configuration's output (max |diff| <= 1e-5 x max |y|),
+timed as HIP-graph replays; the fastest per shape goes to a table the engine loads at plan time.
+
+    python scripts/tune_textcnn.py --batch 128 --steps 50 --out task-specific-pretraining-multimodal_amd/tuned/mi355x_mosi_b128.json
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.dirname(HERE), HERE]
+from tspm_amd import _lib as L  # noqa: E402
+from tune_convs import LDS_SPLITS, LDS_TILES, LDS_WAVES, graph_time  # noqa: E402
+
+
+def candidates(s):
+    for tm, tn in LDS_TILES:
+        for wn, wk in LDS_WAVES:
+            wm = 4 // (wn * wk)
+            bm, bn = wm * tm * 32, wn * tn * 32
+            if s.c % 32 or s.n % bm:
+                continue
+            wgs = (s.p * s.q * s.n // bm) * -(-s.k // bn)
+            for sp in LDS_SPLITS:
+                if sp > 1 and wgs * sp > 4096:
+                    break
+                yield (tm, tn, wn, wk, sp, 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--feat", type=int, default=768)
+    ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--heights", default="3,4,5")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    lib = L.lib()
+    B, T, F, C = args.batch, args.steps, args.feat, args.channels
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(T * B * F, generator=g).to(dev)
+    entries = []
+    for h in [int(v) for v in args.heights.split(",")]:
+        s = L.ConvShape(B, T, 1, F, C, h, 1, 1, 0, T - h + 1, 1)
+        w = (torch.randn(C * h * F, generator=g) * 0.03).to(dev)
+        y = torch.empty((T - h + 1) * B * C, device=dev)
+        ws = [torch.zeros(256, dtype=torch.uint8, device=dev)]
+
+        def make(algo):
+            a = L.ConvAlgo(*algo)
+            need = lib.tspm_conv_fwd_workspace(ctypes.byref(s), ctypes.byref(a))
+            if need > ws[0].numel():
+                ws[0] = torch.zeros(need, dtype=torch.uint8, device=dev)
+            buf = ws[0]
+
+            def f():
+                return lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x.data_ptr(), None, w.data_ptr(), y.data_ptr(),
+                                         None, buf.data_ptr(), buf.numel(), L.stream_handle())
+            return f
+        base = (1, 2, 2, 1, 1, 1) if B % 64 == 0 else (0, 0, 0, 0, 0, 0)  # mosi._conv_algo
+        if make(base)() != 0:
+            raise SystemExit(f"default algo failed for h={h}")
+        torch.cuda.synchronize()
+        ref = y.clone()
+        scale = float(ref.abs().max())
+        t_base = graph_time(lambda: make(base), args.reps, args.iters)
+        best = (t_base, base)
+        for algo in candidates(s):
+            y.fill_(float("nan"))
+            if make(algo)() != 0:
+                continue
+            torch.cuda.synchronize()
+            err = float((y - ref).abs().max())
+            if not err <= 1e-5 * scale:
+                print(f"  MISMATCH h={h} {algo} err={err:.3e}", flush=True)
+                continue
+            t = graph_time(lambda: make(algo), args.reps, args.iters)
+            if t is not None and t < best[0]:
+                best = (t, algo)
+        t_best = graph_time(lambda: make(best[1]), args.reps, 4 * args.iters)
+        fl = 2 * B * (T - h + 1) * h * F * C
+        print(f"h={h}: default {t_base:7.2f} us  best {t_best:7.2f} us {best[1]}  "
+              f"({fl / (t_best * 1e-6) / 1e12:.1f} TFLOP/s)", flush=True)
+        if best[1] != base:
+            entries.append({"kind": "fwd", "shape": [s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad],
+                            "algo": list(best[1]), "us": round(t_best, 2), "base_us": round(t_base, 2), "count": 1})
+    if args.out:
+        with open(args.out, "w") as fh:
+            json.dump({"device": torch.cuda.get_device_name(0), "batch": B, "timing": "hip-graph replay",
+                       "what": "MOSI TextCNN convolutions (scripts/tune_textcnn.py)", "entries": entries}, fh, indent=1)
+        print("wrote", args.out)
+
+
+if __name__ == "__main__":
+    main()

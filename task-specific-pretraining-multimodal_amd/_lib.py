@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -120,6 +120,9 @@ _SIGS = {
     "tspm_linear_bwd_multi": (c_int32, [c_int32, POINTER(LinearBwdDesc), _P]),
     "tspm_linear_bwd_data": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P]),
     "tspm_linear_bwd_weight": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P]),
+    "tspm_linear_bwd_weight_splitk": (c_int32, [c_int32, c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, c_int32,
+                                                _P, c_size_t, _P]),
+    "tspm_linear_bwd_weight_splitk_workspace": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
     "tspm_act_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, c_float, _P]),
     "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
     "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),

@@ -32,6 +32,7 @@ struct GemmArgs {
   float* slab;  // split-K: raw partial products to slab[blockIdx.y][M][N] (epilogue in k_splitk_reduce)
   int quad;     // set by gemm_small: 64x64 tiles, one quadrant per wave (see k_gemm_small)
   int wkeff;    // pair launches: the product's own wave count (K split as in its own launch; extra waves idle)
+  float* slab_rs;  // split-K with rowsum: per-slice row sums to slab_rs[blockIdx.y][M] (summed in k_splitk_reduce)
 };
 
 // One round of UU*8 reduction steps for the K-contiguous path of k_gemm_small: lane half kh covers
@@ -169,6 +170,7 @@ TSPM_DEV void gemm_body(const GemmArgs& g, int bid, float* lds) {
         if (cm < g.M) sl[(long long)cm * g.N + ccol] = acc[r];
       }
     }
+    if (want_rs && g.slab_rs && lane < 32 && mok) g.slab_rs[(long long)blockIdx.y * g.M + m] = rs;
     return;
   }
   if (ccol < g.N) {
@@ -221,11 +223,20 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs g, int splits) {
   for (long long t = blockIdx.x * 256LL + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     const int cm = (int)(t / g.N), ccol = (int)(t % g.N);
     float v = 0.f;
-    for (int sidx = 0; sidx < splits; ++sidx) v += g.slab[(long long)sidx * total + t];
+#pragma unroll 8
+    for (int sidx = 0; sidx < splits; ++sidx) v += g.slab[(long long)sidx * total + t];  // loads in flight together
     if (g.bias) v += g.bias[ccol];
     if (g.relu) v = fmaxf(v, 0.f);
     if (g.keep) v = g.keep[t] ? v * g.kscale : 0.f;
     g.C[(long long)cm * g.ldc + ccol] = v;
+  }
+  if (g.rowsum && g.slab_rs) {
+    for (long long t = blockIdx.x * 256LL + threadIdx.x; t < g.M; t += (long long)gridDim.x * 256) {
+      float v = 0.f;
+#pragma unroll 8
+      for (int sidx = 0; sidx < splits; ++sidx) v += g.slab_rs[(long long)sidx * g.M + t];
+      g.rowsum[t] = v;
+    }
   }
 }
 
@@ -443,6 +454,28 @@ extern "C" int tspm_linear_bwd_weight(int32_t n, int32_t in, int32_t out, const 
   // dw[o,i] = sum_n dy[n,o] x[n,i]  (A(m=o, k=n) = dy[n,o]);  db[o] = sum_n dy[n,o]
   GemmArgs g{out, in, n, dy, 1, ldy, x, ldx, 1, dw, in, nullptr, 0, nullptr, 1.f, db};
   return gemm_small(g, static_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t tspm_linear_bwd_weight_splitk_workspace(int32_t n, int32_t in, int32_t out, int32_t splits) {
+  if (n <= 0 || in <= 0 || out <= 0 || splits <= 1) return 0;
+  const int ks = ((cdiv(n, splits) + 31) / 32) * 32;
+  const long long sl = cdiv(n, ks);
+  return (size_t)sl * ((long long)out * in + out) * sizeof(float);
+}
+
+extern "C" int tspm_linear_bwd_weight_splitk(int32_t n, int32_t in, int32_t out, const float* x, int32_t ldx,
+                                             const float* dy, int32_t ldy, float* dw, float* db, int32_t splits,
+                                             void* workspace, size_t workspace_bytes, tspm_stream_t stream) {
+  if (n <= 0 || in <= 0 || out <= 0 || ldx < in || ldy < out || !x || !dy || !dw || splits < 1) return TSPM_ERR_INVALID;
+  const size_t need = tspm_linear_bwd_weight_splitk_workspace(n, in, out, splits);
+  if (need > 0 && (!workspace || workspace_bytes < need)) return TSPM_ERR_WORKSPACE;
+  GemmArgs g{out, in, n, dy, 1, ldy, x, ldx, 1, dw, in, nullptr, 0, nullptr, 1.f, db};
+  if (need > 0) {
+    const int ks = ((cdiv(n, splits) + 31) / 32) * 32;
+    g.slab = static_cast<float*>(workspace);
+    g.slab_rs = g.slab + (long long)cdiv(n, ks) * out * in;
+  }
+  return gemm_small(g, static_cast<hipStream_t>(stream), need > 0 ? splits : 1);
 }
 
 // Up to 4 independent products in one launch: blocks are dealt out to the problems in order.

@@ -275,6 +275,69 @@ __global__ __launch_bounds__(256) void k_textcnn_wgrad(int B, int F, int C, Wgra
   }
 }
 
+// Same gradient, organised for HBM reuse (C = 128 channels): one workgroup per (conv, 8-float slice of
+// the 768 features).  Each step stages NBS batch rows' [T][8] input slices, the g and argmax of those
+// rows in LDS; thread (c = tid / 2, 4 features) accumulates dW[c][0..kh)[4] over b in ascending order —
+// the same fmaf sequence as k_textcnn_wgrad, so the two are bitwise identical — while the input is read
+// from HBM once per conv (T*B*F*4 bytes) instead of once per (channel, batch row) window.
+constexpr int kWgFB = 8;    // features per workgroup
+constexpr int kWgNBS = 8;   // batch rows staged per LDS round
+constexpr int kWgC = 128;   // channels (2 threads each)
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_textcnn_wgrad_slab(int B, int T, int F, WgradSet ws, const float* __restrict__ x,
+                                                            const float* __restrict__ g,
+                                                            const uint8_t* __restrict__ arg, int nc, int nfb) {
+  __shared__ float4 xs[kWgNBS][256][kWgFB / 4];  // [row][t][8 floats]; T <= 256
+  __shared__ float gs[kWgNBS][kWgC];
+  __shared__ int as_[kWgNBS][kWgC];
+  const int i = blockIdx.x / nfb, fb = blockIdx.x - (blockIdx.x / nfb) * nfb;
+  const int kh = ws.kh[i], f0 = fb * kWgFB;
+  const int tid = threadIdx.x, c = tid >> 1, half = tid & 1;
+  const int ci = i * kWgC + c;
+  float4 acc[KMAX];
+#pragma unroll
+  for (int dt = 0; dt < KMAX; ++dt) acc[dt] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dbs = 0.f;
+  for (int b0 = 0; b0 < B; b0 += kWgNBS) {
+    const int nb = B - b0 < kWgNBS ? B - b0 : kWgNBS;
+    __syncthreads();
+    for (int e = tid; e < nb * T * 2; e += 256) {  // 2 float4 per (row, t)
+      const int q = e & 1, rt = e >> 1, r = rt / T, t = rt - r * T;
+      xs[r][t][q] = *reinterpret_cast<const float4*>(x + ((long long)t * B + b0 + r) * F + f0 + 4 * q);
+    }
+    for (int e = tid; e < nb * kWgC; e += 256) {
+      const int r = e / kWgC, cc = e - r * kWgC;
+      gs[r][cc] = g[(long long)(b0 + r) * nc + i * kWgC + cc];
+      as_[r][cc] = arg[(long long)(b0 + r) * nc + i * kWgC + cc];
+    }
+    __syncthreads();
+    for (int r = 0; r < nb; ++r) {
+      const float gv = gs[r][c];
+      if (half == 0) dbs += gv;
+      if (gv == 0.f) continue;
+      const int t0 = as_[r][c];
+#pragma unroll
+      for (int dt = 0; dt < KMAX; ++dt) {
+        if (dt >= kh) break;
+        const float4 v = xs[r][t0 + dt][half];
+        acc[dt].x = fmaf(gv, v.x, acc[dt].x);
+        acc[dt].y = fmaf(gv, v.y, acc[dt].y);
+        acc[dt].z = fmaf(gv, v.z, acc[dt].z);
+        acc[dt].w = fmaf(gv, v.w, acc[dt].w);
+      }
+    }
+  }
+  float* dw = ws.dw[i] + (long long)c * kh * F;
+#pragma unroll
+  for (int dt = 0; dt < KMAX; ++dt) {
+    if (dt >= kh) break;
+    *reinterpret_cast<float4*>(dw + (long long)dt * F + f0 + 4 * half) = acc[dt];
+  }
+  if (fb == 0 && half == 0 && ws.db[i]) ws.db[i][c] = dbs;
+  (void)ci;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Global-norm gradient clip (torch.nn.utils.clip_grad_norm_, norm 2): sum of squares of
 // (grad * grad_scale) in double per workgroup, then one workgroup sums the partials in index order
@@ -435,8 +498,18 @@ extern "C" int tspm_textcnn_bwd(int32_t batch, int32_t steps, int32_t feat, int3
   hipLaunchKernelGGL(k_textcnn_pool_grad, dim3(grid_for(total)), dim3(256), 0, st, total, nc, dout, ld_dout, keep,
                      keep_scale, pooled, g_work);
   TSPM_LAUNCH_CHECK();
-  hipLaunchKernelGGL((k_textcnn_wgrad<5, 4>), dim3(nc), dim3(256), 0, st, batch, feat, channels, ws, x, g_work, argmax,
-                     nc);
+  const bool slab = channels == kWgC && feat % kWgFB == 0 && steps <= 256 &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && getenv("TSPM_TEXTCNN_WGRAD_ROWS") == nullptr;
+  if (slab) {
+    for (int i = 0; i < nconv; ++i)
+      if (reinterpret_cast<uintptr_t>(dw[i]) & 15) return TSPM_ERR_INVALID;
+    const int nfb = feat / kWgFB;
+    hipLaunchKernelGGL((k_textcnn_wgrad_slab<5>), dim3(nconv * nfb), dim3(256), 0, st, batch, steps, feat, ws, x, g_work,
+                       argmax, nc, nfb);
+  } else {
+    hipLaunchKernelGGL((k_textcnn_wgrad<5, 4>), dim3(nc), dim3(256), 0, st, batch, feat, channels, ws, x, g_work,
+                       argmax, nc);
+  }
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

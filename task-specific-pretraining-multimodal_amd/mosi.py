@@ -193,6 +193,15 @@ class MosiEngine:
         self.keep_override: Optional[Dict[str, torch.Tensor]] = None
         self.rng_ctr_ptr: Optional[int] = None
         self._host_ctr: Optional[torch.Tensor] = None
+        # LSTM weight gradients reduce over T*B rows into 256 x {in, 64} outputs (8-16 output tiles): split
+        # the reduction so the launch fills the chip (tspm_linear_bwd_weight_splitk)
+        # — one split for all four (db_ih and db_hh come from two calls and must stay bitwise equal)
+        sp = max(1, min(32, (T * B) // 128))
+        self.wg_splits = {fin: sp for fin in (self.fa, self.fv, H)}
+        wsb = max(int(lib.tspm_linear_bwd_weight_splitk_workspace(T * B, fin, 4 * H, sp)) for fin in (self.fa, self.fv, H))
+        self.wg_ws = torch.empty(max(wsb // 4, 1), **f)
+        self.concurrent = os.environ.get("TSPM_MOSI_SERIAL", "0") != "1"
+        self.side: Optional[torch.cuda.Stream] = None
         self.clip_coef = torch.ones(1, **f)
         self.total_norm = torch.zeros(1, **f)
         self.clip_ws = torch.zeros(int(lib.tspm_grad_clip_workspace()) // 4 + 1, **f)
@@ -237,10 +246,39 @@ class MosiEngine:
         L.check(L.lib().tspm_dropout_mask(self.keep_all.numel(), p, self.m._rng_seed, self.rng_ctr_ptr,
                                           self.keep_all.data_ptr(), sh), "dropout_mask")
 
+    def _fork(self):
+        """Side stream for the LSTM half of the step (it shares no buffer with the TextCNN half until the
+        classifier): returns (side torch stream, its handle) after making it wait for the main stream."""
+        if self.side is None:
+            self.side = torch.cuda.Stream(device=self.device)
+            self._ev = [torch.cuda.Event() for _ in range(4)]
+        main = torch.cuda.current_stream(self.device)
+        self._ev[0].record(main)
+        self.side.wait_event(self._ev[0])
+        return self.side, self.side.cuda_stream
+
+    def _join(self) -> None:
+        self._ev[1].record(self.side)
+        torch.cuda.current_stream(self.device).wait_event(self._ev[1])
+
     def forward(self, sh: int, train: bool) -> None:
+        """Dropout masks, then the LSTM half (side stream) concurrently with the TextCNN half (caller's
+        stream), joined before the classifier; everything graph-capturable."""
+        self._keep_masks(train, sh)
+        if self.concurrent:
+            side, sh_side = self._fork()
+            with torch.cuda.stream(side):
+                self._forward_lstm(sh_side)
+            self._forward_text(sh, train)
+            self._join()
+        else:
+            self._forward_lstm(sh)
+            self._forward_text(sh, train)
+        self._forward_classifier(sh, train)
+
+    def _forward_lstm(self, sh: int) -> None:
         lib, m = L.lib(), self.m
         B, T = self.B, self.T
-        self._keep_masks(train, sh)
         # LSTM input projections over all T*B rows, then both recurrences in one launch
         descs = (L.LstmFwdDesc * 2)()
         for i, (name, enc, x, fin, col) in enumerate((("a", m.netA, self.A, self.fa, 0),
@@ -255,6 +293,10 @@ class MosiEngine:
             d.gates, d.cs, d.hs = bufs["gates"].data_ptr(), bufs["cs"].data_ptr(), bufs["hs"].data_ptr()
             d.h_out = self.fused.data_ptr() + col * 4
         L.check(lib.tspm_lstm_fwd(2, descs, sh), "lstm_fwd")
+
+    def _forward_text(self, sh: int, train: bool) -> None:
+        lib, m = L.lib(), self.m
+        B, T = self.B, self.T
         # TextCNN: three convolutions (implicit GEMM), pooling + dropout, embedding Linear + ReLU
         t = m.netT
         for conv, s, al, y in zip(t.convs(), self.conv_shapes, self.conv_algos, self.conv_out):
@@ -274,6 +316,9 @@ class MosiEngine:
         L.check(lib.tspm_linear_fwd(B, self.nc, emb.out_features, self.fc_in.data_ptr(), self.nc, emb.weight.data_ptr(),
                                     emb.bias.data_ptr(), 1, None, 1.0, self.fused.data_ptr() + col_t * 4, self.E, sh),
                 "textcnn embd")
+
+    def _forward_classifier(self, sh: int, train: bool) -> None:
+        lib, m, B = L.lib(), self.m, self.B
         # FcClassifier: (Linear, ReLU, Dropout) per layer, fc_out
         c = m.netC
         cp = c.dropout_p
@@ -312,6 +357,19 @@ class MosiEngine:
             dx, lddx = (self.dh[j - 1], self.widths[j - 1]) if j > 0 else (self.dfused, self.E)
             linear_bwd(B, fin, w, xin.data_ptr(), fin, self.dh[j].data_ptr(), w, lins[j].weight.data_ptr(),
                        g(lins[j].weight).data_ptr(), g(lins[j].bias).data_ptr(), dx.data_ptr(), lddx, sh)
+        if self.concurrent:
+            side, sh_side = self._fork()
+            with torch.cuda.stream(side):
+                self._backward_lstm(sh_side)
+            self._backward_text(sh)
+            self._join()
+        else:
+            self._backward_text(sh)
+            self._backward_lstm(sh)
+
+    def _backward_text(self, sh: int) -> None:
+        lib, m, g = L.lib(), self.m, self.grad_of
+        B, T = self.B, self.T
         # TextCNN: embedding ReLU, Linear, then pooling/dropout and the sparse conv weight gradients
         t = m.netT
         col_t = m.netA.hidden_size + m.netV.hidden_size
@@ -329,6 +387,10 @@ class MosiEngine:
                                      self.nc, self.keeps[0].data_ptr() if tp > 0 else None,
                                      1.0 / (1.0 - tp) if 0 < tp < 1 else 1.0, self.pooled.data_ptr(),
                                      self.argmax.data_ptr(), dws, dbs, self.g_work.data_ptr(), sh), "textcnn bwd")
+
+    def _backward_lstm(self, sh: int) -> None:
+        lib, m, g = L.lib(), self.m, self.grad_of
+        B, T = self.B, self.T
         # LSTMs: backward through time (one launch for both), then the weight gradients as GEMMs over T*B rows
         descs = (L.LstmBwdDesc * 2)()
         for i, (name, enc, col) in enumerate((("a", m.netA, 0), ("v", m.netV, m.netA.hidden_size))):
@@ -341,12 +403,15 @@ class MosiEngine:
         for name, enc, x, fin in (("a", m.netA, self.A, self.fa), ("v", m.netV, self.V, self.fv)):
             bufs, rnn, H = self.lstm[name], enc.rnn, enc.hidden_size
             # dW_hh = dgates^T h_{t-1} (rows (t, b) of hs[0:T]); db_hh = column sums of dgates
-            L.check(lib.tspm_linear_bwd_weight(T * B, H, 4 * H, bufs["hs"].data_ptr(), H, bufs["dg"].data_ptr(), 4 * H,
-                                               g(rnn.weight_hh_l0).data_ptr(), g(rnn.bias_hh_l0).data_ptr(), sh),
+            ws, wsb = self.wg_ws.data_ptr(), self.wg_ws.numel() * 4
+            L.check(lib.tspm_linear_bwd_weight_splitk(T * B, H, 4 * H, bufs["hs"].data_ptr(), H, bufs["dg"].data_ptr(),
+                                                      4 * H, g(rnn.weight_hh_l0).data_ptr(),
+                                                      g(rnn.bias_hh_l0).data_ptr(), self.wg_splits[H], ws, wsb, sh),
                     "lstm dW_hh")
-            # dW_ih = dgates^T x; db_ih = the same column sums (same reduction order: bitwise db_hh)
-            L.check(lib.tspm_linear_bwd_weight(T * B, fin, 4 * H, x.data_ptr(), fin, bufs["dg"].data_ptr(), 4 * H,
-                                               g(rnn.weight_ih_l0).data_ptr(), g(rnn.bias_ih_l0).data_ptr(), sh),
+            # dW_ih = dgates^T x; db_ih = the same column sums (same split and order: bitwise db_hh)
+            L.check(lib.tspm_linear_bwd_weight_splitk(T * B, fin, 4 * H, x.data_ptr(), fin, bufs["dg"].data_ptr(),
+                                                      4 * H, g(rnn.weight_ih_l0).data_ptr(),
+                                                      g(rnn.bias_ih_l0).data_ptr(), self.wg_splits[fin], ws, wsb, sh),
                     "lstm dW_ih")
 
     def clip(self, sh: int, flat_grad: torch.Tensor, grad_scale: float) -> None:
@@ -489,6 +554,8 @@ class _UttFn(torch.autograd.Function):
                 t = torch.empty_like(p)
                 grads[id(p)] = t
             return t
+        for p in model.parameters():  # allocate on this stream before the backward forks its side stream
+            grad_of(p)
         eng.grad_of = grad_of
         try:
             eng.backward(L.stream_handle())
@@ -528,6 +595,16 @@ class UttFusionModel(nn.Module):
             eng = MosiEngine(self, b, t, device)
             self._engines[key] = eng
         return eng
+
+    def fused_step(self, optimizer: FusedAdam, loss_functions, batch: int, steps: int) -> FusedMosiStep:
+        """The cached FusedMosiStep for (optimizer, loss group, batch, padded steps) — one captured graph per
+        padded length (mosi_data.MOSI.device_loader(step_for=...) gathers straight into its inputs)."""
+        key = (id(optimizer), id(loss_functions), int(batch), int(steps))
+        st = self._steps.get(key)
+        if st is None:
+            st = FusedMosiStep(self, optimizer, loss_functions, int(batch), int(steps))
+            self._steps[key] = st
+        return st
 
     def load_pretrained(self) -> None:
         """utt_fusion.py:63-78 (weights-only checkpoint load)."""
@@ -578,12 +655,7 @@ class UttFusionModel(nn.Module):
         labels = batch["label"].to(device)
         miss = batch.get("pattern_name")
         if isinstance(optimizer, FusedAdam) and _ce_weight(loss_functions) is not None and A.is_cuda:
-            key = (id(optimizer), id(loss_functions), A.shape[0], A.shape[1])
-            st = self._steps.get(key)
-            if st is None:
-                st = FusedMosiStep(self, optimizer, loss_functions, A.shape[0], A.shape[1])
-                self._steps[key] = st
-            out = st.step(A, V, T, labels)
+            out = self.fused_step(optimizer, loss_functions, A.shape[0], A.shape[1]).step(A, V, T, labels)
             logits, loss = out["logits"], out["loss"]
         else:
             self.train()

@@ -269,3 +269,85 @@ def test_seq_gather_pads_like_pad_sequence(gpu):
     torch.cuda.synchronize()
     assert torch.equal(out.cpu().transpose(0, 1), ref)
     assert torch.equal(lab.cpu(), torch.from_numpy(labels[idx.numpy()]))
+
+
+def test_mosi_dataset_collate_and_step_loader(gpu):
+    """mosi_data.MOSI: collate_fn = pad_sequence(batch_first) x pattern mask per modality (data/mosi.py:198-247)
+    with labels, eval batches grouped by pattern; device_loader(step_for=...) gathers the same batch
+    time-major into the step's inputs, and the step on it equals the step on the collated batch."""
+    from tspm_amd.mosi_data import MOSI, PATTERNS, pattern_keep, synthetic_mosi_corpus
+    corpus = synthetic_mosi_corpus(40, seed=3, steps=12, min_len=4)
+    ev = MOSI(split="valid", corpus=corpus, device=gpu)
+    assert len(ev) == 40 * len(PATTERNS)
+    items = [3, 41, 85, 200, 279]  # several patterns (pattern-major indexing)
+    out = ev.collate_fn(ev.__getitems__(items))
+    for it in items:
+        p, s = PATTERNS[it // 40], it % 40
+        b = out[p]
+        j = [i % 40 for i in items if PATTERNS[i // 40] == p].index(s)
+        for k, m in enumerate(("audio", "video", "text")):
+            seqs = [torch.from_numpy(corpus.data[m][corpus.offsets[m][i % 40]:corpus.offsets[m][i % 40] +
+                                                    corpus.lengths[m][i % 40]]) for i in items if PATTERNS[i // 40] == p]
+            ref = torch.nn.utils.rnn.pad_sequence(seqs, batch_first=True) * pattern_keep(p)[m]
+            assert torch.equal(b[m].cpu(), ref), (p, m)
+        assert b["label"][j].item() == corpus.labels[s]
+    # train loader straight into a step's buffers == the collated batch through train_step's load
+    tr = MOSI(split="train", corpus=synthetic_mosi_corpus(16, seed=4, steps=10), device=gpu, selected_patterns=["atv"])
+    m1 = _dropin(0).to(gpu)
+    opt = tspm_amd.FusedAdam(m1.parameters(), lr=LR, weight_decay=WD)
+    seen = []
+    for b in tr.device_loader(8, shuffle=False, step_for=lambda n, t: seen.append((n, t)) or m1.fused_step(opt, None, n, t)):
+        st = m1.fused_step(opt, None, 8, 10)
+        assert b["audio"] is st.eng.A and b["time_major"]
+        ref = tr.collate_fn(tr.__getitems__(list(range(len(seen) * 8 - 8, len(seen) * 8))))
+        for m, buf in (("audio", st.eng.A), ("video", st.eng.V), ("text", st.eng.X)):
+            assert torch.equal(buf.transpose(0, 1).cpu(), ref[m].cpu()), m
+        assert torch.equal(st.eng.labels.cpu(), ref["label"].cpu())
+    assert seen == [(8, 10), (8, 10)]
+
+
+@pytest.mark.parametrize("B,T", [(128, 50), (6, 9)])
+def test_textcnn_wgrad_slab_equals_rows_kernel(gpu, B, T):
+    """The feature-slab TextCNN weight-gradient kernel is bitwise the per-(conv, channel) kernel (same fmaf
+    order over the batch), including zero gradients and the bias sums."""
+    import ctypes
+    import os
+    g = torch.Generator().manual_seed(B)
+    F, C, hs = 768, 128, [3, 4, 5]
+    nc = 3 * C
+    x = torch.randn(T * B * F, generator=g).to(gpu)
+    dout = torch.randn(B, nc, generator=g).to(gpu)
+    keep = (torch.rand(B, nc, generator=g) > 0.5).to(torch.uint8).to(gpu)
+    pooled = torch.randn(B, nc, generator=g).relu().to(gpu)
+    arg = torch.stack([torch.randint(0, T - h + 1, (B, C), generator=g) for h in hs], 1).reshape(B, nc)
+    arg = arg.to(torch.uint8).to(gpu)
+    work = torch.empty(B, nc, device=gpu)
+
+    def run():
+        dws = [torch.full((C, h, F), float("nan"), device=gpu) for h in hs]
+        dbs = [torch.full((C,), float("nan"), device=gpu) for _ in hs]
+        L.check(L.lib().tspm_textcnn_bwd(B, T, F, 3, (ctypes.c_int32 * 3)(*hs), C, x.data_ptr(), dout.data_ptr(), nc,
+                                         keep.data_ptr(), 2.0, pooled.data_ptr(), arg.data_ptr(),
+                                         (ctypes.c_void_p * 3)(*[d.data_ptr() for d in dws]),
+                                         (ctypes.c_void_p * 3)(*[d.data_ptr() for d in dbs]), work.data_ptr(),
+                                         L.stream_handle()), "textcnn_bwd")
+        torch.cuda.synchronize()
+        return [d.cpu() for d in dws + dbs]
+    slab = run()
+    os.environ["TSPM_TEXTCNN_WGRAD_ROWS"] = "1"
+    try:
+        rows = run()
+    finally:
+        del os.environ["TSPM_TEXTCNN_WGRAD_ROWS"]
+    for a, b in zip(slab, rows):
+        assert torch.equal(a, b)
+    # and against a dense float64 restatement
+    gw = (dout * keep.float() * 2.0 * (pooled > 0).float()).cpu().double()
+    xx = x.cpu().double().view(T, B, F)
+    for i, h in enumerate(hs):
+        ref = torch.zeros(C, h, F, dtype=torch.float64)
+        a = arg.cpu().long()[:, i * C:(i + 1) * C]
+        for dt in range(h):
+            rowsx = xx[a + dt, torch.arange(B)[:, None]]  # [B, C, F]
+            ref[:, dt] += (gw[:, i * C:(i + 1) * C, None] * rowsx).sum(0)
+        assert rel_l2(slab[i], ref) < 1e-6

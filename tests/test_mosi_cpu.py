@@ -98,3 +98,31 @@ netC: !FcClassifier {input_dim: 192, layers: [192, 64, 32], output_dim: 3, dropo
     assert isinstance(doc["netA"], M.LSTMEncoder) and isinstance(doc["netT"], M.TextCNN)
     assert isinstance(doc["netC"], M.FcClassifier)
     assert tspm_amd.plugin.MODELS["utt-fusion"] is M.UttFusionModel
+
+
+def test_mosi_corpus_packing_and_padded_length():
+    """mosi_data: ragged rows packed per modality (offsets/lengths), pad length = the batch maximum
+    (pad_sequence), an unaligned batch is refused unless pad_to covers it, pattern semantics."""
+    from tspm_amd import mosi_data as D
+    g = np.random.default_rng(0)
+    lens = [3, 7, 5]
+    seqs = {"audio": [g.standard_normal((l, 5), dtype=np.float32) for l in lens],
+            "video": [g.standard_normal((l, 20), dtype=np.float32) for l in lens],
+            "text": [g.standard_normal((l, 8), dtype=np.float32) for l in [3, 7, 6]]}
+    c = D.MosiCorpus(seqs, np.array([0, 2, 1]))
+    assert list(c.offsets["audio"]) == [0, 3, 10] and list(c.lengths["text"]) == [3, 7, 6]
+    np.testing.assert_array_equal(c.data["video"][3:10], seqs["video"][1])
+
+    class _Dc(D.DeviceMosiCorpus):  # host-side length logic only (no upload)
+        def __init__(self, corpus):
+            self.host_lengths = corpus.lengths
+    dc = _Dc(c)
+    assert dc.steps_for(np.array([0, 1])) == 7
+    with pytest.raises(tspm_amd._lib.TspmError):
+        dc.steps_for(np.array([2]))  # audio 5 vs text 6: pad_sequence would pad them differently
+    assert dc.steps_for(np.array([2]), pad_to=50) == 50
+    assert D.pattern_keep("at") == {"audio": 1.0, "video": 0.0, "text": 1.0}
+    split = {"audio": np.zeros((2, 4, 5)), "vision": np.zeros((2, 4, 20)), "text": np.zeros((2, 4, 8)),
+             "classification_labels": np.array([[1], [2]])}
+    c2 = D.MosiCorpus.from_split(split)
+    assert len(c2) == 2 and c2.labels.dtype == np.int64 and list(c2.lengths["text"]) == [4, 4]
