@@ -20,7 +20,8 @@ FAMILIES = [("conv", ("k_fwd_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k
             ("bn", ("k_bn_", "k_bn1d")), ("pool", ("k_maxpool", "k_avgpool")), ("adam", ("k_adam",)),
             ("gather", ("k_avmnist_gather",)), ("head", ("k_gemm_small", "k_gemm_pair", "k_splitk_reduce",
                                                          "k_cross_entropy", "k_act_bwd", "k_dropout")),
-            ("mmimdb_ew", ("k_gmu", "k_maxout", "k_bce"))]  # "head" = every small-GEMM (Linear) launch
+            ("mmimdb_ew", ("k_gmu", "k_maxout", "k_bce")),
+            ("mosi", ("k_lstm_", "k_textcnn", "k_seq_gather", "k_sumsq", "k_clip_coef"))]  # "head" = every small-GEMM (Linear) launch
 
 
 def family(name: str) -> str:

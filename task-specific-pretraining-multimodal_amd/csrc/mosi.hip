@@ -362,11 +362,21 @@ __global__ __launch_bounds__(256) void k_sumsq(long long count, const float* __r
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-__global__ __launch_bounds__(64) void k_clip_coef(int nparts, const double* __restrict__ partial, float max_norm,
-                                                  float* __restrict__ coef, float* __restrict__ norm_out) {
+// one workgroup: strided partial sums then a fixed-order LDS tree (deterministic; all loads in flight
+// together instead of one thread's dependent chain)
+__global__ __launch_bounds__(256) void k_clip_coef(int nparts, const double* __restrict__ partial, float max_norm,
+                                                   float* __restrict__ coef, float* __restrict__ norm_out) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) a += partial[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += partial[i];
+  const double s = red[0];
   const float total = (float)sqrt(s);
   const float cf = max_norm / (total + 1e-6f);
   coef[0] = cf < 1.f ? cf : 1.f;
@@ -524,7 +534,7 @@ extern "C" int tspm_grad_clip_coef(int64_t count, const float* grad, float grad_
   double* part = static_cast<double*>(workspace);
   hipLaunchKernelGGL(k_sumsq, dim3(kClipBlocks), dim3(256), 0, st, (long long)count, grad, grad_scale, part);
   TSPM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_clip_coef, dim3(1), dim3(64), 0, st, kClipBlocks, part, max_norm, coef, total_norm);
+  hipLaunchKernelGGL(k_clip_coef, dim3(1), dim3(256), 0, st, kClipBlocks, part, max_norm, coef, total_norm);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }
