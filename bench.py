@@ -121,14 +121,35 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
     same mapping.  ``run_concurrent``: optionally also profile the benched two-stream graph (kernels
     of the two encoders overlap there and stretch each other)."""
     from tspm_amd.roofline import CONV_KERNEL, attribute_conv_kernels, device_kernels, launch_flops
-    ks = device_kernels(run_serial, replays)
+    ks_all = device_kernels(run_serial, replays)
+    # split the trace into steps at the optimizer's k_adam (the last kernel of every step) and keep
+    # the steps whose conv-kernel count matches the recorded launch sequence (the profiler can drop
+    # a few records in a long capture; a partial step would skew every per-step figure)
+    from tspm_amd.roofline import CONV_SECONDARY
+    steps, cur = [], []
+    for k in ks_all:
+        cur.append(k)
+        if "k_adam(" in k["name"] or k["name"].startswith("k_adam") or "::k_adam(" in k["name"]:
+            steps.append(cur)
+            cur = []
+    good = [st for st in steps if sum(1 for k in st if CONV_KERNEL.search(k["name"])
+                                      and not CONV_SECONDARY.search(k["name"])) == len(seq)]
+    if len(steps) != replays:  # not one k_adam per step (several parameter groups): no split
+        good = []
+    dropped = len(steps) - len(good)
+    if good:
+        replays = len(good)
+        ks = [k for st in good for k in st]
+    else:
+        ks = ks_all
     conv = [k for k in ks if CONV_KERNEL.search(k["name"])]
     conv_us = sum(k["dur"] for k in conv) / replays
     flops = sum(launch_flops(op, kind) for _, op, kind in seq)
     out = {"conv_kernel_ms_per_step": conv_us / 1e3, "valid_tap_flop_per_step": flops,
            "achieved": flops / (conv_us * 1e-6) / 1e12 if conv_us else None,
            "kernel_ms_per_step": sum(k["dur"] for k in ks) / replays / 1e3, "kernels_per_step": len(ks) / replays,
-           "conv_launches_per_step": len(seq), "families": {}}
+           "conv_launches_per_step": len(seq), "families": {}, "profiled_steps": replays,
+           "incomplete_steps_dropped": dropped}
     for k in ks:
         fam = ("conv" if CONV_KERNEL.search(k["name"]) else "bn" if "k_bn_" in k["name"] else
                "adam" if "k_adam" in k["name"] else "pool" if "pool" in k["name"] else "other")

@@ -205,7 +205,10 @@ int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* runnin
  *   dy  = gamma*invstd*(g' - dbeta/M - xhat*dgamma/M)
  *   dy2 likewise for the second BN; if dres != NULL it receives g' (identity residual grad).
  * dy_t / dy2_t (nullable): also write dy / dy2 transposed, [c][ld_t] (see "transposed copies").
- * Workspace: tspm_bn_bwd_workspace. */
+ * Workspace: tspm_bn_bwd_workspace bytes; its first 256 bytes hold the barrier counters of the
+ * single-launch path (ABI 13: layers whose [rows x 64-channel] grid fits 256 workgroups run partial
+ * sums, merge and apply in ONE launch) — zero them before the first call; every call leaves them zero.
+ * One workspace must not be used by two launches in flight at once. */
 int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y,
                 const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                 float* dy, const float* y2, const float* mean2, const float* invstd2,
@@ -213,6 +216,10 @@ int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const fl
                 float* dy_t, float* dy2_t, int64_t ld_t, void* workspace, size_t workspace_bytes,
                 tspm_stream_t stream);
 size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
+/* Diagnostics (ABI 13): how many in-launch barrier waits of the single-launch BN backward timed out
+ * since the library was loaded (0 in a healthy run; a timed-out launch writes NaN gradients instead
+ * of hanging).  0xffffffff if the counter cannot be read. */
+uint32_t tspm_debug_barrier_timeouts(void);
 
 /* ------------------------------------------------------------------------------------------------
  * Pooling — nn.MaxPool2d(3, 2, 1) (resnet.py:140,208) and AdaptiveAvgPool2d(1)+flatten (:149,215-216)
@@ -323,6 +330,9 @@ typedef struct tspm_adam_hyper {
 } tspm_adam_hyper;
 /* hyper->step += 1 (device-side, so a captured graph advances the bias correction per replay). */
 int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream);
+/* counters[i] += value for i < count (ABI 13): every BatchNorm's num_batches_tracked (one shared
+ * int64 vector) advanced once per training step inside the captured step. */
+int tspm_counters_add(int64_t* counters, int64_t count, int64_t value, tspm_stream_t stream);
 /* One fused Adam update over `count` contiguous fp32 elements (the flat parameter buffer). */
 int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    const tspm_adam_hyper* hyper, tspm_stream_t stream);

@@ -108,6 +108,7 @@ _SIGS = {
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
+    "tspm_debug_barrier_timeouts": (ctypes.c_uint32, []),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),
@@ -126,6 +127,7 @@ _SIGS = {
     "tspm_act_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, c_float, _P]),
     "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
     "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
+    "tspm_counters_add": (c_int32, [_P, c_int64, c_int64, _P]),
     "tspm_adam_begin": (c_int32, [_P, _P]),
     "tspm_adam_step": (c_int32, [c_int64, _P, _P, _P, _P, _P, _P]),
     "tspm_image_lut": (c_int32, [c_int64, _P, _P, _P, _P]),
@@ -225,3 +227,11 @@ def require_cuda_f32(t: torch.Tensor, name: str) -> None:
 
 def hwnc_strides(n: int, h: int, w: int, c: int) -> Strides4:
     return Strides4(c, w * n * c, n * c, 1)
+
+
+def counters_add(t: torch.Tensor, value: int = 1, stream: Optional[int] = None) -> None:
+    """t (contiguous int64 on the device) += value in one libtspm launch (num_batches_tracked)."""
+    if t.dtype != torch.int64 or not t.is_cuda or not t.is_contiguous():
+        raise TspmError("counters_add: contiguous int64 device tensor")
+    check(lib().tspm_counters_add(t.data_ptr(), t.numel(), int(value), stream_handle() if stream is None else stream),
+          "counters_add")

@@ -350,6 +350,11 @@ __global__ __launch_bounds__(256) void k_cross_entropy(int N, int K, const float
 
 __global__ void k_adam_begin(tspm_adam_hyper* h) { h->step += 1; }
 
+// num_batches_tracked += value for every BatchNorm of a model (one shared int64 vector)
+__global__ __launch_bounds__(64) void k_counters_add(long long n, int64_t* __restrict__ c, long long v) {
+  for (long long i = blockIdx.x * 64LL + threadIdx.x; i < n; i += (long long)gridDim.x * 64) c[i] += v;
+}
+
 __global__ __launch_bounds__(256) void k_adam(long long count, float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const tspm_adam_hyper* __restrict__ hp,
@@ -615,6 +620,16 @@ extern "C" int tspm_cross_entropy(int32_t n, int32_t classes, const float* logit
   if (n <= 0 || classes <= 0 || !logits || !labels) return TSPM_ERR_INVALID;
   hipLaunchKernelGGL(k_cross_entropy, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), n, classes, logits,
                      labels, loss, dlogits, grad_scale, stats);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_counters_add(int64_t* counters, int64_t count, int64_t value, tspm_stream_t stream) {
+  if (count < 0 || (count > 0 && !counters)) return TSPM_ERR_INVALID;
+  if (count == 0) return TSPM_OK;
+  const long long blocks = cdiv64(count, 64) > 64 ? 64 : cdiv64(count, 64);
+  hipLaunchKernelGGL(k_counters_add, dim3((unsigned)blocks), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     (long long)count, counters, (long long)value);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

@@ -482,7 +482,7 @@ class MMIMDb(nn.Module):
         if self.training:
             eng._host_ctr.add_(1)
             nbt = shared_batches_tracked(self, I.device, (nn.BatchNorm1d,))
-            nbt.add_(1)
+            L.counters_add(nbt)
         return eng.logits.clone()
 
     def train_step(self, batch: Dict[str, Any], optimizer, loss_functions, device, metric_recorder=None,
@@ -572,7 +572,7 @@ class FusedMMIMDbStep:
         self.eng.forward(sh, True)
         self.eng.loss_fn(sh, self.weight, True, self.log_stats)
         self.eng.backward(sh)
-        self.nbt.add_(1)
+        L.counters_add(self.nbt)
 
     def _all(self) -> None:
         self._fwd_bwd()

@@ -245,7 +245,7 @@ class FusedMonoStep(_MonoBuffers):
         linear_bwd(n, hid, K, self.emb.data_ptr(), hid, self.dlogits.data_ptr(), K, cls.weight.data_ptr(),
                    cls.weight.grad.data_ptr(), cls.bias.grad.data_ptr(), self.demb.data_ptr(), hid, sh)
         self.eng.backward(self.demb, hid)
-        self.nbt.add_(1)
+        L.counters_add(self.nbt)
         self.opt.launch(sh)
 
     def run(self) -> None:

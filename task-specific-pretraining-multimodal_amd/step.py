@@ -235,7 +235,7 @@ class FusedTrainStep:
             main.wait_stream(self.aux_a)
             main.wait_stream(self.aux_i)
         if phase in (0, 2):
-            self.nbt.add_(1)
+            L.counters_add(self.nbt)
 
     def phased_allreduce(self, force: bool = False, bucket_mb: float = 64.0, group=None):
         """The overlapped DP exchange for this step: gradient ranges of FusedAdam's flat buffers in
@@ -274,7 +274,7 @@ class FusedTrainStep:
                                            self.stats.data_ptr(), sh), "cross_entropy")
         self._classify(sh)
         self._head_bwd(sh)
-        self.nbt.add_(1)
+        L.counters_add(self.nbt)
 
     def _run_phased(self) -> None:
         """DP step with the RCCL exchange overlapped with backward:
@@ -384,7 +384,7 @@ class FusedTrainStep:
             self.eng_a.backward(None, F, phase=2)
             main.wait_stream(self.side)
             self.opt.launch_ranges(main.cuda_stream, early)
-            self.nbt.add_(1)
+            L.counters_add(self.nbt)
             return
         s3 = self.aux_a
         self._fwd_bwd(phase=1)
@@ -468,8 +468,6 @@ class FusedTrainStep:
                 self.graph_opt.replay()
             else:
                 self._opt()
-                if self.use_graph and self.calls >= 1 and self.graph_opt is None:
-                    pass
         self.opt.note_steps(1)
         self.calls += 1
 

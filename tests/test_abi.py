@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "tspm.h")
 
 def header_prototypes():
     src = open(HEADER).read()
-    return dict(re.findall(r"\n(?:int|int32_t|int64_t|size_t|const char\*)\s+(tspm_\w+)\(([^;]*?)\);", src, re.S))
+    return dict(re.findall(r"\n(?:int|int32_t|int64_t|uint32_t|size_t|const char\*)\s+(tspm_\w+)\(([^;]*?)\);", src, re.S))
 
 
 def test_library_loads_and_version():

@@ -239,10 +239,14 @@ def _bn_ref_block(y, y2, gamma, beta, gamma2, beta2, res, mode, relu):
     return out, [y, ga, be] + extra
 
 
-@pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (384, 512)])
+@pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (384, 512), (24576, 64), (1536, 256), (100, 8)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_bn_block_fwd_bwd(gpu, m, c, mode):
+@pytest.mark.parametrize("fused", [True, False])
+def test_bn_block_fwd_bwd(gpu, m, c, mode, fused, monkeypatch):
+    """BN apply + backward against float64 autograd; the backward both as the single launch with the
+    in-launch barrier (fused) and as the two-launch partial / apply pair."""
     from tspm_amd import _lib as L
+    monkeypatch.setenv("TSPM_BN_BWD_FUSED", "1" if fused else "0")
     lib = L.lib()
     g = torch.Generator().manual_seed(5)
     y = torch.randn(m, c, generator=g) * 3 + 1
@@ -300,6 +304,48 @@ def test_bn_block_fwd_bwd(gpu, m, c, mode):
         assert torch.allclose(dy2o.double().cpu(), leaves[3].grad, rtol=1e-3, atol=2e-5)
         assert torch.allclose(gw2.double().cpu(), leaves[4].grad, rtol=1e-4, atol=1e-3)
         assert torch.allclose(gb2.double().cpu(), leaves[5].grad, rtol=1e-4, atol=1e-3)
+    assert lib.tspm_debug_barrier_timeouts() == 0
+    assert not ws[:256].any()  # barrier counters re-armed
+
+
+def test_bn_bwd_fused_concurrent_streams(gpu):
+    """Two single-launch BN backwards with in-launch barriers in flight at once on two streams (as the
+    two encoders' backward passes run), many times: no barrier wait times out, counters re-arm, and
+    the results equal the same launches run one after the other."""
+    from tspm_amd import _lib as L
+    lib = L.lib()
+    g = torch.Generator().manual_seed(11)
+    shapes = [(24576, 64), (6272, 64)]  # the largest fused grids of the two encoders (192 + 196 rows blocks)
+    bufs = []
+    for m, c in shapes:
+        y = (torch.randn(m, c, generator=g) * 2).to(gpu)
+        out = torch.randn(m, c, generator=g).relu().to(gpu)
+        gg = torch.randn(m, c, generator=g).to(gpu)
+        mean, inv = y.mean(0).contiguous(), (1 / (y.var(0, unbiased=False) + 1e-5).sqrt()).contiguous()
+        gamma = torch.randn(c, generator=g).to(gpu)
+        ws, wsb = _bn_ws(lib, m, c, gpu, bwd=True)
+        bufs.append(dict(m=m, c=c, y=y, out=out, g=gg, mean=mean, inv=inv, gamma=gamma, ws=ws, wsb=wsb,
+                         dy=torch.empty(m, c, device=gpu), gw=torch.empty(c, device=gpu), gb=torch.empty(c, device=gpu)))
+
+    def launch(b, stream):
+        L.check(lib.tspm_bn_bwd(b["m"], b["c"], b["g"].data_ptr(), b["out"].data_ptr(), b["y"].data_ptr(),
+                                b["mean"].data_ptr(), b["inv"].data_ptr(), b["gamma"].data_ptr(), b["gw"].data_ptr(),
+                                b["gb"].data_ptr(), b["dy"].data_ptr(), None, None, None, None, None, None, None, None,
+                                None, None, 0, b["ws"].data_ptr(), b["wsb"], stream.cuda_stream), "bn_bwd")
+    s0 = torch.cuda.current_stream()
+    for b in bufs:
+        launch(b, s0)
+    torch.cuda.synchronize()
+    want = [(b["dy"].clone(), b["gw"].clone(), b["gb"].clone()) for b in bufs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(50):
+        launch(bufs[0], s1)
+        launch(bufs[1], s2)
+    torch.cuda.synchronize()
+    assert lib.tspm_debug_barrier_timeouts() == 0
+    for b, (dy, gw, gb) in zip(bufs, want):
+        assert torch.equal(b["dy"], dy) and torch.equal(b["gw"], gw) and torch.equal(b["gb"], gb)
+        assert not b["ws"][:256].any()
 
 
 # ------------------------------------------------------------------------------------------------
