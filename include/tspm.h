@@ -160,6 +160,29 @@ int tspm_conv_bwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo_dgrad
                   const tspm_conv_algo* algo_wgrad, const float* x, const tspm_strides4* x_strides,
                   const float* dy, const float* w, float* dx, int32_t beta, float* dw, void* ws_dgrad,
                   size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, tspm_stream_t stream);
+/* BatchNorm-backward partial sums in the data-gradient epilogue (ABI 13): when the conv's input
+ * gradient dx is the FINAL gradient g of a `relu(BN(y) [+ BN2(y2)])` output `out` (beta = 1: dx
+ * accumulates onto the other contributions first), the epilogue also writes, per row tile of
+ * tspm_conv_dgrad_bn_tiles rows-tiles and channel, sum g', sum g'(y - mean) [, sum g'(y2 - mean2)]
+ * with g' = g * (out > 0) into `partial` (3 planes of [tiles][c]; out / y2 / mean2 nullable) —
+ * the input of tspm_bn_bwd_apply.  LDS-staged (variant 1) algorithms only. */
+typedef struct tspm_bn_bwd_fuse {
+  float* partial;
+  const float* out;
+  const float* y;
+  const float* mean;
+  const float* y2;
+  const float* mean2;
+} tspm_bn_bwd_fuse;
+int32_t tspm_conv_dgrad_bn_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);  /* 0: unsupported */
+int tspm_conv_dgrad_bnfuse(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy, const float* w,
+                           float* dx, int32_t beta, void* workspace, size_t workspace_bytes,
+                           const tspm_bn_bwd_fuse* bn, tspm_stream_t stream);
+int tspm_conv_bwd_bnfuse(const tspm_conv_shape* shape, const tspm_conv_algo* dgrad_algo,
+                         const tspm_conv_algo* wgrad_algo, const float* x, const tspm_strides4* x_strides,
+                         const float* dy, const float* w, float* dx, int32_t beta, float* dw, void* ws_dgrad,
+                         size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, const tspm_bn_bwd_fuse* bn,
+                         tspm_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * BatchNorm2d, training mode (batch statistics over N*H*W, biased variance for normalisation,
@@ -216,6 +239,17 @@ int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const fl
                 float* dy_t, float* dy2_t, int64_t ld_t, void* workspace, size_t workspace_bytes,
                 tspm_stream_t stream);
 size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
+/* BN backward with the partial sums already computed (ABI 13): by the producing conv's data-gradient
+ * epilogue (tspm_conv_dgrad_bnfuse / tspm_conv_bwd_bnfuse) as `tiles` row tiles, 3 planes of
+ * [tiles][c] floats (sum g', sum g'(y - mean), sum g'(y2 - mean2)).  Merges them per channel in double
+ * (fixed order) and applies — one launch instead of tspm_bn_bwd's two.  Same arguments and results
+ * as tspm_bn_bwd otherwise (no transposed copies).  tiles <= tspm_bn_bwd_apply_max_tiles(). */
+int tspm_bn_bwd_apply(int64_t m, int32_t c, int32_t tiles, const float* partial, const float* g, const float* out,
+                      const float* y, const float* mean, const float* invstd, const float* gamma, float* dgamma,
+                      float* dbeta, float* dy, const float* y2, const float* mean2, const float* invstd2,
+                      const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres,
+                      tspm_stream_t stream);
+int32_t tspm_bn_bwd_apply_max_tiles(void);
 /* Diagnostics (ABI 13): how many in-launch barrier waits of the single-launch BN backward timed out
  * since the library was loaded (0 in a healthy run; a timed-out launch writes NaN gradients instead
  * of hanging).  0xffffffff if the counter cannot be read. */

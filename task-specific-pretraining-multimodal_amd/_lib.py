@@ -38,6 +38,12 @@ class ConvAlgo(Structure):
     _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits", "variant")]
 
 
+class BnBwdFuse(Structure):
+    """tspm_bn_bwd_fuse: BN-backward partial sums written by a dgrad epilogue."""
+    _fields_ = [("partial", c_void_p), ("out", c_void_p), ("y", c_void_p), ("mean", c_void_p), ("y2", c_void_p),
+                ("mean2", c_void_p)]
+
+
 class Strides4(Structure):
     _fields_ = [(n, c_int64) for n in ("sn", "sh", "sw", "sc")]
 
@@ -108,6 +114,13 @@ _SIGS = {
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
+    "tspm_bn_bwd_apply": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 18 + [_P]),
+    "tspm_bn_bwd_apply_max_tiles": (c_int32, []),
+    "tspm_conv_dgrad_bn_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
+    "tspm_conv_dgrad_bnfuse": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, _P, _P, c_int32, _P, c_size_t,
+                                         POINTER(BnBwdFuse), _P]),
+    "tspm_conv_bwd_bnfuse": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), _P, POINTER(Strides4),
+                                       _P, _P, _P, c_int32, _P, _P, c_size_t, _P, c_size_t, POINTER(BnBwdFuse), _P]),
     "tspm_debug_barrier_timeouts": (ctypes.c_uint32, []),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),

@@ -789,6 +789,39 @@ bool c_ok(int C) { return C >= 4 && C % 4 == 0; }
 
 }  // namespace
 
+extern "C" int32_t tspm_bn_bwd_apply_max_tiles(void) { return kMergeTiles; }
+
+extern "C" int tspm_bn_bwd_apply(int64_t m, int32_t c, int32_t tiles, const float* partial, const float* g,
+                                 const float* out, const float* y, const float* mean, const float* invstd,
+                                 const float* gamma, float* dgamma, float* dbeta, float* dy, const float* y2,
+                                 const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
+                                 float* dbeta2, float* dy2, float* dres, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > kMergeTiles || !partial || !g || !y || !mean || !invstd || !gamma ||
+      !dy)
+    return TSPM_ERR_INVALID;
+  const bool two = y2 != nullptr;
+  if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool ho = out != nullptr, dr = dres != nullptr;
+  const int cblk = cdiv(c, kChanPerBlock);
+  long long rb = cdiv64(m, std::max(1, 512 / cblk));  // ~512 workgroups, >= 64 rows each
+  if (rb < 64) rb = 64;
+  const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
+#define BNB_A(HO, TW, DR)                                                                                       \
+  hipLaunchKernelGGL((k_bn_bwd_apply_m<HO, TW, DR>), agrid, dim3(256), 0, st, (long long)m, c, tiles, partial, invstd, \
+                     gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, g, out, y, mean, y2, mean2, rb, dy, dy2, dres)
+  if (ho) {
+    if (two) { if (dr) BNB_A(true, true, true); else BNB_A(true, true, false); }
+    else { if (dr) BNB_A(true, false, true); else BNB_A(true, false, false); }
+  } else {
+    if (two) { if (dr) BNB_A(false, true, true); else BNB_A(false, true, false); }
+    else { if (dr) BNB_A(false, false, true); else BNB_A(false, false, false); }
+  }
+#undef BNB_A
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
 extern "C" uint32_t tspm_debug_barrier_timeouts(void) {
   unsigned v = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(tspm_g_barrier_timeouts), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)

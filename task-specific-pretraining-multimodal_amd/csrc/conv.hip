@@ -651,6 +651,7 @@ ConvArgs make_args(const tspm_conv_shape* s) {
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = (long long)s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
+  g.bnb = BnbFuse{};
   return g;
 }
 
@@ -867,6 +868,45 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   return tspm_detail::lds_bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w,
                               ws_w_bytes, static_cast<hipStream_t>(stream));
+}
+
+// ---- dgrad epilogue with BatchNorm-backward partial sums (ABI 13, variant 1 only) --------------
+extern "C" int32_t tspm_conv_dgrad_bn_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
+  if (!shape_ok(s) || !is_lds(user) || s->c % 32 != 0) return 0;  // whole 32-channel fragments
+  const tspm_detail::LdsAlgo la = lds_algo(user);
+  if (!tspm_detail::lds_dgrad_supported(s, la)) return 0;
+  return tspm_detail::lds_dgrad_tiles(s, la);
+}
+
+static bool bnb_of(const tspm_conv_shape* s, const tspm_conv_algo* user, const tspm_bn_bwd_fuse* f, BnbFuse& out) {
+  if (!f || !f->partial || !f->y || !f->mean) return false;
+  if ((f->y2 == nullptr) != (f->mean2 == nullptr)) return false;
+  const int tiles = tspm_conv_dgrad_bn_tiles(s, user);
+  if (tiles <= 0) return false;
+  out = BnbFuse{f->partial, f->out, f->y, f->mean, f->y2, f->mean2, tiles};
+  return true;
+}
+
+extern "C" int tspm_conv_dgrad_bnfuse(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* dy,
+                                      const float* w, float* dx, int32_t beta, void* ws, size_t ws_bytes,
+                                      const tspm_bn_bwd_fuse* bn, tspm_stream_t stream) {
+  if (!shape_ok(s) || !dy || !w || !dx || !is_lds(user)) return TSPM_ERR_INVALID;
+  BnbFuse b;
+  if (!bnb_of(s, user, bn, b)) return TSPM_ERR_INVALID;
+  const tspm_detail::LdsAlgo la = lds_algo(user);
+  return tspm_detail::lds_dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), &b);
+}
+
+extern "C" int tspm_conv_bwd_bnfuse(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                                    const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
+                                    int32_t beta, float* dw, void* ws_d, size_t ws_d_bytes, void* ws_w,
+                                    size_t ws_w_bytes, const tspm_bn_bwd_fuse* bn, tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
+  if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
+  BnbFuse b;
+  if (!bnb_of(s, dg, bn, b)) return TSPM_ERR_INVALID;
+  return tspm_detail::lds_bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w,
+                              ws_w_bytes, static_cast<hipStream_t>(stream), &b);
 }
 
 extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x_t, int64_t ldx,

@@ -425,7 +425,15 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
-  if (id.wk == 0 && col0 < Cc) acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
+  if (id.wk == 0 && col0 < Cc) {
+    if (g.bnb.part) {  // the final gradient, then the BN-backward partial sums of its row tile
+      if (g.beta) acc.add_from(dx, row0, col0, Cc, Cc, lane);
+      acc.store(dx, row0, col0, g.m, Cc, Cc, lane, false);
+      acc.bnb_partials(g.bnb, bk.x * C::WM + id.wm, row0, col0, Cc, lane);
+    } else {
+      acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
+    }
+  }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
   TSPM_STAMP_CLK(tspm_g_stamps_lds, 7);
 }
@@ -579,6 +587,7 @@ ConvArgs args_of(const tspm_conv_shape* s) {
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
+  g.bnb = BnbFuse{};
   return g;
 }
 
@@ -701,12 +710,15 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
   return TSPM_OK;
 }
 
+int lds_dgrad_tiles(const tspm_conv_shape* s, const LdsAlgo& a) { return s->h * s->w * s->n / (a.tm * 32); }
+
 int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
-              void* ws, size_t ws_bytes, hipStream_t st) {
+              void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb) {
   ConvArgs g = args_of(s);
   g.m = s->h * s->w * s->n;
   g.splits = a.splits;
   g.beta = beta ? 1 : 0;
+  if (bnb) g.bnb = *bnb;
   float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_dgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
@@ -797,13 +809,14 @@ bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(a
 
 int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
             const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-            hipStream_t st) {
+            hipStream_t st, const BnbFuse* bnb) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
   BwdLaunch L{};
   L.gd = args_of(s);
   L.gd.m = s->h * s->w * s->n;
   L.gd.splits = ad.splits;
   L.gd.beta = beta ? 1 : 0;
+  if (bnb) L.gd.bnb = *bnb;
   if (ad.splits > 1) {
     if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
     L.gd.cnt = static_cast<unsigned*>(wsd);

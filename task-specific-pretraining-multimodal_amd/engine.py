@@ -153,6 +153,9 @@ class EncoderEngine:
         # batch 128 the merge tail on the conv's critical path costs more than the finalize launch
         # (2.88 vs 2.83 ms per step)
         self.bn_two_level = os.environ.get("TSPM_BN_TWO_LEVEL", "0") == "1"
+        # BN-backward partial sums emitted by the producing dgrad's epilogue (small-row BatchNorms: one
+        # launch instead of partial + apply); TSPM_BN_DGRAD_FUSE=0 for the two-launch path (A/B)
+        self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "1") != "0"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -268,6 +271,11 @@ class EncoderEngine:
         self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_conv_aux = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
+        # BN-backward partial sums written by the producing dgrad's epilogue (tspm_conv_*_bnfuse) for the
+        # small-row BatchNorms: 3 planes of [<= max_tiles][C]
+        self.bnb_max_tiles = int(lib.tspm_bn_bwd_apply_max_tiles())
+        cmax = max(bn.channels for bn in self.all_bns())
+        self.bnb_part = torch.zeros(3 * self.bnb_max_tiles * cmax, device=self.device, dtype=torch.float32)
         # BN statistics merged in-launch (one or two levels, tspm_conv_fwd_bn_counters / _partial_floats)
         ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
         ncnt = max(op.bn_counters() for op in self.all_convs())
@@ -467,6 +475,32 @@ class EncoderEngine:
                                 bn.rows if dy_t is not None else 0, self.ws_bn.data_ptr(), self.ws_bn_bytes, sh),
                 "bn_bwd")
 
+    def _bn_bwd_apply(self, bn: BNOp, tiles: int, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None,
+                      dres=None, sh=0):
+        """tspm_bn_bwd with the partial sums already written by the producing dgrad (one launch)."""
+        m = bn.module
+        gw, gb = self._grad(m.weight), self._grad(m.bias)
+        m2 = bn2.module if bn2 is not None else None
+        gw2, gb2 = (self._grad(m2.weight), self._grad(m2.bias)) if m2 is not None else (None, None)
+        L.check(L.lib().tspm_bn_bwd_apply(
+            bn.rows, bn.channels, tiles, self.bnb_part.data_ptr(), g.data_ptr(), L.ptr(out_mask), y.data_ptr(),
+            bn.mean.data_ptr(), bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
+            L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
+            L.ptr(m2.weight) if m2 is not None else None, L.ptr(gw2), L.ptr(gb2), L.ptr(dy2), L.ptr(dres), sh),
+            "bn_bwd_apply")
+
+    def _bnb_for(self, op: ConvOp, out_mask, y, bn: BNOp, y2=None, bn2: Optional[BNOp] = None):
+        """(tspm_bn_bwd_fuse, tiles) when op's dgrad can emit bn's backward partial sums in its epilogue
+        (LDS-staged dgrad with <= max_tiles row tiles), else None."""
+        if not self.fuse_bnb or self.use_t:
+            return None
+        tiles = int(L.lib().tspm_conv_dgrad_bn_tiles(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad)))
+        if not (0 < tiles <= self.bnb_max_tiles):
+            return None
+        f = L.BnBwdFuse(self.bnb_part.data_ptr(), L.ptr(out_mask), y.data_ptr(), bn.mean.data_ptr(), L.ptr(y2),
+                        L.ptr(bn2.mean) if bn2 is not None else None)
+        return f, tiles
+
     def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int,
                x_t: Optional[torch.Tensor] = None, dy_t: Optional[torch.Tensor] = None) -> None:
         lib = L.lib()
@@ -497,7 +531,7 @@ class EncoderEngine:
             self.conv_timer.end()
 
     def _bwd_pair(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, dx: torch.Tensor, beta: int,
-                  sh: int) -> bool:
+                  sh: int, bnb=None) -> bool:
         """Input and weight gradient of ``op`` in one launch (tspm_conv_bwd: the two GEMMs read the same
         dy and are independent, so their workgroups share the grid).  False (nothing launched) when
         the pair is not built in, an auxiliary stream carries the weight gradients, or the transposed
@@ -515,20 +549,32 @@ class EncoderEngine:
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
         if self.conv_timer:
             self.conv_timer.begin(op, "bwd")
-        L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
-                                  x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
-                                  beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
-                                  self.ws_conv_aux.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
+        if bnb is not None:
+            L.check(lib.tspm_conv_bwd_bnfuse(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
+                                             ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides), dy.data_ptr(),
+                                             self._w(op).data_ptr(), dx.data_ptr(), beta, gw.data_ptr(),
+                                             self.ws_conv.data_ptr(), self.ws_conv_bytes, self.ws_conv_aux.data_ptr(),
+                                             self.ws_conv_bytes, ctypes.byref(bnb), sh), "conv_bwd_bnfuse")
+        else:
+            L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
+                                      x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
+                                      beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
+                                      self.ws_conv_aux.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
         if self.conv_timer:
             self.conv_timer.end()
         return True
 
-    def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
+    def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int, bnb=None) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "dgrad")
-        L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
-                                        self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
-                                        self.ws_conv_bytes, sh), "conv_dgrad")
+        if bnb is not None:
+            L.check(L.lib().tspm_conv_dgrad_bnfuse(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
+                                                   self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
+                                                   self.ws_conv_bytes, ctypes.byref(bnb), sh), "conv_dgrad_bnfuse")
+        else:
+            L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
+                                            self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
+                                            self.ws_conv_bytes, sh), "conv_dgrad")
         if self.conv_timer:
             self.conv_timer.end()
 
@@ -573,8 +619,9 @@ class EncoderEngine:
             L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(),
                                          sh), "avgpool_bwd")
             lo, hi = (self.split_block if phase == 1 else 0), len(self.blocks)
+            pend = None  # row tiles of the block-output BN's partial sums, written by the previous dgrad
         else:
-            G, Gn = self._bw_state
+            G, Gn, pend = self._bw_state
             lo, hi = 0, self.split_block
         for i in range(hi - 1, lo - 1, -1):
             bp = self.blocks[i]
@@ -588,19 +635,32 @@ class EncoderEngine:
             d2 = bp.g_y2
             if bp.ds_conv is not None:
                 dd = bp.g_yd
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh, dy_t=bp.g_y2_t,
-                             dy2_t=bp.g_yd_t)
+                if pend is not None:
+                    self._bn_bwd_apply(bp.bn2, pend, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+                else:
+                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh,
+                                 dy_t=bp.g_y2_t, dy2_t=bp.g_yd_t)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh, dy_t=bp.g_y2_t)
+                if pend is not None:
+                    self._bn_bwd_apply(bp.bn2, pend, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
+                else:
+                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh, dy_t=bp.g_y2_t)
+            pend = None
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
-            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh):
+            # conv2's input gradient is bn1's whole gradient: its epilogue emits bn1's backward partials
+            fb1 = self._bnb_for(bp.conv2, bp.a1, bp.y1, bp.bn1)
+            bnb1 = fb1[0] if fb1 else None
+            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, bnb1):
                 self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh, bp.a1_t, bp.g_y2_t)
-                self._dgrad(bp.conv2, d2, da1, 0, sh)
+                self._dgrad(bp.conv2, d2, da1, 0, sh, bnb1)
             d1 = bp.g_y1
-            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh, dy_t=bp.g_y1_t)
+            if fb1:
+                self._bn_bwd_apply(bp.bn1, fb1[1], da1, bp.a1, bp.y1, d1, sh=sh)
+            else:
+                self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh, dy_t=bp.g_y1_t)
             if self.debug_hook is not None:
                 self.debug_hook(f"block{i}.g_out", Gv)
                 self.debug_hook(f"block{i}.d_y2", d2)
@@ -611,12 +671,21 @@ class EncoderEngine:
             if bp.ds_conv is not None and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
                 self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh, xin_t, bp.g_yd_t)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
-            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh):
+            # conv1's input gradient accumulates last onto the previous block's output gradient: its epilogue
+            # emits that block's bn2 (+ downsample BN) backward partials
+            fb2 = None
+            if i > 0:
+                pb = self.blocks[i - 1]
+                fb2 = self._bnb_for(bp.conv1, pb.out, pb.y2, pb.bn2, pb.yd if pb.ds_conv is not None else None,
+                                    pb.ds_bn if pb.ds_conv is not None else None)
+            bnb2 = fb2[0] if fb2 else None
+            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, bnb2):
                 self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh, xin_t, bp.g_y1_t)
-                self._dgrad(bp.conv1, d1, Gnv, 1, sh)
+                self._dgrad(bp.conv1, d1, Gnv, 1, sh, bnb2)
+            pend = fb2[1] if fb2 else None
             G, Gn = Gn, G
         if phase == 1:
-            self._bw_state = (G, Gn)
+            self._bw_state = (G, Gn, pend)
             if self.aux is not None and self.join_aux:
                 torch.cuda.current_stream().wait_stream(self.aux)
             return
