@@ -250,9 +250,14 @@ def mmimdb_bench(args) -> None:
     B = args.mmimdb_batch
     torch.manual_seed(0)
     ie, te = M.MMIMDbModalityEncoder(4096, 512), M.MMIMDbModalityEncoder(300, 512)
-    gmu = M.GatedBiModalNetwork(input_one_dim=512, output_one_dim=512, input_two_dim=512, output_two_dim=512)
-    clf = M.MLPGenreClassifier(input_size=512, hidden_size=512, output_size=23)
-    model = M.MMIMDb(ie, te, gated_bimodal_network=gmu, classifier=clf).to(dev)
+    if args.mmimdb_pooling:  # configs/mmimdb/centralised/pooling/mmimdb_pooling_<kind>.yaml
+        clf = M.MLPGenreClassifier(input_size=512, hidden_size=512, output_size=23)
+        model = M.MMIMDb(ie, te, multimodal_pooling={"pooling_type": args.mmimdb_pooling, "hidden_dim": 512,
+                                                      "dropout": 0.1}, classifier=clf).to(dev)
+    else:
+        gmu = M.GatedBiModalNetwork(input_one_dim=512, output_one_dim=512, input_two_dim=512, output_two_dim=512)
+        clf = M.MLPGenreClassifier(input_size=512, hidden_size=512, output_size=23)
+        model = M.MMIMDb(ie, te, gated_bimodal_network=gmu, classifier=clf).to(dev)
     opt = tspm_amd.FusedAdam(model.parameters(), lr=1e-5, weight_decay=1e-3, grad_scale=1.0 / world)
     allreduce = None
     if world > 1:  # data parallel: one RCCL all-reduce of the flat gradient buffer (15.4 MB) per step
@@ -295,7 +300,9 @@ def mmimdb_bench(args) -> None:
            "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic MM-IMDb-shaped features (4096-d ReLU image, 300-d text, 23 multi-hot genres), 16 "
                    "batches resident in HBM; random-init weights (seed 0)",
-           "config": {"workload": "mmimdb_late_fusion_train_step(bn1d+linear encoders, gmu, maxout mlp, bce, adam)",
+           "config": {"workload": "mmimdb_late_fusion_train_step(bn1d+linear encoders, "
+                                  f"{('pooling_' + args.mmimdb_pooling) if args.mmimdb_pooling else 'gmu'}, "
+                                  "maxout mlp, bce, adam)",
                       "per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}", "params": nparam},
            "roofline": {"bound": "mfma", "kernel": "whole step (k_gemm_small MFMA products dominate the FLOPs)",
                         "achieved": round(tf, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -308,7 +315,8 @@ def mmimdb_bench(args) -> None:
         from oracle.avmnist_ref import OracleAdam
         threads, hcpu = cpu_threads()
         torch.set_num_threads(threads)
-        ref = orc.build_oracle_mmimdb(0)
+        ref = orc.build_oracle_mmimdb(0, pooling=None if not args.mmimdb_pooling else {
+            "pooling_type": args.mmimdb_pooling, "hidden_dim": 512, "dropout": 0.1})
         ropt = OracleAdam(list(ref.parameters()), lr=1e-5, weight_decay=1e-3)
         I, T, y = orc.synthetic_batch(B, seed=1234)
         orc.train_step(ref, ropt, I, T, y)
@@ -809,6 +817,8 @@ def main() -> None:
     ap.add_argument("--mono-batch", type=int, default=256)
     ap.add_argument("--mmimdb", action="store_true", help="BASELINE configs[3]: MMIMDb late-fusion step (one JSON line)")
     ap.add_argument("--mmimdb-batch", type=int, default=256)
+    ap.add_argument("--mmimdb-pooling", default=None, choices=["max", "avg", "sum", "attention", "gated"],
+                    help="--mmimdb with multimodal_pooling fusion instead of the GMU")
     ap.add_argument("--mosi", action="store_true", help="BASELINE configs[4]: MOSI UTT-Fusion step (one JSON line)")
     ap.add_argument("--mosi-batch", type=int, default=128)
     ap.add_argument("--mosi-corpus", type=int, default=4096, help="samples in the HBM-resident MOSI corpus")

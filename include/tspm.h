@@ -438,6 +438,28 @@ int tspm_gmu_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const float*
  * the gate pre-activation; hidden_sigmoid.weight.grad = ds^T @ h via tspm_linear_bwd_weight). */
 int tspm_gmu_bwd(int32_t n, int32_t d, const float* dz, int32_t lddz, const float* h, int32_t ldh,
                  const float* gate, const float* wz, float* du, int32_t lddu, float* ds, tspm_stream_t stream);
+/* MultimodalPooling (ABI 13; models/pooling.py:6-127), the MMIMDb `multimodal_pooling` fusion.
+ * u = [proj_a(x_a) | proj_b(x_b)] [n, 2d] from the small GEMM (with biases).
+ * tspm_pool_act_fwd: tu = tanh(u), ab = tu * keep * keep_scale ([n, 2d] contiguous; keep nullable =
+ *   no dropout; the module's one Dropout draws a and b independently).
+ * tspm_pool_mix_fwd: z = max(a, b) (kind 0, NaN-propagating) / (a + b) / 2 (1) / a + b (2) /
+ *   attention (3: w = softmax(W2 tanh(hpre) + b2), z = w0 a + w1 b) / gated (4: g = sigmoid(W2
+ *   tanh(hpre) + b2), z = g a + (1 - g) b); hpre [n, hd] = the scoring MLP's first Linear (+ bias) of
+ *   [a | b] (small GEMM); hh receives tanh(hpre), wts [n][2] the mixing weights (kinds 3-4).
+ * tspm_pool_mix_bwd: dab [n, 2d] through the mix (max: ties split the gradient in half, as torch.maximum);
+ *   kinds 3-4 also ds [n, 2 | 1] (scores' gradient: W2 grad = ds^T hh, b2 grad = column sums) and
+ *   dhpre [n, hd] (through W2 and the tanh).
+ * tspm_pool_act_bwd: du = (dab + dab2) * keep * keep_scale * (1 - tu^2) (dab2 nullable: the scoring
+ *   MLP's input gradient). */
+int tspm_pool_act_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const uint8_t* keep, float keep_scale,
+                      float* tu, float* ab, tspm_stream_t stream);
+int tspm_pool_mix_fwd(int32_t n, int32_t d, int32_t hd, int32_t kind, const float* ab, const float* hpre, float* hh,
+                      const float* w2, const float* b2, float* wts, float* z, int32_t ldz, tspm_stream_t stream);
+int tspm_pool_mix_bwd(int32_t n, int32_t d, int32_t hd, int32_t kind, const float* dz, int32_t lddz, const float* ab,
+                      const float* hh, const float* w2, const float* wts, float* dab, float* ds, float* dhpre,
+                      tspm_stream_t stream);
+int tspm_pool_act_bwd(int32_t n, int32_t d, const float* dab, const float* dab2, const float* tu, const uint8_t* keep,
+                      float keep_scale, float* du, tspm_stream_t stream);
 /* MaxOut(num_units=2) (models/maxout.py) + the Dropout after it (models/mmimdb.py:40-45): a[n,2d] is
  * the product with both units' weights stacked ([2d, in] — layers.0.weight then layers.1.weight);
  * y = max(a[:, :d], a[:, d:]) * (keep ? keep_scale : 0)  (keep NULL: no dropout). */

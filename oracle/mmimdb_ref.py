@@ -8,6 +8,8 @@ Restates, with plain ``torch.nn`` / ``torch.nn.functional`` on the CPU:
                                  g*h1 + (1-g)*h2, no biases                    (models/gates/gated_bimodal.py)
   * ``MLPGenreClassifier``     = BN → MaxOut(2, no bias) → Dropout(.5) → BN → MaxOut → Dropout → BN → Linear
                                                                                (models/mmimdb.py:20-60, models/maxout.py)
+  * ``MultimodalPooling``     = proj_a/proj_b → tanh → dropout, max/avg/sum/attention/gated pooling
+                                                                               (models/pooling.py:6-127)
   * ``MMIMDb.forward`` / ``train_step``: BCEWithLogits(mean) × weight 1.0, Adam (lr 1e-5, wd 1e-3)
                                                                                (models/mmimdb.py:164-245,
                                                                                 configs/mmimdb/centralised/mmimdb_baseline.yaml)
@@ -85,6 +87,56 @@ class OracleGMU(nn.Module):
         return g.view(g.size(0), 1) * h1 + (1 - g).view(g.size(0), 1) * h2
 
 
+class OracleMultimodalPooling(nn.Module):
+    """models/pooling.py:6-127 (MultimodalPooling): proj_a / proj_b → tanh → dropout (one module, two
+    independent draws), then max / avg / sum / attention (Linear → tanh → Linear(·, 2) → softmax) /
+    gated (Linear → tanh → Linear(·, 1) → sigmoid) pooling.  Module names, construction order and
+    state_dict keys as the reference's."""
+
+    def __init__(self, da: int, db: int, out: int, pooling_type: str = "gated", hidden_dim: Optional[int] = None,
+                 dropout: float = 0.0):
+        super().__init__()
+        self.pooling_type = pooling_type.lower()
+        self.hidden_dim = hidden_dim or max(da, db)
+        self.dropout = dropout
+        self.proj_a = nn.Linear(da, out)
+        self.proj_b = nn.Linear(db, out)
+        self.dropout_layer = nn.Dropout(dropout) if dropout > 0 else nn.Identity()
+        self.activation = nn.Tanh()
+        if self.pooling_type == "attention":
+            self.attention_layer = nn.Sequential(nn.Linear(out * 2, self.hidden_dim), nn.Tanh(),
+                                                 nn.Linear(self.hidden_dim, 2), nn.Softmax(dim=1))
+        elif self.pooling_type == "gated":
+            self.gate_layer = nn.Sequential(nn.Linear(out * 2, self.hidden_dim), nn.Tanh(),
+                                            nn.Linear(self.hidden_dim, 1), nn.Sigmoid())
+
+    def forward(self, x_a, x_b, keep_a=None, keep_b=None, trace=None):
+        a = self.activation(self.proj_a(x_a))
+        b = self.activation(self.proj_b(x_b))
+        if self.training and self.dropout > 0:
+            if keep_a is None:
+                a, b = self.dropout_layer(a), self.dropout_layer(b)
+            else:
+                s = 1.0 / (1.0 - self.dropout)
+                a = a * (keep_a.to(a.dtype) * s)
+                b = b * (keep_b.to(b.dtype) * s)
+        t = self.pooling_type
+        if t == "max":
+            return trace.maxout("pool", a, b) if trace is not None else torch.max(a, b)
+        if t in ("avg", "average"):
+            return (a + b) / 2
+        if t == "sum":
+            return a + b
+        combined = torch.cat([a, b], dim=1)
+        if t == "attention":
+            s = self.attention_layer(combined)
+            return s[:, 0].unsqueeze(1).expand_as(a) * a + s[:, 1].unsqueeze(1).expand_as(b) * b
+        if t == "gated":
+            g = self.gate_layer(combined)
+            return g * a + (1 - g) * b
+        raise ValueError(f"Unknown pooling type: {t}")
+
+
 class OracleClassifier(nn.Module):
     def __init__(self, i: int, o: int, h: int):
         super().__init__()
@@ -109,15 +161,34 @@ def _dropout(x, keep, training):
 
 
 class OracleMMIMDb(nn.Module):
-    def __init__(self, image_dim=IMAGE_DIM, text_dim=TEXT_DIM, embed=EMBED, hidden=HIDDEN, genres=GENRES):
+    """``pooling`` (the YAML's ``multimodal_pooling`` dict) replaces the GMU: the reference builds the
+    encoders and the classifier from the YAML first and MultimodalPooling inside MMIMDb.__init__
+    (models/mmimdb.py:128-141), which is the seeded construction order reproduced here."""
+
+    def __init__(self, image_dim=IMAGE_DIM, text_dim=TEXT_DIM, embed=EMBED, hidden=HIDDEN, genres=GENRES,
+                 pooling: Optional[Dict] = None):
         super().__init__()
         self.image_model = OracleEncoder(image_dim, embed)
         self.text_model = OracleEncoder(text_dim, embed)
-        self.fusion_module = OracleGMU(embed, embed, embed, embed)
-        self.mm_mlp = OracleClassifier(embed, genres, hidden)
+        if pooling is None:
+            self.fusion_module = OracleGMU(embed, embed, embed, embed)
+            self.mm_mlp = OracleClassifier(embed, genres, hidden)
+            self.fusion_type = "gated"
+        else:
+            clf = OracleClassifier(embed, genres, hidden)
+            self.fusion_module = OracleMultimodalPooling(embed, embed, embed, pooling.get("pooling_type", "gated"),
+                                                         pooling.get("hidden_dim"), pooling.get("dropout", 0.0))
+            self.mm_mlp = clf
+            self.fusion_type = "pooling"
 
-    def forward(self, I, T, keep1=None, keep2=None, trace=None):
-        return self.mm_mlp(self.fusion_module(self.image_model(I), self.text_model(T)), keep1, keep2, trace)
+    def forward(self, I, T, keep1=None, keep2=None, trace=None, keep_pool=None):
+        a, b = self.image_model(I), self.text_model(T)
+        if self.fusion_type == "pooling":
+            ka, kb = (None, None) if keep_pool is None else keep_pool
+            z = self.fusion_module(a, b, ka, kb, trace)
+        else:
+            z = self.fusion_module(a, b)
+        return self.mm_mlp(z, keep1, keep2, trace)
 
 
 def build_oracle_mmimdb(seed: int = 0, **dims) -> OracleMMIMDb:
@@ -142,13 +213,13 @@ def bce_loss(logits, labels):
 
 
 def train_step(model: OracleMMIMDb, opt, image, text, labels, keep1=None, keep2=None,
-               trace: Optional[MaxOutTrace] = None) -> Dict[str, torch.Tensor]:
+               trace: Optional[MaxOutTrace] = None, keep_pool=None) -> Dict[str, torch.Tensor]:
     """models/mmimdb.py:203-245 (minus the host metric recorder): zero_grad, forward, BCE, backward, Adam
     (``opt=None``: gradients only)."""
     model.train()
     for p in model.parameters():
         p.grad = None
-    logits = model(image, text, keep1, keep2, trace)
+    logits = model(image, text, keep1, keep2, trace, keep_pool)
     loss = bce_loss(logits, labels)
     loss.backward()
     if opt is not None:

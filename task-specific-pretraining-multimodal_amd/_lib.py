@@ -150,6 +150,10 @@ _SIGS = {
                                           _P]),
     "tspm_reduce_slabs": (c_int32, [c_int64, c_int32, c_int64, _P, _P, _P]),
     "tspm_gmu_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _P, c_int32, _P]),
+    "tspm_pool_act_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_float, _P, _P, _P]),
+    "tspm_pool_mix_fwd": (c_int32, [c_int32, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, c_int32, _P]),
+    "tspm_pool_mix_bwd": (c_int32, [c_int32, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tspm_pool_act_bwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_gmu_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, c_int32, _P, _P]),
     "tspm_maxout_fwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
     "tspm_maxout_fwd_rng": (c_int32, [c_int32, c_int32, _P, c_int32, c_float, c_uint64, _P, c_int64, _P, c_float, _P,

@@ -374,6 +374,147 @@ int ew_grid(long long work) {
   return (int)(b < 1 ? 1 : b);
 }
 
+// ------------------------------------------------------------------------------------------------
+// MultimodalPooling (models/pooling.py:6-127): u = [proj_a(x_a) | proj_b(x_b)] [n, 2d] (+ bias, from
+// the small GEMM), a | b = dropout(tanh(u)) (one Dropout module, two draws: keep [n, 2d]), then
+// kind 0 max / 1 avg / 2 sum / 3 attention / 4 gated.  Attention and gated run their scoring MLP's
+// first Linear (+ bias) on the small GEMM into hpre [n, hd]; tanh, the second Linear (hd -> 2 / 1 +
+// bias), softmax / sigmoid and the mix run here, one workgroup per row, fixed-order block sums.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pool_act_fwd(long long total, int d2, const float* __restrict__ u, int ldu,
+                                                      const uint8_t* __restrict__ keep, float scale,
+                                                      float* __restrict__ tu, float* __restrict__ ab) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long r = e / d2;
+    const int j = (int)(e - r * d2);
+    const float t = tanhf(u[r * ldu + j]);
+    tu[e] = t;
+    ab[e] = keep ? t * (keep[e] ? scale : 0.f) : t;
+  }
+}
+
+__global__ __launch_bounds__(kRowThreads) void k_pool_mix_fwd(int d, int hd, int kind, const float* __restrict__ ab,
+                                                              const float* __restrict__ hpre, float* __restrict__ hh,
+                                                              const float* __restrict__ w2, const float* __restrict__ b2,
+                                                              float* __restrict__ wts, float* __restrict__ z, int ldz) {
+  __shared__ float red[kRowThreads / 64];
+  const long long r = blockIdx.x;
+  const float* a = ab + r * 2 * d;
+  const float* b = a + d;
+  float* zr = z + r * ldz;
+  if (kind <= 2) {
+    for (int j = threadIdx.x; j < d; j += kRowThreads) {
+      const float x = a[j], y = b[j];
+      zr[j] = kind == 0 ? ((x > y || x != x) ? x : y) : (kind == 1 ? (x + y) / 2.f : x + y);
+    }
+    return;
+  }
+  const float* hp = hpre + r * hd;
+  float* hr = hh + r * hd;
+  float s0 = 0.f, s1 = 0.f;
+  for (int j = threadIdx.x; j < hd; j += kRowThreads) {
+    const float t = tanhf(hp[j]);
+    hr[j] = t;
+    s0 = fmaf(w2[j], t, s0);
+    if (kind == 3) s1 = fmaf(w2[hd + j], t, s1);
+  }
+  s0 = block_sum(s0, red) + b2[0];
+  float wa, wb;
+  if (kind == 3) {
+    s1 = block_sum(s1, red) + b2[1];
+    const float m = fmaxf(s0, s1);
+    const float e0 = expf(s0 - m), e1 = expf(s1 - m);
+    const float inv = 1.f / (e0 + e1);
+    wa = e0 * inv;
+    wb = e1 * inv;
+  } else {
+    wa = 1.f / (1.f + expf(-s0));
+    wb = 1.f - wa;
+  }
+  if (threadIdx.x == 0) {
+    wts[2 * r] = wa;
+    wts[2 * r + 1] = wb;
+  }
+  for (int j = threadIdx.x; j < d; j += kRowThreads) zr[j] = wa * a[j] + wb * b[j];
+}
+
+// dz -> dab [n, 2d] through the mix; attention / gated also: ds [n, k] (scores' gradient, for the
+// second Linear's weight gradient ds^T @ hh) and dhpre [n, hd] (through that Linear and the tanh).
+__global__ __launch_bounds__(kRowThreads) void k_pool_mix_bwd(int d, int hd, int kind, const float* __restrict__ dz,
+                                                              int lddz, const float* __restrict__ ab,
+                                                              const float* __restrict__ hh, const float* __restrict__ w2,
+                                                              const float* __restrict__ wts, float* __restrict__ dab,
+                                                              float* __restrict__ ds, float* __restrict__ dhpre) {
+  __shared__ float red[kRowThreads / 64];
+  const long long r = blockIdx.x;
+  const float* a = ab + r * 2 * d;
+  const float* b = a + d;
+  const float* g = dz + r * lddz;
+  float* da = dab + r * 2 * d;
+  float* db = da + d;
+  if (kind <= 2) {
+    for (int j = threadIdx.x; j < d; j += kRowThreads) {
+      const float gv = g[j];
+      if (kind == 0) {  // torch.maximum's derivative: ties split the gradient in half
+        const float x = a[j], y = b[j];
+        const float h = gv / 2.f;
+        da[j] = x == y ? h : (x > y ? gv : 0.f);
+        db[j] = x == y ? h : (y > x ? gv : 0.f);
+      } else {
+        const float v = kind == 1 ? gv / 2.f : gv;
+        da[j] = v;
+        db[j] = v;
+      }
+    }
+    return;
+  }
+  const float wa = wts[2 * r], wb = wts[2 * r + 1];
+  float pa = 0.f, pb = 0.f;
+  for (int j = threadIdx.x; j < d; j += kRowThreads) {
+    const float gv = g[j];
+    pa = fmaf(gv, a[j], pa);
+    pb = fmaf(gv, b[j], pb);
+    da[j] = wa * gv;
+    db[j] = wb * gv;
+  }
+  pa = block_sum(pa, red);
+  pb = block_sum(pb, red);
+  float d0, d1 = 0.f;
+  if (kind == 3) {  // softmax backward over the two scores
+    const float dot = wa * pa + wb * pb;
+    d0 = wa * (pa - dot);
+    d1 = wb * (pb - dot);
+  } else {          // z = g a + (1 - g) b: dg = sum dz (a - b); sigmoid backward
+    d0 = (pa - pb) * wa * (1.f - wa);
+  }
+  if (threadIdx.x == 0) {
+    ds[r * (kind == 3 ? 2 : 1)] = d0;
+    if (kind == 3) ds[r * 2 + 1] = d1;
+  }
+  const float* hr = hh + r * hd;
+  float* dh = dhpre + r * hd;
+  for (int j = threadIdx.x; j < hd; j += kRowThreads) {
+    float v = d0 * w2[j];
+    if (kind == 3) v = fmaf(d1, w2[hd + j], v);
+    const float t = hr[j];
+    dh[j] = v * (1.f - t * t);
+  }
+}
+
+// du = (dab [+ dab2]) * keep * scale * (1 - tanh(u)^2)
+__global__ __launch_bounds__(256) void k_pool_act_bwd(long long total, const float* __restrict__ dab,
+                                                      const float* __restrict__ dab2, const float* __restrict__ tu,
+                                                      const uint8_t* __restrict__ keep, float scale,
+                                                      float* __restrict__ du) {
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    float v = dab[e];
+    if (dab2) v += dab2[e];
+    if (keep) v = v * (keep[e] ? scale : 0.f);
+    const float t = tu[e];
+    du[e] = v * (1.f - t * t);
+  }
+}
+
 }  // namespace
 
 extern "C" int tspm_gmu_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const float* wz, float* h,
@@ -502,6 +643,48 @@ extern "C" int tspm_maxout_fwd_rng(int32_t n, int32_t d, const float* a, int32_t
   hipLaunchKernelGGL(k_maxout_fwd_rng, dim3(ew_grid((long long)n * d)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      n, d, a, lda, p, (unsigned long long)seed, counter, (long long)index_offset, keep, keep_scale, y,
                      ldy);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_pool_act_fwd(int32_t n, int32_t d, const float* u, int32_t ldu, const uint8_t* keep, float keep_scale,
+                                 float* tu, float* ab, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || ldu < 2 * d || !u || !tu || !ab) return TSPM_ERR_INVALID;
+  const long long total = (long long)n * 2 * d;
+  hipLaunchKernelGGL(k_pool_act_fwd, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, 2 * d,
+                     u, ldu, keep, keep_scale, tu, ab);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_pool_mix_fwd(int32_t n, int32_t d, int32_t hd, int32_t kind, const float* ab, const float* hpre,
+                                 float* hh, const float* w2, const float* b2, float* wts, float* z, int32_t ldz,
+                                 tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || kind < 0 || kind > 4 || ldz < d || !ab || !z) return TSPM_ERR_INVALID;
+  if (kind >= 3 && (hd <= 0 || !hpre || !hh || !w2 || !b2 || !wts)) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_pool_mix_fwd, dim3(n), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), d, hd, kind, ab,
+                     hpre, hh, w2, b2, wts, z, ldz);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_pool_mix_bwd(int32_t n, int32_t d, int32_t hd, int32_t kind, const float* dz, int32_t lddz,
+                                 const float* ab, const float* hh, const float* w2, const float* wts, float* dab,
+                                 float* ds, float* dhpre, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || kind < 0 || kind > 4 || lddz < d || !dz || !ab || !dab) return TSPM_ERR_INVALID;
+  if (kind >= 3 && (hd <= 0 || !hh || !w2 || !wts || !ds || !dhpre)) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_pool_mix_bwd, dim3(n), dim3(kRowThreads), 0, static_cast<hipStream_t>(stream), d, hd, kind, dz,
+                     lddz, ab, hh, w2, wts, dab, ds, dhpre);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_pool_act_bwd(int32_t n, int32_t d, const float* dab, const float* dab2, const float* tu,
+                                 const uint8_t* keep, float keep_scale, float* du, tspm_stream_t stream) {
+  if (n <= 0 || d <= 0 || !dab || !tu || !du) return TSPM_ERR_INVALID;
+  const long long total = (long long)n * 2 * d;
+  hipLaunchKernelGGL(k_pool_act_bwd, dim3(ew_grid(total)), dim3(256), 0, static_cast<hipStream_t>(stream), total, dab,
+                     dab2, tu, keep, keep_scale, du);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

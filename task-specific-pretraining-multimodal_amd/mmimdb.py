@@ -16,8 +16,9 @@ BCEWithLogits = ``tspm_gmu_*``, ``tspm_maxout_*``, ``tspm_bce_logits``, Adam = `
 ``FusedMMIMDbStep`` captures forward + loss + backward + Adam in one HIP graph.  No CPU or ATen
 fallback: a CPU tensor raises ``TspmError``.
 
-Supported configuration = the reference's MMIMDb configs: GMU fusion (``multimodal_pooling`` is
-rejected), MaxOut with 2 units and no bias, Dropout 0.5, biasless GMU.
+Supported configuration = the reference's MMIMDb configs: GMU fusion or ``multimodal_pooling``
+(``MultimodalPooling``, models/pooling.py: max / avg / sum / attention / gated; ``tspm_pool_*``),
+MaxOut with 2 units and no bias, Dropout 0.5, biasless GMU.
 """
 from __future__ import annotations
 
@@ -88,6 +89,45 @@ class GatedBiModalNetwork(nn.Module):
         raise L.TspmError("GatedBiModalNetwork runs inside MMIMDb's HIP engine (call the MMIMDb model)")
 
 
+POOLING_KINDS = {"max": 0, "avg": 1, "average": 1, "sum": 2, "attention": 3, "gated": 4}
+
+
+class MultimodalPooling(nn.Module):
+    """models/pooling.py:6-127 parameter container (same construction order and state_dict keys):
+    proj_a / proj_b, Dropout, Tanh, and the attention (Linear → Tanh → Linear(·, 2) → Softmax) or gate
+    (Linear → Tanh → Linear(·, 1) → Sigmoid) scoring MLP; the engine runs it (tspm_pool_*)."""
+
+    def __init__(self, input_dim_a: int, input_dim_b: int, output_dim: int, pooling_type: str = "gated",
+                 hidden_dim: Optional[int] = None, dropout: float = 0.0):
+        super().__init__()
+        self.pooling_type = pooling_type.lower()
+        if self.pooling_type not in POOLING_KINDS:
+            raise ValueError(f"Unknown pooling type: {self.pooling_type}")
+        self.input_dim_a, self.input_dim_b, self.output_dim = input_dim_a, input_dim_b, output_dim
+        self.hidden_dim = hidden_dim or max(input_dim_a, input_dim_b)
+        self.dropout = dropout
+        self.proj_a = nn.Linear(input_dim_a, output_dim)
+        self.proj_b = nn.Linear(input_dim_b, output_dim)
+        self.dropout_layer = nn.Dropout(dropout) if dropout > 0 else nn.Identity()
+        self.activation = nn.Tanh()
+        if self.pooling_type == "attention":
+            self.attention_layer = nn.Sequential(nn.Linear(output_dim * 2, self.hidden_dim), nn.Tanh(),
+                                                 nn.Linear(self.hidden_dim, 2), nn.Softmax(dim=1))
+        elif self.pooling_type == "gated":
+            self.gate_layer = nn.Sequential(nn.Linear(output_dim * 2, self.hidden_dim), nn.Tanh(),
+                                            nn.Linear(self.hidden_dim, 1), nn.Sigmoid())
+
+    @property
+    def kind(self) -> int:
+        return POOLING_KINDS[self.pooling_type]
+
+    def scorer(self) -> Optional[nn.Sequential]:
+        return getattr(self, "attention_layer", None) or getattr(self, "gate_layer", None)
+
+    def forward(self, a, b):  # pragma: no cover - the engine runs the fusion
+        raise L.TspmError("MultimodalPooling runs inside the MMIMDb HIP engine")
+
+
 class MLPGenreClassifier(nn.Module):
     """models/mmimdb.py:20-60."""
 
@@ -137,11 +177,19 @@ class MMIMDbEngine:
         ie, te, gmu, clf = model.image_model, model.text_model, model.fusion_module, model.mm_mlp
         self.di, self.dt = ie.net[0].num_features, te.net[0].num_features
         self.e = ie.net[1].out_features
-        if te.net[1].out_features != self.e or gmu.fc_one.in_features != self.e or gmu.fc_two.in_features != self.e:
-            raise L.TspmError("MMIMDb HIP engine: both encoders and the GMU inputs must share one width")
-        self.d = gmu.fc_one.out_features
-        if gmu.fc_two.out_features != self.d or gmu.use_bias:
-            raise L.TspmError("MMIMDb HIP engine: GMU outputs must match and carry no bias")
+        self.pool = gmu if model.fusion_type == "pooling" else None
+        if self.pool is not None:
+            if te.net[1].out_features != self.e or self.pool.proj_a.in_features != self.e:
+                raise L.TspmError("MMIMDb HIP engine: both encoders must share one width")
+            self.d = self.pool.output_dim
+            self.hd = self.pool.hidden_dim
+            self.pool_p = float(self.pool.dropout)
+        else:
+            if te.net[1].out_features != self.e or gmu.fc_one.in_features != self.e or gmu.fc_two.in_features != self.e:
+                raise L.TspmError("MMIMDb HIP engine: both encoders and the GMU inputs must share one width")
+            self.d = gmu.fc_one.out_features
+            if gmu.fc_two.out_features != self.d or gmu.use_bias:
+                raise L.TspmError("MMIMDb HIP engine: GMU outputs must match and carry no bias")
         if clf.input_size != self.d:
             raise L.TspmError("MMIMDb HIP engine: classifier input_size must equal the GMU output width")
         self.h, self.c = clf.hidden_size, clf.output_size
@@ -167,6 +215,12 @@ class MMIMDbEngine:
             z(n, h), z(n, 2 * h)
         self.dZn, self.dZ, self.dU, self.ds = z(n, d), z(n, d), z(n, 2 * d), z(n)
         self.dEI, self.dET = z(n, e), z(n, e)
+        if self.pool is not None:  # U = [proj_a | proj_b], TU = tanh(U), H = dropout(TU) = [a | b]
+            hd = self.hd
+            self.TU, self.Hpre, self.Hh, self.wts = z(n, 2 * d), z(n, hd), z(n, hd), z(n, 2)
+            self.dAB2, self.dS, self.dHpre = z(n, 2 * d), z(n, 2), z(n, hd)
+            self.keep_pool = torch.ones(n, 2 * d, dtype=torch.uint8, device=device)
+            self.pool_keep_override: Optional[torch.Tensor] = None
         self.dXn, self.dXnT = z(n, self.di), z(n, self.dt)
         # TSPM_MMIMDB_STREAMS=2: text branch on a side stream (forward: text encoder + fc_two; backward:
         # their gradients), joined by events before the gate / at the end of the backward.  Measured
@@ -293,26 +347,32 @@ class MMIMDbEngine:
             L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
                                                ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e,
                                                self.enc_splits, self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
-            L.check(lib.tspm_linear_fwd_pair(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(),
-                                             self.U.data_ptr(), 2 * d, self.ET.data_ptr(), e,
-                                             gmu.fc_two.weight.data_ptr(), self.U.data_ptr() + d * 4, 2 * d, sh),
-                    "gmu fc_one/fc_two")
+            if self.pool is None:
+                L.check(lib.tspm_linear_fwd_pair(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(),
+                                                 self.U.data_ptr(), 2 * d, self.ET.data_ptr(), e,
+                                                 gmu.fc_two.weight.data_ptr(), self.U.data_ptr() + d * 4, 2 * d, sh),
+                        "gmu fc_one/fc_two")
         else:
             st = self._fork()
             bn_s("t", te[0], self.T, self.dt, self.XnT, st)
             L.check(lib.tspm_linear_fwd(n, self.dt, e, self.XnT.data_ptr(), self.dt, te[1].weight.data_ptr(),
                                         te[1].bias.data_ptr(), 0, None, 1.0, self.ET.data_ptr(), e, st), "text fc")
-            L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, gmu.fc_two.weight.data_ptr(), None, 0, None,
-                                        1.0, self.U.data_ptr() + d * 4, 2 * d, st), "gmu fc_two")
+            if self.pool is None:
+                L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, gmu.fc_two.weight.data_ptr(), None, 0,
+                                            None, 1.0, self.U.data_ptr() + d * 4, 2 * d, st), "gmu fc_two")
             bn("i", ie[0], self.I, self.di, self.XnI)
             L.check(lib.tspm_linear_fwd_splitk(n, self.di, e, self.XnI.data_ptr(), self.di, ie[1].weight.data_ptr(),
                                                ie[1].bias.data_ptr(), 0, None, 1.0, self.EI.data_ptr(), e,
                                                self.enc_splits, self.ws.data_ptr(), self.ws_bytes, sh), "image fc")
-            L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(), None, 0, None,
-                                        1.0, self.U.data_ptr(), 2 * d, sh), "gmu fc_one")
+            if self.pool is None:
+                L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, gmu.fc_one.weight.data_ptr(), None, 0,
+                                            None, 1.0, self.U.data_ptr(), 2 * d, sh), "gmu fc_one")
             self._join()
-        L.check(lib.tspm_gmu_fwd(n, d, self.U.data_ptr(), 2 * d, gmu.hidden_sigmoid.weight.data_ptr(),
-                                 self.H.data_ptr(), 2 * d, self.gate.data_ptr(), self.Z.data_ptr(), d, sh), "gmu")
+        if self.pool is None:
+            L.check(lib.tspm_gmu_fwd(n, d, self.U.data_ptr(), 2 * d, gmu.hidden_sigmoid.weight.data_ptr(),
+                                     self.H.data_ptr(), 2 * d, self.gate.data_ptr(), self.Z.data_ptr(), d, sh), "gmu")
+        else:
+            self._pool_fwd(sh, train)
         # classifier (models/mmimdb.py:38-47)
         keep, k1, k2, scale = None, None, None, 1.0
         # in-launch masks: each MaxOut forward draws its half of the mask tspm_dropout_mask would write
@@ -340,6 +400,60 @@ class MMIMDbEngine:
         bn("b2", net[6], self.Y2, h, self.Y2n)
         L.check(lib.tspm_linear_fwd(n, h, c, self.Y2n.data_ptr(), h, net[7].weight.data_ptr(), net[7].bias.data_ptr(),
                                     0, None, 1.0, self.logits.data_ptr(), c, sh), "output fc")
+
+    _POOL_SEED_MIX = 0x5DEECE66D  # the pooling dropout's stream, distinct from the classifier's
+
+    def _pool_fwd(self, sh: int, train: bool) -> None:
+        """MultimodalPooling (models/pooling.py:81-127): [proj_a | proj_b] (+ biases) → tanh → dropout →
+        max / avg / sum, or the attention / gate scoring MLP → softmax / sigmoid mix."""
+        lib, pl = L.lib(), self.pool
+        n, e, d, hd = self.n, self.e, self.d, self.hd
+        L.check(lib.tspm_linear_fwd(n, e, d, self.EI.data_ptr(), e, pl.proj_a.weight.data_ptr(),
+                                    pl.proj_a.bias.data_ptr(), 0, None, 1.0, self.U.data_ptr(), 2 * d, sh), "proj_a")
+        L.check(lib.tspm_linear_fwd(n, e, d, self.ET.data_ptr(), e, pl.proj_b.weight.data_ptr(),
+                                    pl.proj_b.bias.data_ptr(), 0, None, 1.0, self.U.data_ptr() + d * 4, 2 * d, sh),
+                "proj_b")
+        keep, scale = None, 1.0
+        if train and self.pool_p > 0:
+            scale = 1.0 / (1.0 - self.pool_p)
+            if self.pool_keep_override is None:
+                L.check(lib.tspm_dropout_mask(n * 2 * d, self.pool_p,
+                                              (self.model._rng_seed ^ self._POOL_SEED_MIX) & ((1 << 63) - 1),
+                                              self.rng_ctr_ptr, self.keep_pool.data_ptr(), sh), "pool dropout_mask")
+            keep = self.keep_pool.data_ptr()
+        L.check(lib.tspm_pool_act_fwd(n, d, self.U.data_ptr(), 2 * d, keep, scale, self.TU.data_ptr(),
+                                      self.H.data_ptr(), sh), "pool tanh+dropout")
+        kind, sc = pl.kind, pl.scorer()
+        if kind >= 3:
+            L.check(lib.tspm_linear_fwd(n, 2 * d, hd, self.H.data_ptr(), 2 * d, sc[0].weight.data_ptr(),
+                                        sc[0].bias.data_ptr(), 0, None, 1.0, self.Hpre.data_ptr(), hd, sh), "pool score fc")
+        L.check(lib.tspm_pool_mix_fwd(n, d, hd, kind, self.H.data_ptr(), self.Hpre.data_ptr(), self.Hh.data_ptr(),
+                                      sc[2].weight.data_ptr() if kind >= 3 else None,
+                                      sc[2].bias.data_ptr() if kind >= 3 else None, self.wts.data_ptr(),
+                                      self.Z.data_ptr(), d, sh), "pool mix")
+
+    def _pool_bwd(self, sh: int) -> None:
+        """Backward of _pool_fwd: dZ → d[a | b] (+ the scoring MLP's gradients) → dU."""
+        lib, pl = L.lib(), self.pool
+        n, d, hd = self.n, self.d, self.hd
+        kind, sc = pl.kind, pl.scorer()
+        g = lambda p: p.grad.data_ptr()  # noqa: E731
+        L.check(lib.tspm_pool_mix_bwd(n, d, hd, kind, self.dZ.data_ptr(), d, self.H.data_ptr(), self.Hh.data_ptr(),
+                                      sc[2].weight.data_ptr() if kind >= 3 else None, self.wts.data_ptr(),
+                                      self.dU.data_ptr(), self.dS.data_ptr(), self.dHpre.data_ptr(), sh), "pool mix bwd")
+        dab2 = None
+        if kind >= 3:
+            k = 2 if kind == 3 else 1
+            L.check(lib.tspm_linear_bwd_weight(n, hd, k, self.Hh.data_ptr(), hd, self.dS.data_ptr(), k,
+                                               g(sc[2].weight), g(sc[2].bias), sh), "pool score fc2 dW")
+            linear_bwd(n, 2 * d, hd, self.H.data_ptr(), 2 * d, self.dHpre.data_ptr(), hd, sc[0].weight.data_ptr(),
+                       g(sc[0].weight), g(sc[0].bias), self.dAB2.data_ptr(), 2 * d, sh)
+            dab2 = self.dAB2.data_ptr()
+        keep = self.keep_pool.data_ptr() if self.pool_p > 0 else None
+        scale = 1.0 / (1.0 - self.pool_p) if self.pool_p > 0 else 1.0
+        # dU overwrites the mix gradient in place (same element, read before written)
+        L.check(lib.tspm_pool_act_bwd(n, d, self.dU.data_ptr(), dab2, self.TU.data_ptr(), keep, scale,
+                                      self.dU.data_ptr(), sh), "pool tanh+dropout bwd")
 
     def _maxout_product(self, mo: MaxOut, x, width, A, sh) -> None:
         """A[:, :h] = x @ W0^T, A[:, h:] = x @ W1^T — one [2h, in] product when the units' weights are
@@ -381,17 +495,22 @@ class MMIMDbEngine:
         linear_bwd(n, d, 2 * h, self.Zn.data_ptr(), d, self.dA1.data_ptr(), 2 * h, net[1].layers[0].weight.data_ptr(),
                    g(net[1].layers[0].weight), None, self.dZn.data_ptr(), d, sh)
         self._bn_bwd("b0", net[0], self.dZn, self.Z, d, self.dZ, sh)
-        # GMU
-        L.check(lib.tspm_gmu_bwd(n, d, self.dZ.data_ptr(), d, self.H.data_ptr(), 2 * d, self.gate.data_ptr(),
-                                 gmu.hidden_sigmoid.weight.data_ptr(), self.dU.data_ptr(), 2 * d, self.ds.data_ptr(), sh),
-                "gmu bwd")
-        L.check(lib.tspm_linear_bwd_weight(n, 2 * d, 1, self.H.data_ptr(), 2 * d, self.ds.data_ptr(), 1,
-                                           g(gmu.hidden_sigmoid.weight), None, sh), "gmu gate dW")
+        if self.pool is None:  # GMU
+            L.check(lib.tspm_gmu_bwd(n, d, self.dZ.data_ptr(), d, self.H.data_ptr(), 2 * d, self.gate.data_ptr(),
+                                     gmu.hidden_sigmoid.weight.data_ptr(), self.dU.data_ptr(), 2 * d,
+                                     self.ds.data_ptr(), sh), "gmu bwd")
+            L.check(lib.tspm_linear_bwd_weight(n, 2 * d, 1, self.H.data_ptr(), 2 * d, self.ds.data_ptr(), 1,
+                                               g(gmu.hidden_sigmoid.weight), None, sh), "gmu gate dW")
+            fa, fb = gmu.fc_one, gmu.fc_two
+        else:
+            self._pool_bwd(sh)
+            fa, fb = self.pool.proj_a, self.pool.proj_b
         dU1, dU2 = self.dU.data_ptr(), self.dU.data_ptr() + d * 4
         if _PAIRS and self.side is None:
-            # fc_two + fc_one backward in one launch, then both encoder Linears, then both input BNs
-            self._linear_bwd_multi([(n, e, d, self.ET, e, dU2, 2 * d, gmu.fc_two.weight, None, self.dET, e),
-                                    (n, e, d, self.EI, e, dU1, 2 * d, gmu.fc_one.weight, None, self.dEI, e)], sh)
+            # fc_two + fc_one (proj_b + proj_a) backward in one launch, then both encoder Linears, then
+            # both input BNs
+            self._linear_bwd_multi([(n, e, d, self.ET, e, dU2, 2 * d, fb.weight, fb.bias, self.dET, e),
+                                    (n, e, d, self.EI, e, dU1, 2 * d, fa.weight, fa.bias, self.dEI, e)], sh)
             self._linear_bwd_multi([(n, self.dt, e, self.XnT, self.dt, self.dET.data_ptr(), e, te[1].weight,
                                      te[1].bias, self.dXnT, self.dt),
                                     (n, self.di, e, self.XnI, self.di, self.dEI.data_ptr(), e, ie[1].weight,
@@ -406,10 +525,10 @@ class MMIMDbEngine:
             return
         st = self._fork()  # text branch (fc_two, text encoder) on the side stream
         for (dUp, fc, E, dE, key, enc, Xn, X, w, dXn, q) in (
-                (dU2, gmu.fc_two, self.ET, self.dET, "t", te, self.XnT, self.T, self.dt, self.dXnT, st),
-                (dU1, gmu.fc_one, self.EI, self.dEI, "i", ie, self.XnI, self.I, self.di, self.dXn, sh)):
-            linear_bwd(n, e, d, E.data_ptr(), e, dUp, 2 * d, fc.weight.data_ptr(), g(fc.weight), None, dE.data_ptr(),
-                       e, q)
+                (dU2, fb, self.ET, self.dET, "t", te, self.XnT, self.T, self.dt, self.dXnT, st),
+                (dU1, fa, self.EI, self.dEI, "i", ie, self.XnI, self.I, self.di, self.dXn, sh)):
+            linear_bwd(n, e, d, E.data_ptr(), e, dUp, 2 * d, fc.weight.data_ptr(), g(fc.weight),
+                       g(fc.bias) if fc.bias is not None else None, dE.data_ptr(), e, q)
             # encoder (the BatchNorm1d input-feature gradient is skipped: nothing consumes it)
             linear_bwd(n, w, e, Xn.data_ptr(), w, dE.data_ptr(), e, enc[1].weight.data_ptr(), g(enc[1].weight),
                        g(enc[1].bias), dXn.data_ptr(), w, q)
@@ -421,22 +540,26 @@ class MMIMDbEngine:
 # the model
 # ------------------------------------------------------------------------------------------------
 class MMIMDb(nn.Module):
-    """Drop-in for MML_Suite/models/mmimdb.py:96-338 (GMU fusion)."""
+    """Drop-in for MML_Suite/models/mmimdb.py:96-338 (GMU or multimodal-pooling fusion)."""
 
     def __init__(self, image_encoder: MMIMDbModalityEncoder, text_encoder: MMIMDbModalityEncoder,
                  gated_bimodal_network: Optional[GatedBiModalNetwork] = None,
                  multimodal_pooling: Optional[Dict[str, Any]] = None, classifier: MLPGenreClassifier = None,
                  binary_threshold: float = 0.5) -> None:
         super().__init__()
-        if multimodal_pooling is not None:
-            raise NotImplementedError("MMIMDb HIP path: multimodal_pooling fusion is not on the configs[3] path; "
-                                      "use gated_bimodal_network (configs/mmimdb/centralised/mmimdb_baseline.yaml)")
-        if gated_bimodal_network is None:
-            raise ValueError("Either gated_bimodal_network or multimodal_pooling must be provided")
         self.image_model = image_encoder
         self.text_model = text_encoder
-        self.fusion_module = gated_bimodal_network
-        self.fusion_type = "gated"
+        if multimodal_pooling is not None:  # built here, after the YAML's modules (models/mmimdb.py:128-141)
+            self.fusion_module = MultimodalPooling(
+                input_dim_a=image_encoder.net[-1].out_features, input_dim_b=text_encoder.net[-1].out_features,
+                output_dim=classifier.input_size, pooling_type=multimodal_pooling.get("pooling_type", "gated"),
+                hidden_dim=multimodal_pooling.get("hidden_dim", None), dropout=multimodal_pooling.get("dropout", 0.0))
+            self.fusion_type = "pooling"
+        elif gated_bimodal_network is not None:
+            self.fusion_module = gated_bimodal_network
+            self.fusion_type = "gated"
+        else:
+            raise ValueError("Either gated_bimodal_network or multimodal_pooling must be provided")
         self.mm_mlp = classifier
         self.binary_threshold = binary_threshold
         self.monitor = None
@@ -592,6 +715,9 @@ class FusedMMIMDbStep:
         self.opt.sync_hyper()
         if self.eng.keep_override is not None:
             self.eng.keep.copy_(self.eng.keep_override.reshape(self.eng.keep.shape).to(torch.uint8), non_blocking=True)
+        if self.eng.pool is not None and self.eng.pool_keep_override is not None:
+            self.eng.keep_pool.copy_(self.eng.pool_keep_override.reshape(self.eng.keep_pool.shape).to(torch.uint8),
+                                     non_blocking=True)
         if not self.use_graph or self.calls == 0:
             self._all()
         else:

@@ -31,6 +31,7 @@ from .modules import AVMNIST, ResNet18, ResNet34, ResNetEncoder
 from .optim import FusedAdam
 from . import mmimdb as _mm
 from . import mosi as _mosi
+from . import mosi_data as _mosi_data
 
 TAGS = {"!ResNet18": ResNet18, "!ResNet34": ResNet34, "!ResNetEncoder": ResNetEncoder,
         # MMIMDb late-fusion path (config/yaml_constructors.py:126-142)
@@ -44,7 +45,7 @@ MODELS = {"avmnist": AVMNIST, "mmimdb": _mm.MMIMDb, "mmimdbmodalityencoder": _mm
 ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder,
             "lstmencoder": _mosi.LSTMEncoder, "textcnn": _mosi.TextCNN}
 OPTIMIZERS = {"adam": FusedAdam}
-DATASETS = {"avmnist": data.AVMNIST}
+DATASETS = {"avmnist": data.AVMNIST, "mosi": _mosi_data.MOSI}
 
 
 def _ctor(cls):

@@ -98,7 +98,8 @@ def test_resolver_rebinding_falls_through():
         assert mod.resolve_optimizer("Adam") is tspm_amd.FusedAdam
         assert mod.resolve_optimizer("sgd") == ("orig", "sgd")
         assert mod.resolve_dataset_name("AVMNIST") is tspm_amd.data.AVMNIST
-        assert mod.resolve_dataset_name("mosi") == ("orig", "mosi")
+        assert mod.resolve_dataset_name("MOSI") is tspm_amd.mosi_data.MOSI
+        assert mod.resolve_dataset_name("iemocap") == ("orig", "iemocap")
         assert user.resolve_optimizer is mod.resolve_optimizer  # imported-by-name copies rebound too
         tspm_amd.plugin.register_resolvers(mod)  # idempotent
         assert mod.resolve_model_name("mosi") == ("orig", "mosi")

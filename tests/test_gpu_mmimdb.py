@@ -549,3 +549,78 @@ def test_maxout_fwd_rng_op_equals_mask_then_maxout(gpu, n, h, ctr):
         assert torch.equal(y, y_ref), u
     frac = keep_all.float().mean().item()
     assert abs(frac - 0.5) < 0.05 or n * h < 64
+
+
+# ------------------------------------------------------------------------------------------------
+# multimodal_pooling fusion (models/pooling.py; configs/mmimdb/centralised/pooling/*.yaml)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["max", "avg", "sum", "attention", "gated"])
+@pytest.mark.parametrize("n", [16, 64])
+def test_pooling_fused_step_vs_oracle(gpu, kind, n):
+    """The MMIMDb step with MultimodalPooling fusion (hidden 512, dropout 0.1) against the forced fp64
+    oracle (pinned to the real reference by make_mmimdb_pooling_golden.py): 2 steps from our own state,
+    MaxOut choices and — for max pooling — the element-wise a/b choices forced, §8(c) bounds, Adam exact.
+    (Batch >= 16: at 4 rows the input BatchNorm1d's gamma gradient is ill-conditioned in ANY fp32
+    implementation — channels with variance ~ eps — see test_fused_step_vs_oracle's n=4 note.)"""
+    from test_mmimdb_cpu import pool_cfg
+    cfg = pool_cfg(kind)
+    ours = dropin(0, cfg).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    st = M.FusedMMIMDbStep(ours, opt, None, n)
+    o32 = orc.build_oracle_mmimdb(0, pooling=cfg)
+    o64 = copy.deepcopy(o32).double()
+    I, T, y = orc.synthetic_batch(n, seed=88)
+    tally = Tally()
+    for s in range(2):
+        keep = _keep(n, 20 + s)
+        kp = (torch.rand(n, 1024, generator=torch.Generator().manual_seed(40 + s)) >= 0.1).to(torch.uint8)
+        if s > 0:
+            _sync_oracle(ours, opt, o32)
+            _sync_oracle(ours, opt, o64)
+        before = snapshot(ours, opt if s else None)
+        st.keep_override = keep.to(gpu)
+        st.eng.pool_keep_override = kp.to(gpu)
+        out = st.step(I.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        forced = _decisions(st)
+        if kind == "max":
+            ab = st.eng.H.detach().cpu()
+            a, b = ab[:, :512], ab[:, 512:]
+            forced["pool"] = torch.where(b > a, 1, torch.where(b == a, 2, 0)).to(torch.int8)
+        t32, t64 = orc.MaxOutTrace(forced), orc.MaxOutTrace(forced)
+        kpool = (kp[:, :512], kp[:, 512:])
+        r32 = orc.train_step(o32, None, I, T, y, keep[0], keep[1], t32, keep_pool=kpool)
+        r64 = orc.train_step(o64, None, I.double(), T.double(), y.double(), keep[0], keep[1], t64, keep_pool=kpool)
+        _flips(t64, forced, keep)
+        if kind == "max":
+            a0, a1 = t64.units["pool"]
+            flip = forced["pool"] != (a1 > a0).to(torch.int8)
+            flip &= ~((a0 == 0) & (a1 == 0))  # both dropped: exact tie either way
+            rms = torch.cat([a0, a1]).pow(2).mean().sqrt().item()
+            worst = ((a1 - a0).abs()[flip].max().item() / rms) if flip.any() else 0.0
+            assert worst <= NEAR and int(flip.sum()) <= max(1, MAX_FLIP_FRAC * flip.numel()), (int(flip.sum()), worst)
+        check_out(f"logits {kind} s{s}", out["logits"], r32["logits"], r64["logits"], tally)
+        check_out(f"loss {kind} s{s}", out["loss"], r32["loss"], r64["loss"], tally)
+        p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
+        for pname, p in ours.named_parameters():
+            check_grad(f"{pname} s{s}", p.grad, p32[pname].grad, p64[pname].grad, tally)
+        check_adam(ours, opt, *before, s + 1, lr=LR, wd=WD)
+    print(f"[{kind} n={n}] {tally}")
+
+
+def test_pooling_device_dropout_and_eval(gpu):
+    """Pooling dropout drawn on the device (p = 0.1 over [n, 2d], a stream distinct from the
+    classifier's masks), and validation_step runs the pooling fusion without dropout."""
+    from test_mmimdb_cpu import pool_cfg
+    ours = dropin(0, pool_cfg("attention")).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    n = 256
+    st = M.FusedMMIMDbStep(ours, opt, None, n)
+    I, T, y = orc.synthetic_batch(n, seed=9)
+    st.step(I.to(gpu), T.to(gpu), y.to(gpu))
+    torch.cuda.synchronize()
+    kp = st.eng.keep_pool.float()
+    assert abs(kp.mean().item() - 0.9) < 0.01
+    assert not torch.equal(st.eng.keep_pool[:, :512].reshape(-1)[:1000], st.eng.keep[0].reshape(-1)[:1000])
+    r = ours.validation_step({"image": I, "text": T, "label": y}, None, gpu)
+    assert np.isfinite(r["loss"])

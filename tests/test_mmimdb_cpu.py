@@ -30,12 +30,56 @@ def _sha(sd):
     return h.hexdigest()
 
 
-def dropin(seed=0):
+def dropin(seed=0, pooling=None):
     torch.manual_seed(seed)
     ie, te = M.MMIMDbModalityEncoder(4096, 512), M.MMIMDbModalityEncoder(300, 512)
+    if pooling is not None:  # YAML order of configs/mmimdb/centralised/pooling/*.yaml: no GMU
+        c = M.MLPGenreClassifier(input_size=512, hidden_size=512, output_size=23)
+        return M.MMIMDb(ie, te, multimodal_pooling=dict(pooling), classifier=c)
     g = M.GatedBiModalNetwork(input_one_dim=512, output_one_dim=512, input_two_dim=512, output_two_dim=512)
     c = M.MLPGenreClassifier(input_size=512, hidden_size=512, output_size=23)
     return M.MMIMDb(ie, te, gated_bimodal_network=g, classifier=c)
+
+
+POOL_KINDS = ["max", "avg", "sum", "attention", "gated"]
+POOL_GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "mmimdb_pool_b4.npz")
+
+
+def pool_cfg(kind):
+    return {"pooling_type": kind, "hidden_dim": 512, "dropout": 0.1}
+
+
+@pytest.mark.parametrize("kind", POOL_KINDS)
+def test_pooling_oracle_and_dropin_match_reference(kind):
+    """multimodal_pooling (models/pooling.py): the oracle replays the REAL reference's 2 train steps
+    bitwise (its own dropout masks; tests/golden/make_mmimdb_pooling_golden.py), and the drop-in builds
+    the same state_dict (keys and seeded values) and parameter order."""
+    from oracle.avmnist_ref import OracleAdam
+    g = dict(np.load(POOL_GOLDEN, allow_pickle=False))
+    I, T, y = (torch.from_numpy(g[k]) for k in ("image", "text", "labels"))
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    try:
+        model = orc.build_oracle_mmimdb(0, pooling=pool_cfg(kind))
+        ours = dropin(0, pool_cfg(kind))
+        assert list(model.state_dict()) == list(ours.state_dict()) == list(g[f"{kind}/state_dict_keys"])
+        for k, v in ours.state_dict().items():
+            assert torch.equal(v, model.state_dict()[k]), k
+        assert [n for n, _ in ours.named_parameters()] == list(g[f"{kind}/param_names"])
+        opt = OracleAdam(list(model.parameters()), lr=1e-5, weight_decay=1e-3)
+        for s in range(2):
+            kp = torch.from_numpy(g[f"{kind}/keep_pool"][s])
+            r = orc.train_step(model, opt, I, T, y, torch.from_numpy(g[f"{kind}/keep1"][s]),
+                               torch.from_numpy(g[f"{kind}/keep2"][s]), keep_pool=(kp[0], kp[1]))
+            assert r["loss"].item() == g[f"{kind}/losses"][s]
+            assert torch.equal(r["logits"], torch.from_numpy(g[f"{kind}/logits"][s]))
+            if s == 0:
+                gn = np.array([p.grad.double().norm().item() for p in model.parameters()])
+                np.testing.assert_array_equal(gn, g[f"{kind}/grad_norm_step1"])
+            ps = np.array([p.detach().double().sum().item() for p in model.parameters()])
+            np.testing.assert_array_equal(ps, g[f"{kind}/param_sums"][s])
+    finally:
+        torch.set_num_threads(nt)
 
 
 def test_oracle_init_matches_reference(mg):
@@ -103,9 +147,11 @@ clf: !MLPGenreClassifier {input_size: 512, hidden_size: 512, output_size: 23}
 
 
 def test_rejects_unsupported_configs():
-    with pytest.raises(NotImplementedError):
-        M.MMIMDb(M.MMIMDbModalityEncoder(8, 8), M.MMIMDbModalityEncoder(8, 8), multimodal_pooling={"x": 1},
-                 classifier=M.MLPGenreClassifier(8, 2, 8))
+    with pytest.raises(ValueError):  # models/pooling.py raises on an unknown pooling type
+        M.MMIMDb(M.MMIMDbModalityEncoder(8, 8), M.MMIMDbModalityEncoder(8, 8),
+                 multimodal_pooling={"pooling_type": "median"}, classifier=M.MLPGenreClassifier(8, 2, 8))
+    with pytest.raises(ValueError):
+        M.MMIMDb(M.MMIMDbModalityEncoder(8, 8), M.MMIMDbModalityEncoder(8, 8), classifier=M.MLPGenreClassifier(8, 2, 8))
 
 
 def test_bce_weight_checks_the_loss_group():
