@@ -229,9 +229,12 @@ LDS_WAVES = [(1, 1), (2, 1), (4, 1), (1, 2), (2, 2), (1, 4)]   # (wn, wk); wm = 
 LDS_SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32]
 
 
+MAX_WGS = int(os.environ.get("TUNE_MAX_WGS", "0"))  # > 0: only grids up to this many workgroups
+
+
 def lds_candidates(kind, s):
     """Supported variant-1 (LDS-staged) configurations of one launch, with split-K only while the
-    grid stays under ~2048 workgroups."""
+    grid stays under ~2048 workgroups (TUNE_MAX_WGS: a tighter cap, for concurrency experiments)."""
     for (tm, tn), (wn, wk) in itertools.product(LDS_TILES, LDS_WAVES):
         wm = 4 // (wn * wk)
         bm, bn = wm * tm * 32, wn * tn * 32
@@ -249,6 +252,8 @@ def lds_candidates(kind, s):
             wgs = -(-s.k // bm) * (s.r * s.s * s.c // bn)
         for sp in LDS_SPLITS:
             if sp > 1 and wgs * sp > 2048:
+                break
+            if MAX_WGS and wgs * sp > MAX_WGS and sp > 1:
                 break
             yield (tm, tn, wn, wk, sp, 1)
 

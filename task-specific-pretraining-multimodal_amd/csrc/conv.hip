@@ -652,6 +652,7 @@ ConvArgs make_args(const tspm_conv_shape* s) {
   g.sn = (long long)s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   g.bnb = BnbFuse{};
+  g.xcd = 0;
   return g;
 }
 

@@ -29,6 +29,7 @@ struct ConvArgs {
   int beta;                  // dgrad accumulate
   unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
   BnbFuse bnb;               // dgrad epilogue: BN-backward partial sums (variant 1 only)
+  int xcd;                   // LDS-staged kernels: XCD-aware workgroup -> tile mapping (1) or identity (0)
 };
 
 template <int TM, int TN>

@@ -116,6 +116,31 @@ struct Blk {
 };
 TSPM_DEV Blk hw_blk() { return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x}; }
 
+// XCD-aware tile order.  The dispatcher deals workgroups round-robin to the 8 XCDs (linear id L goes
+// to XCD L % 8), each with its own L2.  Logical tiles are ordered row block fastest, and neighbouring
+// row blocks read overlapping input rows (the filter taps of adjacent output positions, HWNC row
+// order), so each XCD is given a CONTIGUOUS range of logical tiles: XCD k runs tiles
+// [start_k, start_k + count_k) in dispatch order — the shared rows then hit that XCD's L2 instead of
+// being fetched once per XCD.  A bijection for any grid size (the first W % 8 XCDs take one more).
+constexpr int kXcds = 8;
+TSPM_DEV int xcd_swizzle(int L, int W) {
+  const int q = W / kXcds, r = W % kXcds;
+  const int xcd = L % kXcds, idx = L / kXcds;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+TSPM_DEV Blk grid_blk(int xcd) {
+  if (!xcd) return hw_blk();
+  const int gx = gridDim.x, gy = gridDim.y;
+  if (xcd == 2) {  // within each split-K plane only: every XCD keeps a share of every plane
+    const int T = xcd_swizzle(blockIdx.x + gx * blockIdx.y, gx * gy);
+    return Blk{T % gx, T / gx, (int)blockIdx.z, gx};
+  }
+  const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int T = xcd_swizzle(L, gx * gy * gridDim.z);
+  const int x = T % gx, yz = T / gx;
+  return Blk{x, yz % gy, yz / gy, gx};
+}
+
 // One stage's MFMAs with the next stage's LDS-DMA issues interleaved between them.  Measured
 // (scripts/stamp_conv.py ablations): a global_load_lds blocks its wave ~170 cycles at issue, and
 // with one wave per SIMD issuing them all before the MFMAs serialised DMA issue and matrix work
@@ -250,7 +275,8 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   const int tid = threadIdx.x, lane = tid & 63;
   const WaveId<C> id;
   const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
-  const int m0 = blockIdx.x * C::BM, n0col = blockIdx.y * C::BN;
+  const Blk bk = grid_blk(g.xcd);
+  const int m0 = bk.x * C::BM, n0col = bk.y * C::BN;
   const int pos = m0 / N, nb0 = m0 - pos * N;
   const int pp = pos / g.q, qq = pos - pp * g.q;
   const int h0 = pp * g.st - g.pad, w0 = qq * g.st - g.pad;
@@ -259,7 +285,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   const int nr = r_hi - r_lo + 1, ns = s_hi - s_lo + 1;
   const int cb = Cc >> 5;
   const int T = (nr > 0 && ns > 0) ? nr * ns * cb : 0;
-  const int st0 = split_lo(T, blockIdx.z, g.splits), st1 = split_lo(T, blockIdx.z + 1, g.splits);
+  const int st0 = split_lo(T, bk.z, g.splits), st1 = split_lo(T, bk.z + 1, g.splits);
 
   constexpr int NA = C::BM / 32, NB = C::BN / 32;
   const int wv = tid >> 6;
@@ -304,14 +330,14 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
   const int row0 = m0 + id.wm * C::TM * 32, col0 = n0col + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds, hw_blk()))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds, bk))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
   const bool active = id.wk == 0 && col0 < K;
   if (active) {
     acc.store(y, row0, col0, g.m, K, K, lane, false);
     if (bf.partial)
-      acc.bn_partials(bf.partial, (long long)gridDim.x * C::WM * K, blockIdx.x * C::WM + id.wm, row0, col0, g.m, K,
+      acc.bn_partials(bf.partial, (long long)gridDim.x * C::WM * K, bk.x * C::WM + id.wm, row0, col0, g.m, K,
                       lane, bf.counters != nullptr);
   }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
@@ -326,16 +352,16 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
     if (ng > 0) {
       // two levels: the last workgroup of each group of gw row blocks merges the group's tiles into
       // one tile of the second array; the last group merges those
-      const int grp = blockIdx.x / gw;
+      const int grp = bk.x / gw;
       const int x0 = grp * gw, x1 = min((int)gridDim.x, x0 + gw);
-      if (!last_arriver(bf.counters + gridDim.y + blockIdx.y * ng + grp, (unsigned)(x1 - x0), flag)) return;
+      if (!last_arriver(bf.counters + gridDim.y + bk.y * ng + grp, (unsigned)(x1 - x0), flag)) return;
       float* part1 = bf.partial + 3LL * T * K;
       bn_merge_level1(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu);
-      if (!last_arriver(bf.counters + blockIdx.y, (unsigned)ng, flag)) return;
+      if (!last_arriver(bf.counters + bk.y, (unsigned)ng, flag)) return;
       part = part1;
       G = ng;
       rpt = (long long)gw * C::WM * C::TM * 32;
-    } else if (!last_arriver(bf.counters + blockIdx.y, gridDim.x, flag)) {
+    } else if (!last_arriver(bf.counters + bk.y, gridDim.x, flag)) {
       return;
     }
     bn_merge_block(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
@@ -442,7 +468,7 @@ __global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float*
                                                        const float* __restrict__ w, float* __restrict__ dx,
                                                        float* __restrict__ slabs) {
   extern __shared__ float lds[];
-  dgrad_body<C>(g, dy, w, dx, slabs, lds, hw_blk());
+  dgrad_body<C>(g, dy, w, dx, slabs, lds, grid_blk(g.xcd));
 }
 
 // =============================================================================================
@@ -520,7 +546,7 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float*
                                                        const float* __restrict__ dy, float* __restrict__ dw,
                                                        float* __restrict__ slabs) {
   extern __shared__ float lds[];
-  wgrad_body<C>(g, x, dy, dw, slabs, lds, hw_blk());
+  wgrad_body<C>(g, x, dy, dw, slabs, lds, grid_blk(g.xcd));
 }
 
 // =============================================================================================
@@ -537,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void k_bwd_lds(ConvArgs gd, const float* 
                                                      const float* __restrict__ x, float* __restrict__ dw,
                                                      float* __restrict__ slabs_w, int wgx, int wgy) {
   extern __shared__ float lds[];
-  int b = blockIdx.x;
+  int b = gd.xcd == 1 ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int nw = wgx * wgy * gw.splits;
   if (b < nw) {
     const int z = b / (wgx * wgy);
@@ -581,6 +607,13 @@ bool hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
   return st->sc == 1 && st->sn == s->c && st->sw == (long long)s->n * s->c && st->sh == (long long)s->w * s->n * s->c;
 }
 
+// TSPM_XCD_SWIZZLE=1 / 2: XCD-aware workgroup -> tile mapping over the whole grid / within each
+// split-K plane; default 0 = identity (results are bitwise the same either way)
+int xcd_enabled() {
+  const char* e = getenv("TSPM_XCD_SWIZZLE");
+  return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+}
+
 ConvArgs args_of(const tspm_conv_shape* s) {
   ConvArgs g;
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
@@ -588,6 +621,7 @@ ConvArgs args_of(const tspm_conv_shape* s) {
   g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   g.bnb = BnbFuse{};
+  g.xcd = xcd_enabled();
   return g;
 }
 

@@ -36,7 +36,8 @@ def tuned_table() -> Dict[Tuple, Tuple[int, int, int, int, int]]:
         return {}
     if _tuned_cache is None:
         _tuned_cache = {}
-        for path in sorted(glob.glob(os.path.join(_TUNED_DIR, "*.json"))):
+        only = os.environ.get("TSPM_TUNED_FILE")  # one table instead of tuned/*.json (A/B experiments)
+        for path in ([only] if only else sorted(glob.glob(os.path.join(_TUNED_DIR, "*.json")))):
             with open(path) as fh:
                 doc = json.load(fh)
             for e in doc.get("entries", []):
