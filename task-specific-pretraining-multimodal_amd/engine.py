@@ -155,8 +155,11 @@ class EncoderEngine:
         # (2.88 vs 2.83 ms per step)
         self.bn_two_level = os.environ.get("TSPM_BN_TWO_LEVEL", "0") == "1"
         # BN-backward partial sums emitted by the producing dgrad's epilogue (small-row BatchNorms: one
-        # launch instead of partial + apply); TSPM_BN_DGRAD_FUSE=0 for the two-launch path (A/B)
-        self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "1") != "0"
+        # launch instead of partial + apply).  Opt-in (TSPM_BN_DGRAD_FUSE=1): measured at batch 128 the
+        # BN family drops 1.04 -> 0.87-0.91 ms of device time but the fused conv backward launches grow
+        # by ~5 us each (the epilogue's operand round trips sit in the split-K tail): conv 2.59 -> 2.77
+        # ms, ResNet34 3x3 at 0.133 instead of 0.149 of peak, step time unchanged (2.82 ms)
+        self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "0") == "1"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)

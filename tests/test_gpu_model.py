@@ -359,7 +359,7 @@ def test_bn_partials_in_dgrad_epilogue_match_two_launch_path(gpu, which, monkeyp
     g = torch.randn(128, hid, generator=torch.Generator().manual_seed(3)).to(gpu)
     grads = []
     fused_layers = []
-    for flag in ("1", "0"):
+    for flag in ("1", "0"):  # the epilogue path (opt-in) vs the default two-launch path
         monkeypatch.setenv("TSPM_BN_DGRAD_FUSE", flag)
         torch.manual_seed(0)
         enc = ctor(1, hid).to(gpu).train()
