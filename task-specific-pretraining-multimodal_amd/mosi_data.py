@@ -155,7 +155,7 @@ class MOSI(torch.utils.data.Dataset):
                  missing_patterns=None, selected_patterns: Optional[List[str]] = None,
                  labels_key: str = "classification_labels", aligned: bool = False, length: Optional[int] = None,
                  num_classes: Optional[int] = None, batch_size: int = 1, corpus: Optional[MosiCorpus] = None,
-                 device=None, seed: int = 0) -> None:
+                 device=None, seed: int = 0, allow_pickle: bool = False) -> None:
         split = split.lower()
         if split not in self.VALID_SPLITS:
             raise AssertionError(f"Invalid split provided, must be one of {self.VALID_SPLITS}")
@@ -172,6 +172,7 @@ class MOSI(torch.utils.data.Dataset):
             raise ValueError(f"Invalid patterns: {bad}")
         self.missing_patterns = missing_patterns
         self._batch_size = batch_size
+        self.allow_pickle = allow_pickle
         if corpus is None:
             corpus = self._load(data_fp)
         self.corpus = corpus
@@ -182,9 +183,10 @@ class MOSI(torch.utils.data.Dataset):
         self._keep = torch.tensor([[pattern_keep(p)[m] for m in MODALITIES] for p in PATTERNS], dtype=torch.float32)
 
     def _load(self, data_fp) -> MosiCorpus:
-        """The reference's split pickle (data/mosi.py:122-152: {"train"/"valid"/"test": {...}}) or an .npz of
-        the same keys (``<split>/audio`` ...).  Pickles are the user's own data files, read as the reference
-        reads them."""
+        """An .npz of the reference's split keys (``<split>/audio``, ``<split>/vision``, ...; read with
+        allow_pickle=False), or — only with ``allow_pickle=True``, for a data file the user trusts — the
+        reference's own split pickle (data/mosi.py:122-152: {"train"/"valid"/"test": {...}}), which
+        executes code when loaded."""
         if data_fp is None:
             raise ValueError("MOSI: data_fp or corpus is required")
         path = os.fspath(data_fp)
@@ -194,8 +196,11 @@ class MOSI(torch.utils.data.Dataset):
             with np.load(path, allow_pickle=False) as z:
                 split = {k.split("/", 1)[1]: z[k] for k in z.files if k.startswith(self.split + "/")}
         else:
+            if not self.allow_pickle:
+                raise ValueError(f"{path}: pickled dataset files run code when loaded; convert it to .npz or pass "
+                                 "allow_pickle=True for a file you trust")
             with open(path, "rb") as f:
-                raw = pickle.load(f)  # noqa: S301 (the user's dataset file, data/mosi.py:125-126)
+                raw = pickle.load(f)  # noqa: S301 (explicit opt-in; data/mosi.py:125-126)
             if self.split not in raw:
                 raise KeyError(f"Split '{self.split}' not found in data")
             split = raw[self.split]

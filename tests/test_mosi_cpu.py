@@ -126,3 +126,21 @@ def test_mosi_corpus_packing_and_padded_length():
              "classification_labels": np.array([[1], [2]])}
     c2 = D.MosiCorpus.from_split(split)
     assert len(c2) == 2 and c2.labels.dtype == np.int64 and list(c2.lengths["text"]) == [4, 4]
+
+
+def test_mosi_dataset_loads_npz_and_refuses_pickles_by_default(tmp_path):
+    from tspm_amd import mosi_data as D
+    g = np.random.default_rng(1)
+    arrs = {"train/audio": g.standard_normal((3, 6, 5)).astype(np.float32),
+            "train/vision": g.standard_normal((3, 6, 20)).astype(np.float32),
+            "train/text": g.standard_normal((3, 6, 768)).astype(np.float32),
+            "train/classification_labels": np.array([0, 2, 1])}
+    fp = tmp_path / "mosi.npz"
+    np.savez(fp, **arrs)
+    ds = D.MOSI(str(fp), "train", device="cpu", aligned=True, length=6)
+    assert len(ds) == 3 and list(ds.corpus.lengths["video"]) == [6, 6, 6]
+    np.testing.assert_array_equal(ds.corpus.data["text"][6:12], arrs["train/text"][1])
+    pk = tmp_path / "mosi.pkl"
+    pk.write_bytes(b"not read")
+    with pytest.raises(ValueError):
+        D.MOSI(str(pk), "train", device="cpu")
