@@ -114,3 +114,89 @@ def test_two_rank_phased_dp_step_on_one_gpu():
         assert ok_adam is True, rank
         assert same == [True, True], (rank, same)
         assert captured, rank
+
+
+def _mosi_worker(rank, world, port, q):
+    """MOSI UTT-Fusion data-parallel step (bench.py --mosi at N > 1): fused fwd/bwd graph, bucketed
+    all-reduce of the flat gradient, then the global-norm clip on the AVERAGED gradient and Adam
+    (torch DDP + clip_grad_norm_ semantics)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.dirname(here), here]
+        import torch.distributed as dist
+        import tspm_amd
+        from oracle import mosi_ref as orc
+        from parity import adam_fp64, adam_tolerance
+        from test_mosi_cpu import _dropin
+        from tspm_amd import ddp
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        A, V, T, y = orc.synthetic_batch(64, 30, seed=99)
+        half = slice(32 * rank, 32 * rank + 32)
+        keeps = orc.keep_masks(64, seed=5)
+
+        def run_local(clip):
+            m = _dropin(0, clip=clip).to(dev)
+            o = tspm_amd.FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-3)
+            st = m.fused_step(o, None, 32, 30)
+            st.keep_override = {k: v[half].to(dev) for k, v in keeps.items()}
+            st.step(A[half].to(dev), V[half].to(dev), T[half].to(dev), y[half].to(dev))
+            torch.cuda.synchronize()
+            return o.flat_groups()[0].grad.clone()
+        g_loc = run_local(None)  # this rank's gradient (no clip, no exchange)
+        m = _dropin(0, clip=0.05).to(dev)  # a tight clip so the coefficient is active
+        opt = tspm_amd.FusedAdam(m.parameters(), lr=1e-3, weight_decay=1e-3, grad_scale=1.0 / world)
+        st = m.fused_step(opt, None, 32, 30)
+        fg = opt.flat_groups()[0]
+        st.allreduce = ddp.GradAllReduce([fg.grad])
+        p0 = fg.param.detach().cpu().double().clone()
+        st.keep_override = {k: v[half].to(dev) for k, v in keeps.items()}
+        st.step(A[half].to(dev), V[half].to(dev), T[half].to(dev), y[half].to(dev))
+        torch.cuda.synchronize()
+        gs = [torch.empty_like(g_loc) for _ in range(world)]
+        dist.all_gather(gs, g_loc)
+        ok_sum = bool(torch.equal(fg.grad, gs[0] + gs[1]))
+        avg = fg.grad.double().cpu() / world
+        coef = min(1.0, 0.05 / (float(avg.norm()) + 1e-6))
+        ok_coef = abs(float(st.eng.clip_coef.item()) - coef) <= 1e-5 * coef
+        g = avg * float(st.eng.clip_coef.item())
+        exp, _, v = adam_fp64(p0, g, 1, lr=1e-3, wd=1e-3)
+        got = fg.param.detach().cpu().double()
+        ok_adam = bool(((got - exp).abs() <= 1e-6 * exp.abs() + adam_tolerance(p0, g, 1, v, 1e-3, 1e-3)).all())
+        for s in range(3):
+            st.keep_override = {k: v_[half].to(dev) for k, v_ in orc.keep_masks(64, seed=50 + s).items()}
+            st.step(A[half].to(dev), V[half].to(dev), T[half].to(dev), y[half].to(dev))
+        torch.cuda.synchronize()
+        state = torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).clone()
+        other = [torch.empty_like(state) for _ in range(world)]
+        dist.all_gather(other, state)
+        q.put((rank, ok_sum, ok_coef and ok_adam, bool(torch.equal(other[0], other[1])), st.graph is not None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
+
+
+def test_two_rank_mosi_dp_step_on_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mosi_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_sum, ok_step, same, captured in res:
+        assert ok_sum is True, (rank, ok_sum)
+        assert ok_step is True, rank
+        assert same is True, rank
+        assert captured, rank
