@@ -122,21 +122,23 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
     of the two encoders overlap there and stretch each other)."""
     from tspm_amd.roofline import CONV_KERNEL, attribute_conv_kernels, device_kernels, launch_flops
     ks_all = device_kernels(run_serial, replays)
-    # split the trace into steps at the optimizer's k_adam (the last kernel of every step) and keep
-    # the steps whose conv-kernel count matches the recorded launch sequence (the profiler can drop
-    # a few records in a long capture; a partial step would skew every per-step figure)
+    # split the trace into steps after each k_adam (the optimizer is the last kernel of a step) and
+    # keep only COMPLETE steps: the profiler drops a few records in a long capture (up to ~5 % of a
+    # 10-replay trace), so a chunk is kept when its conv-kernel count equals the recorded launch
+    # sequence and its kernel count equals the largest such chunk's (a chunk that lost its k_adam
+    # spans two steps and fails the first test; several k_adam per step leave no chunk passing it)
     from tspm_amd.roofline import CONV_SECONDARY
     steps, cur = [], []
     for k in ks_all:
         cur.append(k)
-        if "k_adam(" in k["name"] or k["name"].startswith("k_adam") or "::k_adam(" in k["name"]:
+        if re.search(r"\bk_adam\b", k["name"]):
             steps.append(cur)
             cur = []
-    good = [st for st in steps if sum(1 for k in st if CONV_KERNEL.search(k["name"])
+    full = [st for st in steps if sum(1 for k in st if CONV_KERNEL.search(k["name"])
                                       and not CONV_SECONDARY.search(k["name"])) == len(seq)]
-    if len(steps) != replays:  # not one k_adam per step (several parameter groups): no split
-        good = []
-    dropped = len(steps) - len(good)
+    most = max((len(st) for st in full), default=0)
+    good = [st for st in full if len(st) == most]
+    dropped = replays - len(good)
     if good:
         replays = len(good)
         ks = [k for st in good for k in st]
@@ -208,9 +210,12 @@ def pmc_traffic(family: str = "conv", path: str = "main"):
     def ver(p):  # newest = highest r<round>_v<version> (mtimes are equal on a fresh checkout)
         m = re.search(r"r(\d+)_v(\d+)", os.path.basename(p))
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    def tag(p):  # rR_vV_pmc_traffic.json -> "main"; rR_vV_<workload>_pmc_traffic.json -> <workload>
+        m = re.match(r"r\d+_v\d+_(?:(\w+?)_)?pmc_traffic\.json$", os.path.basename(p))
+        return (m.group(1) or "main") if m else None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=ver)
-    # "main": the AVMNIST summaries (r1_vN_pmc_traffic.json); "mmimdb": r1_vN_mmimdb_pmc_traffic.json
-    files = [f for f in files if ("_mmimdb_" in os.path.basename(f)) == (path == "mmimdb")]
+    # "main": the AVMNIST summaries; "mmimdb" / "mosi": that workload's own summaries
+    files = [f for f in files if tag(f) == path]
     if not files:
         return None, None, None
     with open(files[-1]) as f:
@@ -735,6 +740,11 @@ def mosi_bench(args) -> None:
                                        "(LDS-staged MFMA 32x32x2 fp32), 3 launches per step",
             "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
             "flop_per_step": conv_flops, "achieved": None, "frac": None}
+    tr, tr_launches, tr_src = pmc_traffic("conv", "mosi") if B == 128 else (None, None, None)
+    if tr:
+        roof.update({"traffic": tr, "traffic_per_launch": round(tr / tr_launches) if tr_launches else None,
+                     "traffic_unit": "HBM bytes per step of the TextCNN convs (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
+                     "traffic_source": tr_src})
     if args.profile_steps > 0 and world == 1:
         R = args.profile_steps
         ks = device_kernels(one, R)
@@ -968,6 +978,8 @@ def main() -> None:
                 r34["what"] = ("ResNet34 (image encoder) 3x3 convs: fwd + dgrad + wgrad launches, valid-tap FLOPs / "
                                "their device time (north_star target >= 0.70)")
             rl["r34_3x3"] = r34
+            rl["profiled_steps"] = roof["profiled_steps"]
+            rl["incomplete_steps_dropped"] = roof["incomplete_steps_dropped"]
             if roof.get("attribution_failed"):
                 rl["attribution_failed"] = roof["attribution_failed"]
             if args.kernel_table and roof["per_launch"]:

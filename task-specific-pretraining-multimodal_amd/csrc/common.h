@@ -94,6 +94,14 @@ static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Write-through (sc1) store: visible at agent scope once the storing wave drains vmcnt, without
 // a release fence (whose buffer_wbl2 writes back the whole XCD L2).
 TSPM_DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// L1-bypassing (sc1) global load of hand-off payload: `global_load_dword … sc1` (global address
+// space, never flat).  Used for EVERY load of bytes another workgroup published with st_sc1 in
+// the same launch, so the reader needs no agent-scope acquire (MI355X_MICROARCH.md, "Valid forms",
+// first row of the sc1 hand-off table: one lane's relaxed agent add after every storing wave's
+// vmcnt(0) wait and a workgroup barrier; the last adder's workgroup loads behind a barrier).
+TSPM_DEV float ld_sc1(const float* p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // In-launch hand-off to the LAST arriving workgroup of a group (cdna_hip_programming.md §5 and
 // §6 Guideline 16, the sc1 form): every wave has stored its share of the payload with st_sc1 and
@@ -102,15 +110,21 @@ TSPM_DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELA
 // next launch and returns true in every thread.  `flag` is one int of the kernel's LDS.  Every
 // thread of the workgroup must call this (it contains barriers).  Counters must be zero before the
 // first launch that uses them.
-TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag) {
+//
+// acquire == false: the caller reads every byte of the payload with ld_sc1 (L1 bypassed), so the
+// ≈1.7 µs agent acquire (buffer_inv sc1 + its wait) is skipped — the payload's visibility then rests
+// on the sc1 stores and loads alone (MI355X_MICROARCH.md, sc1 hand-off table, first row).
+TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag, bool acquire = true) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == total - 1;
     if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     *flag = last;
@@ -129,8 +143,13 @@ TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag) {
 //
 // bn_merge_range is the merge itself over tiles [g_lo, g_hi) of a partial array with G_all tiles:
 // returns (in the threads with t < CB) the range's mean and sum of squared deviations in double.
+template <bool SC1 = false>  // SC1: the partials are an in-launch hand-off read with ld_sc1
 TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
                              int c0, int CB, double* red, double* smu, double& mean_out, double& m2_out) {
+  auto ld = [](const float* p) -> float {
+    if constexpr (SC1) return ld_sc1(p);
+    else return *p;
+  };
   const int t = threadIdx.x, T = blockDim.x;
   const int GG = T / CB, cl = t % CB, gg = t / CB;
   const int c = c0 + cl;
@@ -141,7 +160,7 @@ TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const
   // they miss in cache, so issue them together)
   auto tile_mean = [&](int g, double& nb, double& mb) {
     nb = (double)min(rpt, M - (long long)g * rpt);
-    mb = (double)part[(long long)g * C + c] + (double)part[plane + (long long)g * C + c];
+    mb = (double)ld(part + (long long)g * C + c) + (double)ld(part + plane + (long long)g * C + c);
   };
   double s = 0.0;
   if (cok)
@@ -173,7 +192,7 @@ TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const
         const int g = g0 + u * GG;
         if (g < g_hi) {
           tile_mean(g, nb[u], mb[u]);
-          m2b[u] = (double)part[2 * plane + (long long)g * C + c];
+          m2b[u] = (double)ld(part + 2 * plane + (long long)g * C + c);
         } else {
           nb[u] = 0.0; mb[u] = mean; m2b[u] = 0.0;
         }
@@ -195,10 +214,11 @@ TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const
 // First level of a two-level merge: tiles [g_lo, g_hi) of `part` (G_all tiles) into ONE tile
 // `g_out` of `part1` (G1 tiles) in the same {K, mean-K, M2} format (K = mean rounded to float, so
 // mean-K carries the rounding residual), written through (sc1) for the second-level merger.
+template <bool SC1 = false>
 TSPM_DEV void bn_merge_level1(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
                               int c0, int CB, float* part1, int G1, int g_out, double* red, double* smu) {
   double mean, m2;
-  bn_merge_range(M, C, G_all, rpt, part, g_lo, g_hi, c0, CB, red, smu, mean, m2);
+  bn_merge_range<SC1>(M, C, G_all, rpt, part, g_lo, g_hi, c0, CB, red, smu, mean, m2);
   const int t = threadIdx.x, c = c0 + t;
   if (t < CB && c < C) {
     const long long plane1 = (long long)G1 * C, o = (long long)g_out * C + c;
@@ -209,11 +229,12 @@ TSPM_DEV void bn_merge_level1(long long M, int C, int G_all, long long rpt, cons
   }
 }
 
+template <bool SC1 = false>
 TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const float* part, int c0, int CB,
                              float* rmean, float* rvar, float momentum, float eps, float* smean, float* sinv,
                              double* red, double* smu) {
   double mean, m2;
-  bn_merge_range(M, C, G, rpt, part, 0, G, c0, CB, red, smu, mean, m2);
+  bn_merge_range<SC1>(M, C, G, rpt, part, 0, G, c0, CB, red, smu, mean, m2);
   const int cl = threadIdx.x, c = c0 + cl;
   if (cl < CB && c < C) {
     const double n = (double)M;

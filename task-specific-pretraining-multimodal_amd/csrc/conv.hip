@@ -653,6 +653,7 @@ ConvArgs make_args(const tspm_conv_shape* s) {
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   g.bnb = BnbFuse{};
   g.xcd = 0;
+  g.acq = 1;  // register-direct kernels: acquire-based hand-offs (conv_common.h tails)
   return g;
 }
 

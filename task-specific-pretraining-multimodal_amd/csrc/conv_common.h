@@ -30,6 +30,8 @@ struct ConvArgs {
   unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
   BnbFuse bnb;               // dgrad epilogue: BN-backward partial sums (variant 1 only)
   int xcd;                   // LDS-staged kernels: XCD-aware workgroup -> tile mapping (1) or identity (0)
+  int acq;                   // LDS-staged kernels: agent acquire before reading split-K slabs / BN partials
+                             // (1), or sc1 loads only (0, default; TSPM_HANDOFF_ACQUIRE=1 for A/B)
 };
 
 template <int TM, int TN>

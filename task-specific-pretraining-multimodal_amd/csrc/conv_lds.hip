@@ -237,10 +237,10 @@ TSPM_DEV void combine_k(Acc<C::TM, C::TN>& acc, float* lds, const WaveId<C>& id,
 template <class C>
 TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lane, float* slabs, long long slab,
                             int splits, unsigned* cnt, int row0, int col0, int rows, int cols, long long ld,
-                            float* lds, const Blk& bk) {
+                            float* lds, const Blk& bk, bool acquire) {
   if (splits <= 1) return true;
   if (id.wk == 0) acc.store(slabs + (long long)bk.z * slab, row0, col0, rows, cols, ld, lane, false, true);
-  if (!last_arriver(cnt + (bk.y * bk.gx + bk.x), (unsigned)splits, reinterpret_cast<int*>(lds)))
+  if (!last_arriver(cnt + (bk.y * bk.gx + bk.x), (unsigned)splits, reinterpret_cast<int*>(lds), acquire))
     return false;
   if (id.wk == 0) {
     acc.zero();
@@ -254,7 +254,7 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int row = min(row0 + a * 32 + acc_row(i, lane), rows - 1);
-            acc.v[a][b][i] += src[(long long)row * ld + col];
+            acc.v[a][b][i] += ld_sc1(src + (long long)row * ld + col);
           }
         }
     }
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
   const int row0 = m0 + id.wm * C::TM * 32, col0 = n0col + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds, bk))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * K, g.splits, g.cnt, row0, col0, g.m, K, K, lds, bk, g.acq != 0))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
   const bool active = id.wk == 0 && col0 < K;
@@ -354,17 +354,17 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
       // one tile of the second array; the last group merges those
       const int grp = bk.x / gw;
       const int x0 = grp * gw, x1 = min((int)gridDim.x, x0 + gw);
-      if (!last_arriver(bf.counters + gridDim.y + bk.y * ng + grp, (unsigned)(x1 - x0), flag)) return;
+      if (!last_arriver(bf.counters + gridDim.y + bk.y * ng + grp, (unsigned)(x1 - x0), flag, g.acq != 0)) return;
       float* part1 = bf.partial + 3LL * T * K;
-      bn_merge_level1(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu);
-      if (!last_arriver(bf.counters + bk.y, (unsigned)ng, flag)) return;
+      bn_merge_level1<true>(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu);
+      if (!last_arriver(bf.counters + bk.y, (unsigned)ng, flag, g.acq != 0)) return;
       part = part1;
       G = ng;
       rpt = (long long)gw * C::WM * C::TM * 32;
-    } else if (!last_arriver(bf.counters + bk.y, gridDim.x, flag)) {
+    } else if (!last_arriver(bf.counters + bk.y, gridDim.x, flag, g.acq != 0)) {
       return;
     }
-    bn_merge_block(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
+    bn_merge_block<true>(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
                    bf.save_mean, bf.save_invstd, red, smu);
   }
 }
@@ -448,7 +448,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
   const int row0 = m0 + id.wm * C::TM * 32, col0 = c0col + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk, g.acq != 0))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
   if (id.wk == 0 && col0 < Cc) {
@@ -537,7 +537,7 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
       });
   combine_k<C>(acc, lds, id, lane);
   const int row0 = co0 + id.wm * C::TM * 32, col0 = col0b + id.wn * C::TN * 32;
-  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds, bk))
+  if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds, bk, g.acq != 0))
     return;
   if (id.wk == 0 && row0 < K) acc.store(dw, row0, col0, K, RSC, RSC, lane, false);
 }
@@ -614,6 +614,13 @@ int xcd_enabled() {
   return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
 }
 
+// TSPM_HANDOFF_ACQUIRE=1: the last arriver of a split-K tile / BN merge group takes an agent-scope
+// acquire before its (sc1) payload loads; default 0 = sc1 stores + sc1 loads only (bitwise the same)
+int acquire_enabled() {
+  const char* e = getenv("TSPM_HANDOFF_ACQUIRE");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
 ConvArgs args_of(const tspm_conv_shape* s) {
   ConvArgs g;
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
@@ -622,6 +629,7 @@ ConvArgs args_of(const tspm_conv_shape* s) {
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   g.bnb = BnbFuse{};
   g.xcd = xcd_enabled();
+  g.acq = acquire_enabled();
   return g;
 }
 

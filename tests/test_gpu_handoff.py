@@ -1,0 +1,115 @@
+"""In-launch hand-offs of the LDS-staged conv kernels without an agent-scope acquire.
+
+The last arriving workgroup of a split-K tile (and of a BatchNorm merge group) reads the other
+workgroups' slabs / partial statistics with L1-bypassing sc1 loads instead of taking an acquire
+(csrc/common.h ld_sc1, last_arriver(acquire=false); TSPM_HANDOFF_ACQUIRE=1 restores the acquire).
+MI355X_MICROARCH.md asks every hand-off to be tested under UNEVEN load, with the consumer's L1 warm,
+checking every word: here the same workspace and output buffers are reused by 48 back-to-back
+launches on fresh inputs each (a stale slab line from the previous launch would change the result)
+while a second stream streams a 1 GiB buffer, and every output word is compared with the acquire
+path's result for the same input."""
+import ctypes
+import os
+
+import pytest
+import torch
+
+from abi_helpers import shape, to_hwnc
+from tspm_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+REPS = 48
+
+# (kind, n, c, h, w, k, r, s, stride, pad, algo): the tuned split-K configurations of the batch-128 step
+CASES = [
+    ("fwd", 128, 256, 2, 2, 256, 3, 3, 1, 1, (1, 1, 1, 2, 4, 1)),
+    ("fwd", 128, 64, 7, 7, 64, 3, 3, 1, 1, (1, 1, 2, 2, 1, 1)),     # many tiles: BN merge hand-off only
+    ("fwd", 128, 512, 1, 3, 512, 3, 3, 1, 1, (1, 1, 1, 2, 4, 1)),
+    ("dgrad", 128, 256, 2, 2, 256, 3, 3, 1, 1, (1, 1, 2, 2, 4, 1)),
+    ("dgrad", 128, 512, 1, 3, 512, 3, 3, 1, 1, (1, 1, 1, 1, 8, 1)),
+    ("wgrad", 128, 128, 4, 12, 128, 3, 3, 1, 1, (1, 1, 2, 1, 12, 1)),
+    ("wgrad", 128, 64, 8, 24, 64, 3, 3, 1, 1, (1, 1, 2, 1, 24, 1)),
+]
+
+
+class _Runner:
+    """One conv launch with persistent workspace / counters / outputs (reused across launches)."""
+
+    def __init__(self, kind, n, c, h, w, k, r, s, st, pad, algo, dev):
+        self.kind, self.dev = kind, dev
+        self.shp = shape(n, h, w, c, k, r, s, st, pad)
+        self.a = L.ConvAlgo(*algo)
+        self.n, self.c, self.h, self.w, self.k, self.r, self.s = n, c, h, w, k, r, s
+        lib = L.lib()
+        ws_fn = {"fwd": lib.tspm_conv_fwd_workspace, "dgrad": lib.tspm_conv_dgrad_workspace,
+                 "wgrad": lib.tspm_conv_wgrad_workspace}[kind]
+        self.wsb = ws_fn(ctypes.byref(self.shp), ctypes.byref(self.a))
+        self.ws = torch.zeros(max(self.wsb, 16), dtype=torch.uint8, device=dev)
+        p, q = self.shp.p, self.shp.q
+        if kind == "fwd":
+            self.out = torch.empty(p * q * n, k, device=dev)
+            # buffers sized for the two-level in-launch merge, so every layer merges in-launch
+            nfl = lib.tspm_conv_fwd_bn_partial_floats(ctypes.byref(self.shp), ctypes.byref(self.a))
+            ncnt = lib.tspm_conv_fwd_bn_counters(ctypes.byref(self.shp), ctypes.byref(self.a))
+            self.part = torch.empty(nfl, device=dev)
+            self.cnt = torch.zeros(ncnt, dtype=torch.int32, device=dev)
+            self.mean = torch.empty(k, device=dev)
+            self.inv = torch.empty(k, device=dev)
+            self.bnf = L.BnFuse(self.part.data_ptr(), self.cnt.data_ptr(), None, None, 0.1, 1e-5,
+                                self.mean.data_ptr(), self.inv.data_ptr(), ncnt, 0, nfl)
+        elif kind == "dgrad":
+            self.out = torch.empty(h * w * n, c, device=dev)
+        else:
+            self.out = torch.empty(k, c, r, s, device=dev).contiguous(memory_format=torch.channels_last)
+
+    def inputs(self, g):
+        n, c, h, w, k, r, s = self.n, self.c, self.h, self.w, self.k, self.r, self.s
+        p, q = self.shp.p, self.shp.q
+        a = to_hwnc(torch.randn(n, c, h, w, generator=g) if self.kind != "dgrad" else torch.randn(n, k, p, q, generator=g))
+        b = (torch.randn(k, c, r, s, generator=g) * 0.05).contiguous(memory_format=torch.channels_last) \
+            if self.kind != "wgrad" else to_hwnc(torch.randn(n, k, p, q, generator=g))
+        return a.to(self.dev), b.to(self.dev)
+
+    def run(self, a, b):
+        lib, sh = L.lib(), L.stream_handle()
+        S, A = ctypes.byref(self.shp), ctypes.byref(self.a)
+        if self.kind == "fwd":
+            st = L.hwnc_strides(self.n, self.h, self.w, self.c)
+            L.check(lib.tspm_conv_fwd(S, A, a.data_ptr(), ctypes.byref(st), b.data_ptr(), self.out.data_ptr(),
+                                      ctypes.byref(self.bnf), self.ws.data_ptr(), self.wsb, sh), "conv_fwd")
+            return torch.cat([self.out.flatten(), self.mean, self.inv])
+        if self.kind == "dgrad":
+            L.check(lib.tspm_conv_dgrad(S, A, a.data_ptr(), b.data_ptr(), self.out.data_ptr(), 0, self.ws.data_ptr(),
+                                        self.wsb, sh), "conv_dgrad")
+            return self.out.flatten().clone()
+        st = L.hwnc_strides(self.n, self.h, self.w, self.c)
+        L.check(lib.tspm_conv_wgrad(S, A, a.data_ptr(), ctypes.byref(st), b.data_ptr(), self.out.data_ptr(),
+                                    self.ws.data_ptr(), self.wsb, sh), "conv_wgrad")
+        return self.out.flatten().clone()
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1:10]}-{c[10]}")
+def test_sc1_handoff_equals_acquire_under_load(gpu, case, monkeypatch):
+    kind, *shp, algo = case
+    run = _Runner(kind, *shp, algo, gpu)
+    g = torch.Generator().manual_seed(77)
+    ins = [run.inputs(g) for _ in range(REPS)]
+    # reference: the acquire path, serial, no concurrent load
+    monkeypatch.setenv("TSPM_HANDOFF_ACQUIRE", "1")
+    ref = [run.run(a, b).clone() for a, b in ins]
+    torch.cuda.synchronize()
+    # the sc1 path, back to back on the same buffers, beside a streaming second stream
+    monkeypatch.setenv("TSPM_HANDOFF_ACQUIRE", "0")
+    big = torch.empty(256 * 1024 * 1024, device=gpu)  # 1 GiB
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(6):
+            big.mul_(1.0000001)
+    got = [run.run(a, b) for a, b in ins]
+    torch.cuda.synchronize()
+    del big
+    for i, (x, y) in enumerate(zip(got, ref)):
+        bad = (x != y) & ~(torch.isnan(x) & torch.isnan(y))
+        assert not bool(bad.any()), f"{kind} {shp} {algo}: launch {i}: {int(bad.sum())} words differ from the acquire path"
+    assert os.environ.get("TSPM_HANDOFF_ACQUIRE") == "0"
