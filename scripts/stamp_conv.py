@@ -75,6 +75,9 @@ def report(lib, kind, key, s, xs, b, algo):
         st = buf.reshape(-1, SLOTS).astype(np.int64)
         used = st[:, 0] > 0
         nw = int(used.sum())
+        if nw == 0:
+            print(f"{kind:6s} {tuple(key[1:])} algo {algo}: no stamps (kernel not instrumented)", flush=True)
+            return
         st = st[used]
         t0 = st[:, 0].min()
         rel = (st - t0) * 0.01  # us
@@ -82,8 +85,8 @@ def report(lib, kind, key, s, xs, b, algo):
         print(f"   start spread: p50 {np.percentile(rel[:, 0], 50):.2f} p90 {np.percentile(rel[:, 0], 90):.2f} "
               f"max {rel[:, 0].max():.2f} us;  last stamp max {rel.max():.2f} us")
         if lds_variant:
-            pairs = [(1, 0, "1st data"), (2, 1, "loop rest"), (3, 2, "combine"), (4, 3, "split-K"), (5, 4, "epilogue"),
-                     (5, 0, "total")]
+            pairs = [(1, 0, "1st data"), (2, 1, "loop rest"), (3, 2, "combine"), (6, 3, "slab+tkt"),
+                     (4, 6, "slab rd"), (4, 3, "split-K"), (5, 4, "epilogue"), (5, 0, "total")]
         else:
             pairs = [(5, 0, "1st data"), (1, 5, "loop rest"), (2, 1, "combine"), (3, 2, "epilogue"), (4, 3, "bn tail")]
         if lds_variant and (st[:, 7] > 0).any():

@@ -242,6 +242,7 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
   if (id.wk == 0) acc.store(slabs + (long long)bk.z * slab, row0, col0, rows, cols, ld, lane, false, true);
   if (!last_arriver(cnt + (bk.y * bk.gx + bk.x), (unsigned)splits, reinterpret_cast<int*>(lds), acquire))
     return false;
+  TSPM_STAMP(tspm_g_stamps_lds, 6);
   if (id.wk == 0) {
     acc.zero();
     for (int z = 0; z < splits; ++z) {
@@ -377,7 +378,6 @@ template <class C>
 TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const float* __restrict__ w,
                          float* __restrict__ dx, float* __restrict__ slabs, float* lds, const Blk& bk) {
   TSPM_STAMP(tspm_g_stamps_lds, 0);
-  TSPM_STAMP_CLK(tspm_g_stamps_lds, 6);
   const int tid = threadIdx.x, lane = tid & 63;
   const WaveId<C> id;
   const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
@@ -461,7 +461,6 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
     }
   }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
-  TSPM_STAMP_CLK(tspm_g_stamps_lds, 7);
 }
 template <class C>
 __global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
