@@ -198,9 +198,23 @@ def compare(out_path: str) -> None:
         t = float(stats.t.ppf(0.975, len(d) - 1)) if len(d) > 1 else float("nan")
         return {"delta_pp": round(m, 3), "stderr_pp": round(se, 3), "ci95_pp": [round(m - t * se, 3), round(m + t * se, 3)],
                 "within_0.2pp": bool(m - t * se >= -0.2 and m + t * se <= 0.2)}
+    def paired90(a, b):  # two one-sided tests at +-0.2 pp: the 90 % interval inside the margin
+        d = 100 * (np.asarray(a) - np.asarray(b))
+        m, se = float(d.mean()), float(d.std(ddof=1) / np.sqrt(len(d)))
+        t = float(stats.t.ppf(0.95, len(d) - 1))
+        return {"ci90_pp": [round(m - t * se, 3), round(m + t * se, 3)],
+                "equivalent_at_0.2pp": bool(m - t * se > -0.2 and m + t * se < 0.2)}
     last = rows[-1]
     fin_o, fin_r = last["ours_test_accuracy"], last["reference_test_accuracy"]
     t3 = lambda c, s: float(np.mean([c[s][k]["test_accuracy"] for k in range(n - 3, n)]))  # noqa: E731
+    tk = lambda c, s, k0: float(np.mean([c[s][k]["test_accuracy"] for k in range(k0, n)]))  # noqa: E731
+    window = {}
+    for k0 in (n - 5, n // 2):
+        o, r = [tk(our, s, k0) for s in seeds], [tk(ref, s, k0) for s in seeds]
+        window[f"epochs_{k0 + 1}_{n}"] = {"reference_mean": round(float(np.mean(r)), 5),
+                                         "ours_mean": round(float(np.mean(o)), 5),
+                                         "reference_std_pp": round(100 * float(np.std(r, ddof=1)), 3),
+                                         "paired": {**paired(o, r), **paired90(o, r)}}
     doc = {"what": "late-fusion AVMNIST on the reference's own sample files (24,000 train / 6,000 test pairs, "
                    "speaker-disjoint test; own pairing — the reference's split CSVs are absent); paired runs: "
                    "same initial weights (seed s), batch order and dropout masks on both sides; batch 128, "
@@ -212,15 +226,17 @@ def compare(out_path: str) -> None:
            "final": {"epoch": last["epoch"], "reference_mean": last["reference_mean"], "ours_mean": last["ours_mean"],
                      "reference_std_pp": round(100 * float(np.std(fin_r, ddof=1)), 3) if len(seeds) > 1 else None,
                      "ours_std_pp": round(100 * float(np.std(fin_o, ddof=1)), 3) if len(seeds) > 1 else None,
-                     "paired": paired(fin_o, fin_r)},
+                     "paired": {**paired(fin_o, fin_r), **paired90(fin_o, fin_r)}},
            "last3_epochs_mean": {"reference_mean": round(float(np.mean([t3(ref, s) for s in seeds])), 5),
                                  "ours_mean": round(float(np.mean([t3(our, s) for s in seeds])), 5),
                                  "paired": paired([t3(our, s) for s in seeds], [t3(ref, s) for s in seeds])},
+           "mean_test_accuracy_over_epoch_windows": window,
            "epochs": rows}
     with open(out_path, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps(doc["final"], indent=1))
     print(json.dumps(doc["last3_epochs_mean"], indent=1))
+    print(json.dumps(window, indent=1))
 
 
 def main() -> None:
