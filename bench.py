@@ -334,7 +334,7 @@ def mmimdb_bench(args) -> None:
                                "sample": f"{n} oracle MMIMDb train steps (fwd+BCE+bwd+Adam, fp32) at batch {B}, "
                                          f"{el:.1f}s, torch.set_num_threads({threads})"}
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.destroy_process_group()
 
@@ -470,7 +470,7 @@ def input_stage_bench(args) -> None:
                            "sample": f"{cnt} samples in the reference file layout through the reference's "
                                      f"per-sample host path (torch.load x2, cm.gist_earth, PIL convert L, "
                                      f"ToDtype scale, mask, stack, .to(cuda)), batch {B}, 1 thread, {el:.1f}s"}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def eval_bench(args) -> None:
@@ -565,7 +565,7 @@ def eval_bench(args) -> None:
         res["cpu_baseline"] = {"value": round(n * B / el, 1), "unit": "samples/sec", "cores": threads, "cpu_model": hcpu["model"], "host_cpus": hcpu, "kind": "port",
                                "sample": f"{n} oracle validation steps (eval fwd + CE + softmax argmax) at batch {B}, "
                                          f"{el:.1f}s, torch.set_num_threads({threads})"}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def mono_bench(args) -> None:
@@ -658,7 +658,7 @@ def mono_bench(args) -> None:
         res["cpu_baseline"] = {"value": round(n * B / el, 1), "unit": "samples/sec", "cores": threads, "cpu_model": hcpu["model"], "host_cpus": hcpu, "kind": "port",
                                "sample": f"{n} oracle monomodal train steps (ResNet18 + Linear, CE, Adam, fp32) at "
                                          f"batch {B}, {el:.1f}s, torch.set_num_threads({threads})"}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def _mosi_family(name: str) -> str:
@@ -800,12 +800,36 @@ def mosi_bench(args) -> None:
                                          f"to the reference on CPU) at batch {B}, T={T}, {el:.1f}s, "
                                          f"torch.set_num_threads({threads})"}
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.destroy_process_group()
 
 
+_JSON_FD = None
+
+
+def quiet_stdout() -> None:
+    """Route everything written to fd 1 (RCCL's init banner, library prints, Python prints) to stderr,
+    keeping a private duplicate of the real stdout for the ONE JSON result line (emit)."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    """Write the bench's one JSON line to the real stdout."""
+    line = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main() -> None:
+    quiet_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -1010,7 +1034,7 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(B, args.cpu_budget)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
