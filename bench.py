@@ -690,20 +690,21 @@ def mosi_bench(args) -> None:
     rank, world, local = ddp.init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    B, T = args.mosi_batch, 50
+    from types import SimpleNamespace
+    cname = "mosei" if args.mosei else "mosi"
+    cfg = SimpleNamespace(**M.YAML_CONFIGS[cname])
+    B, T = args.mosi_batch or cfg.batch, 50
     torch.manual_seed(0)
-    netA = M.LSTMEncoder(input_size=5, hidden_size=64, embd_method="last")
-    netV = M.LSTMEncoder(input_size=20, hidden_size=64, embd_method="last")
-    netT = M.TextCNN(input_size=768, embd_size=64, dropout=0.5, in_channels=1, out_channels=128, kernel_heights=[3, 4, 5])
-    netC = M.FcClassifier(input_dim=192, layers=[192, 64, 32], output_dim=3, dropout=0.5)
-    model = M.UttFusionModel(netA, netV, netT, netC, clip=1.0).to(dev)
-    opt = tspm_amd.FusedAdam(model.parameters(), lr=1e-3, weight_decay=1e-3, grad_scale=1.0 / world)
+    model = M.build_utt_fusion(cname).to(dev)
+    netT = model.netT
+    opt = tspm_amd.FusedAdam(model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay, grad_scale=1.0 / world)
     st = model.fused_step(opt, None, B, T)  # None: the config's single cross-entropy term, weight 1.0
     if world > 1:  # data parallel: one RCCL all-reduce of the flat gradient buffer per step, then clip + Adam
         for fg in opt.flat_groups():
             dist.broadcast(fg.param, src=0)
         st.allreduce = ddp.GradAllReduce([fg.grad for fg in opt.flat_groups()])
-    ds = MOSI(split="train", corpus=synthetic_mosi_corpus(args.mosi_corpus, 1234 + rank, T, min_len=20),
+    ds = MOSI(split="train", corpus=synthetic_mosi_corpus(args.mosi_corpus, 1234 + rank, T, min_len=20,
+                                                          feats=(cfg.audio_dim, cfg.video_dim, 768)),
               selected_patterns=["atv"], device=dev, seed=rank)
     ds.device_corpus  # upload once, outside the timed region
     gen = torch.Generator().manual_seed(1234 + rank)
@@ -740,7 +741,7 @@ def mosi_bench(args) -> None:
                                        "(LDS-staged MFMA 32x32x2 fp32), 3 launches per step",
             "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
             "flop_per_step": conv_flops, "achieved": None, "frac": None}
-    tr, tr_launches, tr_src = pmc_traffic("conv", "mosi") if B == 128 else (None, None, None)
+    tr, tr_launches, tr_src = pmc_traffic("conv", "mosi") if (B == 128 and not args.mosei) else (None, None, None)
     if tr:
         roof.update({"traffic": tr, "traffic_per_launch": round(tr / tr_launches) if tr_launches else None,
                      "traffic_unit": "HBM bytes per step of the TextCNN convs (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
@@ -768,15 +769,18 @@ def mosi_bench(args) -> None:
                                          sorted(names.items(), key=lambda kv: -kv[1][1])},
                      "timing": f"device kernel durations (torch.profiler = rocprofiler timestamps) of {R} graph "
                                "replays after the timed region (one stream)"})
-    res = {"metric": "samples/sec MOSI UTT-Fusion (LSTM audio/video + TextCNN text + FcClassifier) train step "
-                     "(BASELINE.json configs[4])",
+    name = ("MOSEI UTT-Fusion (configs/mosei/centralised/utt_fusion_train_mosei.yaml: maxpool LSTMs, BN classifier)"
+            if args.mosei else "MOSI UTT-Fusion (LSTM audio/video + TextCNN text + FcClassifier)")
+    res = {"metric": f"samples/sec {name} train step" + ("" if args.mosei else " (BASELINE.json configs[4])"),
            "value": round(value, 2), "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32",
-           "data": f"synthetic MOSI-shaped ragged corpus of {args.mosi_corpus} samples (audio 5-d, video 20-d, text "
-                   "768-d, lengths U[20,50]) resident in HBM, padded to 50 and gathered on device each step; random-"
-                   "init weights (seed 0)",
-           "config": {"workload": "mosi_utt_fusion_train_step(lstm x2, textcnn, fc classifier, CE, clip 1.0, Adam)",
+           "data": f"synthetic {'MOSEI' if args.mosei else 'MOSI'}-shaped ragged corpus of {args.mosi_corpus} samples "
+                   f"(audio {cfg.audio_dim}-d, video {cfg.video_dim}-d, text 768-d, lengths U[20,50]) resident in HBM, "
+                   "padded to 50 and gathered on device each step; random-init weights (seed 0)",
+           "config": {"workload": f"{'mosei' if args.mosei else 'mosi'}_utt_fusion_train_step(lstm x2 "
+                                  f"[{cfg.embd_method}], textcnn, fc classifier{' +bn' if cfg.use_bn else ''}, CE, "
+                                  f"clip {cfg.clip}, Adam)",
                       "per_rank_batch": B, "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                       "params": sum(p.numel() for p in model.parameters())},
            "roofline": roof, "final_loss": round(st.eng.loss.item(), 5)}
@@ -785,9 +789,10 @@ def mosi_bench(args) -> None:
         from oracle.avmnist_ref import OracleAdam
         threads, hcpu = cpu_threads()
         torch.set_num_threads(threads)
-        ref = mref.build_oracle_utt(0)
-        ropt = OracleAdam(list(ref.parameters()), lr=1e-3, weight_decay=1e-3)
-        A, V, X, y = mref.synthetic_batch(B, T, seed=1234)
+        ocfg = mref.MOSEI if args.mosei else mref.MOSI
+        ref = mref.build_oracle_utt(0, cfg=ocfg)
+        ropt = OracleAdam(list(ref.parameters()), lr=cfg.lr, weight_decay=cfg.weight_decay)
+        A, V, X, y = mref.synthetic_batch(B, T, seed=1234, cfg=ocfg)
         mref.train_step(ref, ropt, A, V, X, y)
         n, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < args.cpu_budget and n < 500:
@@ -854,7 +859,9 @@ def main() -> None:
     ap.add_argument("--mmimdb-pooling", default=None, choices=["max", "avg", "sum", "attention", "gated"],
                     help="--mmimdb with multimodal_pooling fusion instead of the GMU")
     ap.add_argument("--mosi", action="store_true", help="BASELINE configs[4]: MOSI UTT-Fusion step (one JSON line)")
-    ap.add_argument("--mosi-batch", type=int, default=128)
+    ap.add_argument("--mosi-batch", type=int, default=0, help="default 128 (MOSI YAML) / 256 (--mosei YAML)")
+    ap.add_argument("--mosei", action="store_true",
+                    help="--mosi with the MOSEI UTT-Fusion config (maxpool LSTM embeddings, BN classifier, clip 0.5)")
     ap.add_argument("--mosi-corpus", type=int, default=4096, help="samples in the HBM-resident MOSI corpus")
     ap.add_argument("--profile-steps", type=int, default=10,
                     help="step replays profiled after the timed region for the roofline (0: skip)")

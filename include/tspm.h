@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 13
+#define TSPM_ABI_VERSION 14
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -491,6 +491,18 @@ int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const fl
 int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
                          const float* invstd, const float* gamma, float* dgamma, float* dbeta, const float* a,
                          const uint8_t* keep, float keep_scale, float* da, tspm_stream_t stream);
+/* BatchNorm1d followed by Dropout (FcClassifier(use_bn=True): Linear -> ReLU -> BatchNorm1d -> Dropout,
+ * models/msa/networks/classifier.py:98-104; ABI 14): tspm_bn1d_fwd, then y *= keep ? keep_scale : 0
+ * (keep uint8 [m, c], nullable = no dropout). */
+int tspm_bn1d_fwd_drop(int32_t m, int32_t c, const float* x, const float* gamma, const float* beta,
+                       float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                       float* save_invstd, const uint8_t* keep, float keep_scale, float* y, tspm_stream_t stream);
+/* Its backward (ABI 14): g is the gradient of the Dropout output (g_keep nullable), x the BatchNorm input =
+ * a ReLU output; dgamma / dbeta as tspm_bn1d_bwd on g*keep*g_scale, dx (nullable) = the BN input gradient
+ * with the ReLU's mask applied (0 where x <= 0) — the gradient of the Linear that fed the ReLU. */
+int tspm_bn1d_bwd_drop_relu(int32_t m, int32_t c, const float* g, const uint8_t* g_keep, float g_scale,
+                            const float* x, const float* mean, const float* invstd, const float* gamma,
+                            float* dgamma, float* dbeta, float* dx, tspm_stream_t stream);
 /* Two independent BatchNorm1d layers over the same m rows in one launch (the MMIMDb image and text
  * encoders' input BNs; ABI 11): each half exactly as tspm_bn1d_fwd / tspm_bn1d_bwd (bitwise). */
 int tspm_bn1d_fwd_pair(int32_t m, int32_t c0, const float* x0, const float* gamma0, const float* beta0,
@@ -516,11 +528,14 @@ int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float
  * configs/mosi/centralised/utt_fusion_base_training.yaml.  Sequences are time-major on the device:
  * row (t, b) of a [T][B][F] tensor.
  * ----------------------------------------------------------------------------------------------*/
-/* nn.LSTM(input, hidden, batch_first=True), one layer, zero initial state, embd_method "last"
- * (models/msa/networks/lstm.py:8-67; the reference runs the padded length, no packing).  xg = x W_ih^T
- * + b_ih for all steps (a tspm_linear_fwd over the T*B rows); the recurrence adds h W_hh^T + b_hh.
- * Saved for the backward: activated gates i,f,g,o [T][B][4H], c_t [T][B][H], h_t [T+1][B][H]
- * (hs[0] = h0 = 0).  h_T goes to h_out (row stride ld_out).  hidden must be 64 and batch even. */
+/* nn.LSTM(input, hidden, batch_first=True), one layer, zero initial state, embd_method "last" or
+ * "maxpool" (models/msa/networks/lstm.py:8-67; the reference runs the padded length, no packing).
+ * xg = x W_ih^T + b_ih for all steps (a tspm_linear_fwd over the T*B rows); the recurrence adds
+ * h W_hh^T + b_hh.  Saved for the backward: activated gates i,f,g,o [T][B][4H], c_t [T][B][H], h_t
+ * [T+1][B][H] (hs[0] = h0 = 0).  argmax NULL ("last"): h_T goes to h_out (row stride ld_out); argmax
+ * non-NULL ("maxpool", ABI 14; lstm.py:47-52 F.max_pool1d over r_out): max over t of h_t goes to h_out
+ * and its time index (first maximum, NaN wins) to argmax uint8 [batch][hidden] (steps <= 256).  hidden
+ * must be 64 and batch even. */
 typedef struct tspm_lstm_fwd_desc {
   int32_t batch, steps, hidden, ld_out;
   const float* xg;
@@ -530,10 +545,12 @@ typedef struct tspm_lstm_fwd_desc {
   float* cs;
   float* hs;
   float* h_out;
+  uint8_t* argmax; /* nullable; ABI 14 */
 } tspm_lstm_fwd_desc;
 /* 1 or 2 independent LSTMs (the audio and video encoders) in one launch. */
 int tspm_lstm_fwd(int32_t count, const tspm_lstm_fwd_desc* descs, tspm_stream_t stream);
-/* Backward through time from dh (the gradient of h_T, row stride ld_dh): writes the pre-activation
+/* Backward through time from dh (the gradient of the embedding, row stride ld_dh: of h_T, or with
+ * argmax (ABI 14) of h_{argmax} per unit, the max-pool backward): writes the pre-activation
  * gate gradients dgates [T][B][4H].  The weight gradients are then GEMMs over the T*B rows:
  * dW_hh = dgates^T hs[0:T], dW_ih = dgates^T x, db_hh = db_ih = column sums of dgates. */
 typedef struct tspm_lstm_bwd_desc {
@@ -543,6 +560,7 @@ typedef struct tspm_lstm_bwd_desc {
   const float* cs;
   const float* dh;
   float* dgates;
+  const uint8_t* argmax; /* nullable; ABI 14 */
 } tspm_lstm_bwd_desc;
 int tspm_lstm_bwd(int32_t count, const tspm_lstm_bwd_desc* descs, tspm_stream_t stream);
 /* TextCNN pooling (models/msa/networks/textcnn.py:56-67): for conv i (kernel height heights[i], output

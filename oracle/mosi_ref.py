@@ -5,28 +5,34 @@ leg may import it; the product package never does.
 Restates (reference = TArsenii/task-specific-pretraining-multimodal, paths under ``MML_Suite/``):
 
 * ``LSTMEncoder``   models/msa/networks/lstm.py:8-67 — nn.LSTM(input, hidden, batch_first=True), zero
-                    initial state, the padded length run in full (no packing), embd "last" = h_n
+                    initial state, the padded length run in full (no packing), embd "last" = h_n or
+                    "maxpool" = F.max_pool1d over the time axis of r_out (lstm.py:47-52)
 * ``TextCNN``       models/msa/networks/textcnn.py:10-69 — three nn.Conv2d(1, C, (k, input)), ReLU,
                     max over time, cat, Dropout, Linear + ReLU
-* ``FcClassifier``  models/msa/networks/classifier.py:83-117 — (Linear, ReLU, Dropout) per layer, fc_out
+* ``FcClassifier``  models/msa/networks/classifier.py:83-117 — (Linear, ReLU, [BatchNorm1d if use_bn,]
+                    Dropout) per layer, fc_out
 * ``UttFusionModel`` forward / train_step — models/msa/utt_fusion.py:105-200: cat(A, V, T) embeddings →
                     classifier → CE(logits.squeeze(), labels.squeeze()) → backward →
                     clip_grad_norm_(parameters, clip) → Adam
                     (configs/mosi/centralised/utt_fusion_base_training.yaml: hidden 64, 3x128 filters of
                     heights 3/4/5 over 768-d text, classifier 192 → 192/64/32 → 3, dropout 0.5, clip 1.0,
-                    Adam lr 1e-3 / wd 1e-3)
+                    Adam lr 1e-3 / wd 1e-3); the MOSEI config (configs/mosei/centralised/
+                    utt_fusion_train_mosei.yaml) is ``MOSEI``: 74/35-d inputs, "maxpool" embeddings,
+                    TextCNN dropout 0.7, classifier 192 → 96/48 → 3 with use_bn and dropout 0.66, clip 0.5
 
 Module attribute names follow the reference (identical state_dict keys); construction order is the
 YAML's (netA, netV, netT, netC), so ``torch.manual_seed(s)`` before construction reproduces the
 reference's initial weights.  Dropout takes explicit keep masks; ``MosiTrace`` records or forces the
 ReLU and time-max decisions (parity instrument, as avmnist_ref.MaskTrace).
 
-Pinned: ``tests/golden/mosi_step_b4.npz`` was produced by the REAL reference modules
-(``tests/golden/make_mosi_golden.py``); ``tests/test_mosi_cpu.py`` checks this restatement against it.
+Pinned: ``tests/golden/mosi_step_b4.npz`` and ``mosei_step_b4.npz`` were produced by the REAL reference
+modules (``tests/golden/make_mosi_golden.py [mosei]``); ``tests/test_mosi_cpu.py`` checks this restatement
+against both.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -38,12 +44,35 @@ AUDIO_DIM, VIDEO_DIM, TEXT_DIM, HIDDEN, FILTERS, HEIGHTS = 5, 20, 768, 64, 128, 
 CLS_LAYERS, CLASSES = (192, 64, 32), 3
 
 
+@dataclass(frozen=True)
+class UttConfig:
+    """The YAML's model block (netA / netV / netT / netC / clip) and its optimizer."""
+    audio_dim: int = AUDIO_DIM
+    video_dim: int = VIDEO_DIM
+    text_dim: int = TEXT_DIM
+    embd_method: str = "last"
+    text_dropout: float = 0.5
+    cls_layers: Tuple[int, ...] = CLS_LAYERS
+    cls_dropout: float = 0.5
+    use_bn: bool = False
+    clip: float = 1.0
+    lr: float = 1e-3
+    weight_decay: float = 1e-3
+
+
+# configs/mosi/centralised/utt_fusion_base_training.yaml
+MOSI = UttConfig()
+# configs/mosei/centralised/utt_fusion_train_mosei.yaml
+MOSEI = UttConfig(audio_dim=74, video_dim=35, embd_method="maxpool", text_dropout=0.7, cls_layers=(96, 48),
+                  cls_dropout=0.66, use_bn=True, clip=0.5, lr=2e-4, weight_decay=1e-5)
+
+
 class OracleLSTMEncoder(nn.Module):
     def __init__(self, input_size: int, hidden_size: int, embd_method: str = "last"):
         super().__init__()
         self.input_size, self.hidden_size = input_size, hidden_size
         self.rnn = nn.LSTM(input_size, hidden_size, batch_first=True)
-        assert embd_method == "last"
+        assert embd_method in ("last", "maxpool")
         self.embd_method = embd_method
 
 
@@ -61,11 +90,14 @@ class OracleTextCNN(nn.Module):
 
 
 class OracleFcClassifier(nn.Module):
-    def __init__(self, input_dim: int, layers: List[int], output_dim: int, dropout: float = 0.3):
+    def __init__(self, input_dim: int, layers: List[int], output_dim: int, dropout: float = 0.3,
+                 use_bn: bool = False):
         super().__init__()
         mods = []
         for width in layers:
             mods += [nn.Linear(input_dim, width), nn.ReLU()]
+            if use_bn:
+                mods.append(nn.BatchNorm1d(width))
             if dropout > 0:
                 mods.append(nn.Dropout(dropout))
             input_dim = width
@@ -82,21 +114,23 @@ class OracleUttFusion(nn.Module):
         self.clip = clip
 
 
-def build_oracle_utt(seed: int = 0, audio_dim=AUDIO_DIM, video_dim=VIDEO_DIM, text_dim=TEXT_DIM) -> OracleUttFusion:
+def build_oracle_utt(seed: int = 0, audio_dim=None, video_dim=None, text_dim=None,
+                     cfg: UttConfig = MOSI) -> OracleUttFusion:
     torch.manual_seed(seed)
-    a = OracleLSTMEncoder(audio_dim, HIDDEN)
-    v = OracleLSTMEncoder(video_dim, HIDDEN)
-    t = OracleTextCNN(text_dim, embd_size=HIDDEN, dropout=0.5, in_channels=1, out_channels=FILTERS,
-                      kernel_heights=list(HEIGHTS))
-    c = OracleFcClassifier(3 * HIDDEN, list(CLS_LAYERS), CLASSES, dropout=0.5)
-    return OracleUttFusion(a, v, t, c, clip=1.0)
+    a = OracleLSTMEncoder(audio_dim or cfg.audio_dim, HIDDEN, cfg.embd_method)
+    v = OracleLSTMEncoder(video_dim or cfg.video_dim, HIDDEN, cfg.embd_method)
+    t = OracleTextCNN(text_dim or cfg.text_dim, embd_size=HIDDEN, dropout=cfg.text_dropout, in_channels=1,
+                      out_channels=FILTERS, kernel_heights=list(HEIGHTS))
+    c = OracleFcClassifier(3 * HIDDEN, list(cfg.cls_layers), CLASSES, dropout=cfg.cls_dropout, use_bn=cfg.use_bn)
+    return OracleUttFusion(a, v, t, c, clip=cfg.clip)
 
 
 class MosiTrace:
     """Parity instrument (test infrastructure): records — or, with ``force``, replaces — the ReLU masks
     and time-max argmax decisions of the forward.  Sites: ``text.pool{i}`` (time argmax of conv i, int64
     [B, C]), ``text.relu{i}`` (ReLU of the pooled conv i value, bool [B, C]), ``text.embd`` and
-    ``cls.relu{j}`` (bool masks)."""
+    ``cls.relu{j}`` (bool masks), ``lstm.{a,v}.pool`` (time argmax of the "maxpool" embedding, int64
+    [B, H])."""
 
     def __init__(self, force: Optional[Dict[str, torch.Tensor]] = None):
         self.force = force
@@ -122,9 +156,25 @@ class MosiTrace:
         return at * self.force[site_r].to(device=at.device, dtype=at.dtype)
 
 
-def lstm_forward(enc: OracleLSTMEncoder, x: torch.Tensor) -> torch.Tensor:
-    _, (h_n, _) = enc.rnn(x)
-    return h_n.squeeze(0)
+    def lstm_max(self, site, r_out):  # r_out [B, T, H]
+        in_feat = r_out.transpose(1, 2)
+        _, idx = F.max_pool1d(in_feat, in_feat.size(2), in_feat.size(2), return_indices=True)
+        self.pre[site] = r_out.detach()
+        self.idx[site] = idx.squeeze(2)
+        if self.force is None or site not in self.force:
+            return F.max_pool1d(in_feat, in_feat.size(2), in_feat.size(2)).squeeze(-1)
+        return in_feat.gather(2, self.force[site].to(r_out.device).unsqueeze(2)).squeeze(2)
+
+
+def lstm_forward(enc: OracleLSTMEncoder, x: torch.Tensor, trace: Optional[MosiTrace] = None,
+                 site: str = "lstm") -> torch.Tensor:
+    r_out, (h_n, _) = enc.rnn(x)
+    if enc.embd_method == "last":
+        return h_n.squeeze(0)
+    if trace is not None:
+        return trace.lstm_max(site, r_out)
+    in_feat = r_out.transpose(1, 2)  # lstm.py:47-52
+    return F.max_pool1d(in_feat, in_feat.size(2), in_feat.size(2)).squeeze(-1)
 
 
 def textcnn_forward(net: OracleTextCNN, x: torch.Tensor, training: bool, keep: Optional[torch.Tensor],
@@ -149,9 +199,12 @@ def textcnn_forward(net: OracleTextCNN, x: torch.Tensor, training: bool, keep: O
 def classifier_forward(net: OracleFcClassifier, x: torch.Tensor, training: bool,
                        keeps: Optional[List[torch.Tensor]], trace: Optional[MosiTrace] = None) -> torch.Tensor:
     lin = [m for m in net.module if isinstance(m, nn.Linear)]
+    bns = [m for m in net.module if isinstance(m, nn.BatchNorm1d)]
     for j, l in enumerate(lin):
         z = F.linear(x, l.weight, l.bias)
         x = F.relu(z) if trace is None else trace.relu(f"cls.relu{j}", z)
+        if bns:
+            x = bns[j](x)  # the module: batch statistics + running-stat update in train mode
         if training and net.p > 0:
             x = x * (keeps[j].to(x.dtype) / (1.0 - net.p)) if keeps is not None else F.dropout(x, net.p, True)
     return F.linear(x, net.fc_out.weight, net.fc_out.bias)
@@ -161,8 +214,8 @@ def forward(model: OracleUttFusion, A, V, T, training: bool, keeps: Optional[Dic
             trace: Optional[MosiTrace] = None) -> torch.Tensor:
     """models/msa/utt_fusion.py:105-140 (all three modalities present)."""
     keeps = keeps or {}
-    a = lstm_forward(model.netA, A)
-    v = lstm_forward(model.netV, V)
+    a = lstm_forward(model.netA, A, trace, "lstm.a.pool")
+    v = lstm_forward(model.netV, V, trace, "lstm.v.pool")
     t = textcnn_forward(model.netT, T, training, keeps.get("text"), trace)
     ck = [keeps[f"cls{j}"] for j in range(len(model.netC.widths))] if "cls0" in keeps else None
     return classifier_forward(model.netC, torch.cat([a, v, t], dim=-1), training, ck, trace)
@@ -195,13 +248,15 @@ def validation_step(model: OracleUttFusion, A, V, T, labels) -> Dict:
     return {"loss": loss, "logits": logits, "preds": F.softmax(logits, dim=-1).argmax(dim=-1)}
 
 
-def synthetic_batch(n: int, steps: int = 50, seed: int = 1234, lengths: Optional[List[int]] = None):
-    """MOSI-shaped batch (aligned_50: 5-d COVAREP audio, 20-d Facet video, 768-d BERT text, 3 classes).
-    ``lengths``: per-sample valid steps; the rest is zero padding (pad_sequence)."""
+def synthetic_batch(n: int, steps: int = 50, seed: int = 1234, lengths: Optional[List[int]] = None,
+                    cfg: UttConfig = MOSI):
+    """MOSI-shaped batch (aligned_50: 5-d COVAREP audio, 20-d Facet video, 768-d BERT text, 3 classes; the
+    MOSEI config's 74-d / 35-d with ``cfg=MOSEI``).  ``lengths``: per-sample valid steps; the rest is zero
+    padding (pad_sequence)."""
     g = torch.Generator().manual_seed(seed)
-    A = torch.randn(n, steps, AUDIO_DIM, generator=g)
-    V = 0.5 * torch.randn(n, steps, VIDEO_DIM, generator=g)
-    T = 0.3 * torch.randn(n, steps, TEXT_DIM, generator=g)
+    A = torch.randn(n, steps, cfg.audio_dim, generator=g)
+    V = 0.5 * torch.randn(n, steps, cfg.video_dim, generator=g)
+    T = 0.3 * torch.randn(n, steps, cfg.text_dim, generator=g)
     if lengths is not None:
         for i, ln in enumerate(lengths):
             A[i, ln:] = 0
@@ -211,9 +266,10 @@ def synthetic_batch(n: int, steps: int = 50, seed: int = 1234, lengths: Optional
     return A, V, T, y
 
 
-def keep_masks(n: int, seed: int, p: float = 0.5) -> Dict[str, torch.Tensor]:
+def keep_masks(n: int, seed: int, p: Optional[float] = None, cfg: UttConfig = MOSI) -> Dict[str, torch.Tensor]:
     g = torch.Generator().manual_seed(seed)
-    out = {"text": (torch.rand(n, 3 * FILTERS, generator=g) >= p).to(torch.uint8)}
-    for j, w in enumerate(CLS_LAYERS):
-        out[f"cls{j}"] = (torch.rand(n, w, generator=g) >= p).to(torch.uint8)
+    pt, pc = (cfg.text_dropout, cfg.cls_dropout) if p is None else (p, p)
+    out = {"text": (torch.rand(n, 3 * FILTERS, generator=g) >= pt).to(torch.uint8)}
+    for j, w in enumerate(cfg.cls_layers):
+        out[f"cls{j}"] = (torch.rand(n, w, generator=g) >= pc).to(torch.uint8)
     return out

@@ -92,17 +92,21 @@ def _keep(seed: int, epoch: int, b: int, n: int) -> torch.Tensor:
     return (torch.rand(n, 128, generator=g) >= 0.5).to(torch.uint8)
 
 
-def reference(epochs: int, seed: int) -> None:
+def reference(epochs: int, seed: int, device: str = "cpu") -> None:
+    """The reference's step (oracle/avmnist_ref.py = models/avmnist.py:269-310 restated).  ``device="cuda"``
+    runs the SAME torch code through ATen/MIOpen on the GPU (the reference as PyTorch would run it on an
+    MI355X) — the paired design needs only that the two sides differ in fp32 rounding, nothing else."""
     from oracle import avmnist_eval_ref as eref
     from oracle import avmnist_ref as orc
     tr, te = _load()
+    dev = torch.device(device)
     lut = torch.from_numpy(_lut().astype(np.int64))
 
     def tensors(c, rows):
         a = torch.from_numpy(np.asarray(c.audio[rows]))
         i = (lut[torch.from_numpy(np.asarray(c.image[rows])).long()].float() * (1.0 / 255.0)).unsqueeze(1)
-        return a, i, torch.from_numpy(np.asarray(c.labels[rows]))
-    model = orc.build_oracle_avmnist(seed)
+        return a.to(dev), i.to(dev), torch.from_numpy(np.asarray(c.labels[rows])).to(dev)
+    model = orc.build_oracle_avmnist(seed).to(dev)
     opt = orc.OracleAdam(list(model.parameters()), lr=5e-4, weight_decay=1e-4)
     curve = []
     for ep in range(epochs):
@@ -112,20 +116,23 @@ def reference(epochs: int, seed: int) -> None:
         model.train()
         for b in range(0, len(order), BATCH):
             a, i, lab = tensors(tr, order[b:b + BATCH])
-            keep = _keep(seed, ep, b // BATCH, lab.numel())
-            losses.append(orc.train_step(model, opt, a, i, lab, keep)["loss"].item())
+            keep = _keep(seed, ep, b // BATCH, lab.numel()).to(dev)
+            losses.append(orc.train_step(model, opt, a, i, lab, keep)["loss"].detach())
         model.eval()
         correct = 0
         for b in range(0, len(te), BATCH):
             rows = np.arange(b, min(len(te), b + BATCH))
             a, i, lab = tensors(te, rows)
             correct += int((eref.validation_step(model, a, i, lab)["preds"] == lab).sum())
-        curve.append({"epoch": ep + 1, "train_loss": float(np.mean(losses)), "test_accuracy": correct / len(te),
-                      "seconds": round(time.time() - t0, 1)})
+        curve.append({"epoch": ep + 1, "train_loss": float(np.mean([x.item() for x in losses])),
+                      "test_accuracy": correct / len(te), "seconds": round(time.time() - t0, 1)})
         print(json.dumps(curve[-1]), flush=True)
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(OUT, f"accuracy_reference_s{seed}.json"), "w") as f:
-        json.dump({"side": "reference (oracle on CPU)", "seed": seed, "threads": torch.get_num_threads(),
+    tag = "" if device == "cpu" else "gpu_"
+    side = ("reference (oracle on CPU: bit-exact to the reference)" if device == "cpu" else
+            "reference (oracle = the reference's torch code, ATen/MIOpen on the MI355X)")
+    with open(os.path.join(OUT, f"accuracy_reference_{tag}s{seed}.json"), "w") as f:
+        json.dump({"side": side, "seed": seed, "device": device, "threads": torch.get_num_threads(),
                    "curve": curve}, f, indent=1)
 
 
@@ -170,7 +177,7 @@ def ours(epochs: int, seed: int) -> None:
         json.dump({"side": "ours (HIP path, MI355X)", "seed": seed, "curve": curve}, f, indent=1)
 
 
-def compare(out_path: str) -> None:
+def compare(out_path: str, ref_side: str = "reference") -> None:
     from scipy import stats
 
     def runs(side):
@@ -179,7 +186,7 @@ def compare(out_path: str) -> None:
             d = json.load(open(p))
             out[d["seed"]] = d["curve"]
         return out
-    ref, our = runs("reference"), runs("ours")
+    ref, our = runs(ref_side), runs("ours")
     seeds = sorted(set(ref) & set(our))
     n = min(min(len(ref[s]) for s in seeds), min(len(our[s]) for s in seeds))
     rows = []
@@ -219,6 +226,7 @@ def compare(out_path: str) -> None:
                    "speaker-disjoint test; own pairing — the reference's split CSVs are absent); paired runs: "
                    "same initial weights (seed s), batch order and dropout masks on both sides; batch 128, "
                    "Adam 5e-4 / 1e-4, dropout 0.5",
+           "reference_side": json.load(open(glob.glob(os.path.join(OUT, f"accuracy_{ref_side}_s*.json"))[0]))["side"],
            "seeds": seeds, "epochs_compared": n, "test_samples": TEST_PER_DIGIT * 10,
            "one_sample_pp": round(100 / (TEST_PER_DIGIT * 10), 4),
            "reference_published": {"test_accuracy_scratch_20ep": 0.9870, "source": "README.md:26-29 / "
@@ -246,6 +254,7 @@ def main() -> None:
     ap.add_argument("--seeds", default="0", help="comma-separated dropout seeds (one run each)")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r2_accuracy_parity.json"))
     ap.add_argument("--threads", type=int, default=0, help="reference side: torch threads (0 = all)")
+    ap.add_argument("--device", default="cpu", help="reference side: cpu (bit-exact oracle) or cuda (ATen)")
     a = ap.parse_args()
     if a.what == "prepare":
         prepare()
@@ -253,12 +262,12 @@ def main() -> None:
         if a.threads:
             torch.set_num_threads(a.threads)
         for sd in a.seeds.split(","):
-            reference(a.epochs, int(sd))
+            reference(a.epochs, int(sd), a.device)
     elif a.what == "ours":
         for sd in a.seeds.split(","):
             ours(a.epochs, int(sd))
     else:
-        compare(a.out)
+        compare(a.out, "reference_gpu" if a.device == "cuda" else "reference")
 
 
 if __name__ == "__main__":

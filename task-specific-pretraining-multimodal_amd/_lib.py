@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -73,15 +73,15 @@ class LinearBwdDesc(Structure):
 # name -> (restype, argtypes)
 _P = c_void_p
 class LstmFwdDesc(Structure):
-    """tspm_lstm_fwd_desc (ABI 12)."""
+    """tspm_lstm_fwd_desc (ABI 12; argmax ABI 14)."""
     _fields_ = [(n, c_int32) for n in ("batch", "steps", "hidden", "ld_out")] + \
-        [(n, c_void_p) for n in ("xg", "w_hh", "b_hh", "gates", "cs", "hs", "h_out")]
+        [(n, c_void_p) for n in ("xg", "w_hh", "b_hh", "gates", "cs", "hs", "h_out", "argmax")]
 
 
 class LstmBwdDesc(Structure):
-    """tspm_lstm_bwd_desc (ABI 12)."""
+    """tspm_lstm_bwd_desc (ABI 12; argmax ABI 14)."""
     _fields_ = [(n, c_int32) for n in ("batch", "steps", "hidden", "ld_dh")] + \
-        [(n, c_void_p) for n in ("w_hh", "gates", "cs", "dh", "dgates")]
+        [(n, c_void_p) for n in ("w_hh", "gates", "cs", "dh", "dgates", "argmax")]
 
 
 _SIGS = {
@@ -161,6 +161,9 @@ _SIGS = {
     "tspm_maxout_bwd": (c_int32, [c_int32, c_int32, _P, c_int32, _P, c_int32, _P, c_float, _P, c_int32, _P]),
     "tspm_bn1d_fwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, _P]),
     "tspm_bn1d_bwd": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "tspm_bn1d_fwd_drop": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, c_float, _P,
+                                     _P]),
+    "tspm_bn1d_bwd_drop_relu": (c_int32, [c_int32, c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P]),
     "tspm_bn1d_bwd_maxout": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_bn1d_fwd_pair": (c_int32, [c_int32] + ([c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P] * 2)
                            + [_P]),

@@ -232,6 +232,8 @@ struct Bn1dFwd {
   float* smean;
   float* sinvstd;
   float* y;
+  const uint8_t* keep;  // optional Dropout after the BN (tspm_bn1d_fwd_drop): y *= keep ? keep_scale : 0
+  float keep_scale;
 };
 
 TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red);
@@ -284,7 +286,8 @@ TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red) {
   const float ga = p.gamma[ch], be = p.beta[ch];
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
-    p.y[i] = (x[i] - mean) * invstd * ga + be;
+    const float v = (x[i] - mean) * invstd * ga + be;
+    p.y[i] = p.keep ? v * (p.keep[i] ? p.keep_scale : 0.f) : v;
   }
 }
 
@@ -302,6 +305,9 @@ struct Bn1dBwd {
   const uint8_t* mo_keep;
   float mo_scale;
   float* mo_da;
+  const uint8_t* g_keep;  // tspm_bn1d_bwd_drop_relu: g is the gradient of Dropout(BN(x)) -> g*keep*g_scale,
+  float g_scale;          // and x is a ReLU output: dx = 0 where x <= 0
+  int relu_x;
 };
 
 TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red);
@@ -336,12 +342,15 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
   const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
+  const uint8_t* __restrict__ gk = p.g_keep;
+  const float gs = p.g_scale;
+  auto gval = [&](long long i) -> float { return gk ? g[i] * (gk[i] ? gs : 0.f) : g[i]; };
   double sg = 0.0, sgx = 0.0;
   if (ok)
 #pragma unroll 4
     for (int r = grp; r < m; r += kBnGroups) {
       const long long i = (long long)r * c + ch;
-      const double gv = (double)g[i];
+      const double gv = (double)gval(i);
       sg += gv;
       sgx = fma(gv, ((double)x[i] - (double)mean) * (double)invstd, sgx);
     }
@@ -356,7 +365,8 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   const double k = (double)gamma[ch] * (double)invstd, mg = tg / (double)m, mgx = tgx / (double)m;
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
-    const float v = (float)(k * ((double)g[i] - mg - ((double)x[i] - (double)mean) * (double)invstd * mgx));
+    float v = (float)(k * ((double)gval(i) - mg - ((double)x[i] - (double)mean) * (double)invstd * mgx));
+    if (p.relu_x && !(x[i] > 0.f)) v = 0.f;
     if (dx) dx[i] = v;
     if (mo_da) {  // x was MaxOut(2)+Dropout of a[m, 2c]: route v as k_maxout_bwd does
       const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;
@@ -594,6 +604,29 @@ extern "C" int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const 
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta || !a || !da)
     return TSPM_ERR_INVALID;
   const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da};
+  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+                     m, p);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_fwd_drop(int32_t m, int32_t c, const float* x, const float* gamma, const float* beta,
+                                  float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                                  float* save_invstd, const uint8_t* keep, float keep_scale, float* y,
+                                  tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || !x || !gamma || !beta || !save_mean || !save_invstd || !y) return TSPM_ERR_INVALID;
+  const Bn1dFwd p{c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y, keep, keep_scale};
+  hipLaunchKernelGGL(k_bn1d_fwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+                     m, p);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn1d_bwd_drop_relu(int32_t m, int32_t c, const float* g, const uint8_t* g_keep, float g_scale,
+                                       const float* x, const float* mean, const float* invstd, const float* gamma,
+                                       float* dgamma, float* dbeta, float* dx, tspm_stream_t stream) {
+  if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
+  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr, g_keep, g_scale, 1};
   hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();

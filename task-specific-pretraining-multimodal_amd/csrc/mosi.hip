@@ -30,8 +30,9 @@ struct LstmFwdDesc {
   float* gates;      // [T][B][4H] activated i, f, g, o
   float* cs;         // [T][B][H]
   float* hs;         // [T+1][B][H], hs[0] = 0
-  float* hout;       // h_T rows, stride ldh
+  float* hout;       // h_T rows (embd "last") or max_t h_t (embd "maxpool"), stride ldh
   int ldh;
+  uint8_t* arg;      // embd "maxpool": [B][H] time index of the maximum (F.max_pool1d), else null
 };
 
 template <int H, int RB>
@@ -52,6 +53,8 @@ TSPM_DEV void lstm_fwd_body(const LstmFwdDesc& d, int chunk) {
   const bool cell = j < RB * H;
   const int cr = j / H, cu = j - (j / H) * H;
   float c = 0.f, h = 0.f;
+  float mx = -INFINITY;  // embd "maxpool": running max over t of h_t and its first index (NaN wins, as
+  int am = 0;            // max_pool2d_with_indices: val > max || isnan(val))
   if (cell) {
     hsh[cr][cu] = 0.f;
     d.hs[(long long)(b0 + cr) * H + cu] = 0.f;
@@ -88,10 +91,17 @@ TSPM_DEV void lstm_fwd_body(const LstmFwdDesc& d, int chunk) {
       d.cs[o] = c;
       d.hs[o + (long long)B * H] = h;
       hsh[cr][cu] = h;
+      if (d.arg && (h > mx || h != h)) {
+        mx = h;
+        am = t;
+      }
     }
     __syncthreads();
   }
-  if (cell) d.hout[(long long)(b0 + cr) * d.ldh + cu] = h;
+  if (cell) {
+    d.hout[(long long)(b0 + cr) * d.ldh + cu] = d.arg ? mx : h;
+    if (d.arg) d.arg[(long long)(b0 + cr) * H + cu] = (uint8_t)am;
+  }
 }
 
 template <int H, int RB>
@@ -113,9 +123,10 @@ struct LstmBwdDesc {
   const float* whh;    // [4H][H]
   const float* gates;  // [T][B][4H]
   const float* cs;     // [T][B][H]
-  const float* dh;     // gradient of h_T rows, stride lddh
+  const float* dh;     // gradient of the embedding rows (h_T, or max_t h_t at arg), stride lddh
   int lddh;
   float* dgates;       // [T][B][4H] out
+  const uint8_t* arg;  // embd "maxpool": [B][H] time index that received the embedding (null: T-1)
 };
 
 template <int H, int RB>
@@ -132,11 +143,20 @@ TSPM_DEV void lstm_bwd_body(const LstmBwdDesc& d, int chunk) {
   for (int jj = 0; jj < H; ++jj) wc[jj] = d.whh[(long long)(q * H + jj) * H + k];
   const bool cell = tid < RB * H;
   const int cr = tid / H, cu = tid - (tid / H) * H;
-  float dc = 0.f, dh = 0.f;
-  if (cell) dh = d.dh[(long long)(b0 + cr) * d.lddh + cu];
+  float dc = 0.f, dh = 0.f, gin = 0.f;
+  int am = T - 1;  // the step whose h received the embedding gradient
+  if (cell) {
+    gin = d.dh[(long long)(b0 + cr) * d.lddh + cu];
+    if (d.arg) am = d.arg[(long long)(b0 + cr) * H + cu];
+  }
   for (int t = T - 1; t >= 0; --t) {
     if (cell) {
-      if (t < T - 1) dh = ((part[0][cr][cu] + part[1][cr][cu]) + part[2][cr][cu]) + part[3][cr][cu];
+      if (t < T - 1) {
+        dh = ((part[0][cr][cu] + part[1][cr][cu]) + part[2][cr][cu]) + part[3][cr][cu];
+        if (t == am) dh += gin;  // max-pooled embedding: its gradient joins the recurrent one at the argmax
+      } else {
+        dh = am == T - 1 ? gin : 0.f;
+      }
       const long long go = ((long long)t * B + b0 + cr) * G + cu;
       const float ig = d.gates[go], fg = d.gates[go + H], gg = d.gates[go + 2 * H], og = d.gates[go + 3 * H];
       const long long co = ((long long)t * B + b0 + cr) * H + cu;
@@ -450,7 +470,8 @@ extern "C" int tspm_lstm_fwd(int32_t count, const tspm_lstm_fwd_desc* descs, tsp
     if (!lstm_ok(s.batch, s.steps, s.hidden, s.xg, s.w_hh, s.gates, s.cs) || !s.hs || !s.h_out || s.ld_out < s.hidden)
       return TSPM_ERR_INVALID;
     if (reinterpret_cast<uintptr_t>(s.w_hh) & 15) return TSPM_ERR_INVALID;
-    d[i] = LstmFwdDesc{s.batch, s.steps, s.xg, s.w_hh, s.b_hh, s.gates, s.cs, s.hs, s.h_out, s.ld_out};
+    if (s.steps > 256 && s.argmax) return TSPM_ERR_INVALID;  // uint8 time index
+    d[i] = LstmFwdDesc{s.batch, s.steps, s.xg, s.w_hh, s.b_hh, s.gates, s.cs, s.hs, s.h_out, s.ld_out, s.argmax};
   }
   return launch_lstm_fwd<64, kLstmRB>(d[0], count > 1 ? &d[1] : nullptr, static_cast<hipStream_t>(stream));
 }
@@ -462,7 +483,8 @@ extern "C" int tspm_lstm_bwd(int32_t count, const tspm_lstm_bwd_desc* descs, tsp
     const tspm_lstm_bwd_desc& s = descs[i];
     if (!lstm_ok(s.batch, s.steps, s.hidden, s.w_hh, s.gates, s.cs, s.dh) || !s.dgates || s.ld_dh < s.hidden)
       return TSPM_ERR_INVALID;
-    d[i] = LstmBwdDesc{s.batch, s.steps, s.w_hh, s.gates, s.cs, s.dh, s.ld_dh, s.dgates};
+    if (s.steps > 256 && s.argmax) return TSPM_ERR_INVALID;
+    d[i] = LstmBwdDesc{s.batch, s.steps, s.w_hh, s.gates, s.cs, s.dh, s.ld_dh, s.dgates, s.argmax};
   }
   return launch_lstm_bwd<64, kLstmRB>(d[0], count > 1 ? &d[1] : nullptr, static_cast<hipStream_t>(stream));
 }

@@ -3,7 +3,8 @@
 Drop-ins for the reference's classes, same constructor arguments, attribute names and ``state_dict``
 keys (MML_Suite paths):
 
-* ``LSTMEncoder``     models/msa/networks/lstm.py:8-67   (``rnn`` = nn.LSTM parameter container, "last")
+* ``LSTMEncoder``     models/msa/networks/lstm.py:8-67   (``rnn`` = nn.LSTM parameter container, "last" /
+                      "maxpool")
 * ``TextCNN``         models/msa/networks/textcnn.py:10-69
 * ``FcClassifier``    models/msa/networks/classifier.py:83-117
 * ``UttFusionModel``  models/msa/utt_fusion.py:25-294 (forward, train_step with clip_grad_norm_,
@@ -12,6 +13,9 @@ keys (MML_Suite paths):
 configs/mosi/centralised/utt_fusion_base_training.yaml: LSTM 5→64 (audio) and 20→64 (video), TextCNN
 over 768-d text (3 x 128 filters of heights 3/4/5, dropout 0.5, Linear 384→64 + ReLU), FcClassifier
 192 → 192/64/32 → 3 (ReLU + dropout 0.5 per layer), cross-entropy, clip 1.0, Adam lr 1e-3 / wd 1e-3.
+configs/mosei/centralised/utt_fusion_train_mosei.yaml (the same model on CMU-MOSEI): LSTM 74→64 and 35→64
+with the "maxpool" embedding, TextCNN dropout 0.7, FcClassifier 192 → 96/48 → 3 with ``use_bn`` (Linear →
+ReLU → BatchNorm1d → Dropout 0.66), clip 0.5, Adam lr 2e-4 / wd 1e-5, batch 256.
 
 ``MosiEngine`` is the step's kernel schedule for a fixed (batch, steps): inputs time-major on the device
 ([T][B][F], rows (t, b)); LSTM input projections and weight gradients on the MFMA GEMM
@@ -43,11 +47,35 @@ PATTERNS = {"atv": (1.0, 1.0, 1.0), "at": (1.0, 1.0, 0.0), "av": (1.0, 0.0, 1.0)
             "a": (1.0, 0.0, 0.0), "t": (0.0, 1.0, 0.0), "v": (0.0, 0.0, 1.0)}  # (audio, text, video) data/mosi.py:60-68
 
 
+# The model / optimizer blocks of the two UTT-Fusion YAMLs (configs/mosi/centralised/utt_fusion_base_training.yaml,
+# configs/mosei/centralised/utt_fusion_train_mosei.yaml): what build_utt_fusion constructs, in YAML order.
+YAML_CONFIGS = {
+    "mosi": dict(audio_dim=5, video_dim=20, text_dim=768, embd_method="last", text_dropout=0.5, cls_layers=(192, 64, 32),
+                 cls_dropout=0.5, use_bn=False, clip=1.0, lr=1e-3, weight_decay=1e-3, batch=128),
+    "mosei": dict(audio_dim=74, video_dim=35, text_dim=768, embd_method="maxpool", text_dropout=0.7, cls_layers=(96, 48),
+                  cls_dropout=0.66, use_bn=True, clip=0.5, lr=2e-4, weight_decay=1e-5, batch=256),
+}
+
+
+def build_utt_fusion(name: str = "mosi") -> "UttFusionModel":
+    """UttFusionModel of the named YAML (netA, netV, netT, netC constructed in the YAML's order, so a
+    ``torch.manual_seed`` before the call gives the reference's initial weights)."""
+    c = YAML_CONFIGS[name]
+    netA = LSTMEncoder(input_size=c["audio_dim"], hidden_size=64, embd_method=c["embd_method"])
+    netV = LSTMEncoder(input_size=c["video_dim"], hidden_size=64, embd_method=c["embd_method"])
+    netT = TextCNN(input_size=c["text_dim"], embd_size=64, dropout=c["text_dropout"], in_channels=1, out_channels=128,
+                   kernel_heights=[3, 4, 5])
+    netC = FcClassifier(input_dim=192, layers=list(c["cls_layers"]), output_dim=3, dropout=c["cls_dropout"],
+                        use_bn=c["use_bn"])
+    return UttFusionModel(netA, netV, netT, netC, clip=c["clip"])
+
+
 # ------------------------------------------------------------------------------------------------
 # parameter containers (reference attribute names / state_dict keys / construction order)
 # ------------------------------------------------------------------------------------------------
 class LSTMEncoder(nn.Module):
-    """lstm.py:8-67: one-directional nn.LSTM(batch_first=True); embd "last" = h_n."""
+    """lstm.py:8-67: one-directional nn.LSTM(batch_first=True); embd "last" = h_n, "maxpool" = max over
+    time of r_out (lstm.py:47-52, F.max_pool1d: first maximum)."""
 
     def __init__(self, input_size: int, hidden_size: int, embd_method: str = "last"):
         super().__init__()
@@ -55,8 +83,9 @@ class LSTMEncoder(nn.Module):
         self.hidden_size = hidden_size
         self.rnn = nn.LSTM(self.input_size, self.hidden_size, batch_first=True)
         assert embd_method in ["maxpool", "attention", "last"]
-        if embd_method != "last":
-            raise NotImplementedError("LSTMEncoder HIP path: only embd_method='last' (the MOSI UTT-Fusion config)")
+        if embd_method == "attention":
+            raise NotImplementedError("LSTMEncoder HIP path: embd_method 'last' or 'maxpool' (the MOSI / MOSEI "
+                                      "UTT-Fusion configs)")
         self.embd_method = embd_method
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -94,14 +123,14 @@ class FcClassifier(nn.Module):
     def __init__(self, input_dim: int, layers: List[int], output_dim: int, *, dropout: float = 0.3,
                  use_bn: bool = False) -> None:
         super().__init__()
-        if use_bn:
-            raise NotImplementedError("FcClassifier HIP path: use_bn=False (the MOSI UTT-Fusion config)")
         if len(layers) == 0:
             raise NotImplementedError("FcClassifier HIP path: at least one hidden layer")
         self.all_layers = []
         for i in range(0, len(layers)):
             self.all_layers.append(nn.Linear(input_dim, layers[i]))
             self.all_layers.append(nn.ReLU())
+            if use_bn:
+                self.all_layers.append(nn.BatchNorm1d(layers[i]))
             if dropout > 0:
                 self.all_layers.append(nn.Dropout(dropout))
             input_dim = layers[i]
@@ -109,9 +138,13 @@ class FcClassifier(nn.Module):
         self.fc_out = nn.Linear(layers[-1], output_dim)
         self.dropout_p = float(dropout)
         self.widths = [int(w) for w in layers]
+        self.use_bn = bool(use_bn)
 
     def linears(self):
         return [m for m in self.module if isinstance(m, nn.Linear)]
+
+    def bns(self):
+        return [m for m in self.module if isinstance(m, nn.BatchNorm1d)]
 
 
 # ------------------------------------------------------------------------------------------------
@@ -155,6 +188,9 @@ class MosiEngine:
             self.lstm[name] = dict(xg=torch.empty(T * B, 4 * H, **f), gates=torch.empty(T * B, 4 * H, **f),
                                    cs=torch.empty(T * B, H, **f), hs=torch.empty((T + 1) * B, H, **f),
                                    dg=torch.empty(T * B, 4 * H, **f))
+            # "maxpool" embedding: the time index of each unit's maximum (uint8 [B][H])
+            self.lstm[name]["arg"] = (torch.zeros(B, H, dtype=torch.uint8, device=device)
+                                      if enc.embd_method == "maxpool" else None)
         C, nc = t.out_channels, 3 * t.out_channels
         self.C, self.nc = C, nc
         self.conv_shapes = [L.ConvShape(B, T, 1, self.ft, C, k, 1, 1, 0, T - k + 1, 1) for k in t.heights]
@@ -178,6 +214,14 @@ class MosiEngine:
         self.logits = torch.empty(B, c.fc_out.out_features, **f)
         self.dlogits = torch.empty_like(self.logits)
         self.dh = [torch.empty(B, w, **f) for w in self.widths]
+        # FcClassifier(use_bn): per layer the ReLU output r (the BatchNorm input), its batch statistics and the
+        # gradient of r's Linear (the BN backward writes it with the ReLU mask applied)
+        self.use_bn = c.use_bn
+        if self.use_bn:
+            self.r = [torch.empty(B, w, **f) for w in self.widths]
+            self.bn_mean = [torch.empty(w, **f) for w in self.widths]
+            self.bn_inv = [torch.empty(w, **f) for w in self.widths]
+            self.dr = [torch.empty(B, w, **f) for w in self.widths]
         self.dfused = torch.empty(B, self.E, **f)
         self.dfc_in = torch.empty(B, nc, **f)
         self.g_work = torch.empty(B, nc, **f)
@@ -292,6 +336,7 @@ class MosiEngine:
             d.xg, d.w_hh, d.b_hh = bufs["xg"].data_ptr(), rnn.weight_hh_l0.data_ptr(), rnn.bias_hh_l0.data_ptr()
             d.gates, d.cs, d.hs = bufs["gates"].data_ptr(), bufs["cs"].data_ptr(), bufs["hs"].data_ptr()
             d.h_out = self.fused.data_ptr() + col * 4
+            d.argmax = L.ptr(bufs["arg"])
         L.check(lib.tspm_lstm_fwd(2, descs, sh), "lstm_fwd")
 
     def _forward_text(self, sh: int, train: bool) -> None:
@@ -319,11 +364,35 @@ class MosiEngine:
 
     def _forward_classifier(self, sh: int, train: bool) -> None:
         lib, m, B = L.lib(), self.m, self.B
-        # FcClassifier: (Linear, ReLU, Dropout) per layer, fc_out
+        # FcClassifier: (Linear, ReLU, [BatchNorm1d,] Dropout) per layer, fc_out
         c = m.netC
         cp = c.dropout_p
         x, fin = self.fused, self.E
+        if self.use_bn:
+            for j, (lin, bn, hbuf) in enumerate(zip(c.linears(), c.bns(), self.h)):
+                w = lin.out_features
+                L.check(lib.tspm_linear_fwd(B, fin, w, x.data_ptr(), fin, lin.weight.data_ptr(), lin.bias.data_ptr(),
+                                            1, None, 1.0, self.r[j].data_ptr(), w, sh), f"classifier {j}")
+                if train:
+                    keep = self.keeps[1 + j].data_ptr() if cp > 0 else None
+                    L.check(lib.tspm_bn1d_fwd_drop(B, w, self.r[j].data_ptr(), bn.weight.data_ptr(), bn.bias.data_ptr(),
+                                                   bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                                   float(bn.momentum), float(bn.eps), self.bn_mean[j].data_ptr(),
+                                                   self.bn_inv[j].data_ptr(), keep,
+                                                   1.0 / (1.0 - cp) if 0 < cp < 1 else 1.0, hbuf.data_ptr(), sh),
+                            f"classifier bn {j}")
+                else:
+                    L.check(lib.tspm_bn_apply_eval(B, w, self.r[j].data_ptr(), bn.running_mean.data_ptr(),
+                                                   bn.running_var.data_ptr(), float(bn.eps), bn.weight.data_ptr(),
+                                                   bn.bias.data_ptr(), 0, None, None, None, None, None, 0,
+                                                   hbuf.data_ptr(), sh), f"classifier bn {j} (eval)")
+                x, fin = hbuf, w
+            if train:  # num_batches_tracked += 1 of every classifier BatchNorm1d: one launch
+                from .step import shared_batches_tracked
+                L.counters_add(shared_batches_tracked(m, self.device, (nn.BatchNorm1d,)), 1, sh)
         for j, (lin, hbuf) in enumerate(zip(c.linears(), self.h)):
+            if self.use_bn:
+                break
             keep = self.keeps[1 + j].data_ptr() if (train and cp > 0) else None
             L.check(lib.tspm_linear_fwd(B, fin, lin.out_features, x.data_ptr(), fin, lin.weight.data_ptr(),
                                         lin.bias.data_ptr(), 1, keep, 1.0 / (1.0 - cp) if cp < 1 else 0.0,
@@ -350,12 +419,24 @@ class MosiEngine:
         linear_bwd(B, self.widths[-1], fo.out_features, self.h[-1].data_ptr(), self.widths[-1], self.dlogits.data_ptr(),
                    fo.out_features, fo.weight.data_ptr(), g(fo.weight).data_ptr(), g(fo.bias).data_ptr(),
                    self.dh[-1].data_ptr(), self.widths[-1], sh)
+        bns = c.bns()
         for j in range(len(lins) - 1, -1, -1):
             w = self.widths[j]
-            L.check(lib.tspm_act_bwd(B, w, self.dh[j].data_ptr(), w, self.h[j].data_ptr(), w, cscale, sh), "cls relu")
+            if self.use_bn:  # Dropout → BatchNorm1d → ReLU backward in one launch: dy of the Linear in dr[j]
+                keep = self.keeps[1 + j].data_ptr() if c.dropout_p > 0 else None
+                L.check(lib.tspm_bn1d_bwd_drop_relu(B, w, self.dh[j].data_ptr(), keep, cscale, self.r[j].data_ptr(),
+                                                    self.bn_mean[j].data_ptr(), self.bn_inv[j].data_ptr(),
+                                                    bns[j].weight.data_ptr(), g(bns[j].weight).data_ptr(),
+                                                    g(bns[j].bias).data_ptr(), self.dr[j].data_ptr(), sh),
+                        "cls bn bwd")
+                dy = self.dr[j]
+            else:
+                L.check(lib.tspm_act_bwd(B, w, self.dh[j].data_ptr(), w, self.h[j].data_ptr(), w, cscale, sh),
+                        "cls relu")
+                dy = self.dh[j]
             xin, fin = (self.h[j - 1], self.widths[j - 1]) if j > 0 else (self.fused, self.E)
             dx, lddx = (self.dh[j - 1], self.widths[j - 1]) if j > 0 else (self.dfused, self.E)
-            linear_bwd(B, fin, w, xin.data_ptr(), fin, self.dh[j].data_ptr(), w, lins[j].weight.data_ptr(),
+            linear_bwd(B, fin, w, xin.data_ptr(), fin, dy.data_ptr(), w, lins[j].weight.data_ptr(),
                        g(lins[j].weight).data_ptr(), g(lins[j].bias).data_ptr(), dx.data_ptr(), lddx, sh)
         if self.concurrent:
             side, sh_side = self._fork()
@@ -399,6 +480,7 @@ class MosiEngine:
             d.batch, d.steps, d.hidden, d.ld_dh = B, T, enc.hidden_size, self.E
             d.w_hh, d.gates, d.cs = rnn.weight_hh_l0.data_ptr(), bufs["gates"].data_ptr(), bufs["cs"].data_ptr()
             d.dh, d.dgates = self.dfused.data_ptr() + col * 4, bufs["dg"].data_ptr()
+            d.argmax = L.ptr(bufs["arg"])
         L.check(lib.tspm_lstm_bwd(2, descs, sh), "lstm_bwd")
         for name, enc, x, fin in (("a", m.netA, self.A, self.fa), ("v", m.netV, self.V, self.fv)):
             bufs, rnn, H = self.lstm[name], enc.rnn, enc.hidden_size
@@ -737,6 +819,7 @@ def _encode_lstm(enc: LSTMEncoder, x: torch.Tensor) -> torch.Tensor:
     xt = x.transpose(0, 1).contiguous() if T > 1 else x.reshape(1, B, F).contiguous()
     xg, gates = torch.empty(T * B, 4 * H, **f), torch.empty(T * B, 4 * H, **f)
     cs, hs, out = torch.empty(T * B, H, **f), torch.empty((T + 1) * B, H, **f), torch.empty(B, H, **f)
+    arg = torch.empty(B, H, dtype=torch.uint8, device=dev) if enc.embd_method == "maxpool" else None
     lib, sh, rnn = L.lib(), L.stream_handle(), enc.rnn
     L.check(lib.tspm_linear_fwd(T * B, F, 4 * H, xt.data_ptr(), F, rnn.weight_ih_l0.data_ptr(),
                                 rnn.bias_ih_l0.data_ptr(), 0, None, 1.0, xg.data_ptr(), 4 * H, sh), "lstm proj")
@@ -744,5 +827,6 @@ def _encode_lstm(enc: LSTMEncoder, x: torch.Tensor) -> torch.Tensor:
     d[0].batch, d[0].steps, d[0].hidden, d[0].ld_out = B, T, H, H
     d[0].xg, d[0].w_hh, d[0].b_hh = xg.data_ptr(), rnn.weight_hh_l0.data_ptr(), rnn.bias_hh_l0.data_ptr()
     d[0].gates, d[0].cs, d[0].hs, d[0].h_out = gates.data_ptr(), cs.data_ptr(), hs.data_ptr(), out.data_ptr()
+    d[0].argmax = L.ptr(arg)
     L.check(lib.tspm_lstm_fwd(1, d, sh), "lstm_fwd")
     return out

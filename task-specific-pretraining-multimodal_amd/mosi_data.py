@@ -305,3 +305,8 @@ class MOSI(torch.utils.data.Dataset):
     @staticmethod
     def get_num_classes(is_classification: bool = True) -> int:
         return 3 if is_classification else 1
+
+
+class MOSEI(MOSI):
+    """data/mosi.py:270-283 (CMU-MOSEI: the same MultimodalSentimentDataset, 3 classes) — the dataset of
+    configs/mosei/centralised/utt_fusion_train_mosei.yaml (74-d audio, 35-d video, 768-d text)."""

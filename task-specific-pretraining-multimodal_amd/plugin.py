@@ -45,7 +45,7 @@ MODELS = {"avmnist": AVMNIST, "mmimdb": _mm.MMIMDb, "mmimdbmodalityencoder": _mm
 ENCODERS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnetencoder": ResNetEncoder,
             "lstmencoder": _mosi.LSTMEncoder, "textcnn": _mosi.TextCNN}
 OPTIMIZERS = {"adam": FusedAdam}
-DATASETS = {"avmnist": data.AVMNIST, "mosi": _mosi_data.MOSI}
+DATASETS = {"avmnist": data.AVMNIST, "mosi": _mosi_data.MOSI, "mosei": _mosi_data.MOSEI}
 
 
 def _ctor(cls):

@@ -31,15 +31,24 @@ def _decisions(eng):
         d[f"text.relu{i}"] = (eng.pooled[:, i * C:(i + 1) * C] > 0).cpu()
     col = eng.m.netA.hidden_size + eng.m.netV.hidden_size
     d["text.embd"] = (eng.fused[:, col:] > 0).cpu()
-    for j, h in enumerate(eng.h):
+    for j, h in enumerate(eng.r if eng.use_bn else eng.h):  # with use_bn: the ReLU output before the BN
         d[f"cls.relu{j}"] = (h > 0).cpu()
+    for name in ("a", "v"):  # "maxpool" LSTM embeddings: the time index of every unit's maximum
+        if eng.lstm[name]["arg"] is not None:
+            d[f"lstm.{name}.pool"] = eng.lstm[name]["arg"].long().cpu()
     return d
 
 
-def _flips(t64, forced, keeps):
+def _flips(t64, forced, keeps, use_bn=False):
     rep = {}
     for site, f in forced.items():
-        if site.startswith("text.pool"):
+        if site.startswith("lstm."):
+            r_out = t64.pre[site].double()  # [B, T, H]
+            nat = t64.idx[site]
+            flip = f != nat
+            dist = (r_out.gather(1, f.unsqueeze(1)) - r_out.gather(1, nat.unsqueeze(1))).squeeze(1).abs()[flip]
+            x = r_out
+        elif site.startswith("text.pool"):
             conv = t64.pre[site].double().relu()
             nat = t64.idx[site]
             flip = f != nat
@@ -48,7 +57,7 @@ def _flips(t64, forced, keeps):
         else:
             x = t64.pre[site].double()
             flip = f != (x > 0)
-            if site.startswith("cls.relu"):
+            if site.startswith("cls.relu") and not use_bn:  # dropped after the ReLU: the decision is moot
                 flip &= keeps[f"cls{site[-1]}"].bool()
             dist = x.abs()[flip]
         rms = x.pow(2).mean().sqrt().item() or 1.0
@@ -72,7 +81,7 @@ def _check_step(ours, st, o32, o64, A, V, T, y, keeps, out, tally, ref32_logits=
     eng = st.eng
     forced = _decisions(eng)
     r32, r64, t64 = _forced(o32, o64, A, V, T, y, keeps, forced)
-    rep = _flips(t64, forced, keeps)
+    rep = _flips(t64, forced, keeps, eng.use_bn)
     check_out("logits", out["logits"], r32["logits"] if ref32_logits is None else ref32_logits, r64["logits"], tally)
     check_out("loss", out["loss"], (r32["loss"] if ref32_loss is None else ref32_loss).reshape(1),
               r64["loss"].reshape(1), tally)
@@ -82,28 +91,36 @@ def _check_step(ours, st, o32, o64, A, V, T, y, keeps, out, tally, ref32_logits=
     norm64 = torch.sqrt(sum((q.grad.double() ** 2).sum() for q in o64.parameters()))
     norm32 = torch.sqrt(sum((q.grad.double() ** 2).sum() for q in o32.parameters()))
     check_out("total grad norm", eng.total_norm, norm32.reshape(1), norm64.reshape(1), tally)
+    if eng.use_bn:  # the classifier BatchNorm1d running statistics and num_batches_tracked after the step
+        b32, b64 = dict(o32.named_buffers()), dict(o64.named_buffers())
+        for n, b in ours.named_buffers():
+            if n.endswith("num_batches_tracked"):
+                assert int(b) == int(b64[n]), n
+            else:
+                check_out(n, b, b32[n], b64[n], tally)
     return rep
 
 
-def _check_adam(ours, opt, before, step, coef):
-    check_adam(ours, opt, *before, step, lr=LR, wd=WD, coef=coef)
+def _check_adam(ours, opt, before, step, coef, cfg=orc.MOSI):
+    check_adam(ours, opt, *before, step, lr=cfg.lr, wd=cfg.weight_decay, coef=coef)
 
 
-def _run_steps(gpu, batch, steps, clip, n_steps=3, seed=3, lengths=None, golden=None):
-    ours = _dropin(seed, clip=clip).to(gpu)
-    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+def _run_steps(gpu, batch, steps, clip, n_steps=3, seed=3, lengths=None, golden=None, cfg=orc.MOSI):
+    ours = _dropin(seed, clip=clip, cfg=cfg).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay)
     if golden is not None:
         A, V, T, y = (torch.from_numpy(golden[k]) for k in ("audio", "video", "text", "labels"))
     else:
-        A, V, T, y = orc.synthetic_batch(batch, steps, seed=1234 + batch, lengths=lengths)
+        A, V, T, y = orc.synthetic_batch(batch, steps, seed=1234 + batch, lengths=lengths, cfg=cfg)
+    names = ["text"] + [f"cls{j}" for j in range(len(cfg.cls_layers))]
     st = M.FusedMosiStep(ours, opt, None, batch, steps)
     tally, coefs = Tally(), []
     for s in range(n_steps):
         if golden is not None:
-            keeps = {k: torch.from_numpy(golden[f"keep_{k}"][s]) for k in ("text", "cls0", "cls1", "cls2")}
+            keeps = {k: torch.from_numpy(golden[f"keep_{k}"][s]) for k in names}
         else:
-            keeps = orc.keep_masks(batch, 50 + s)
-        o32, o64 = pair_from(ours, lambda: orc.build_oracle_utt(seed))
+            keeps = orc.keep_masks(batch, 50 + s, cfg=cfg)
+        o32, o64 = pair_from(ours, lambda: orc.build_oracle_utt(seed, cfg=cfg))
         before = snapshot(ours, opt if s else None)
         st.keep_override = {k: v.to(gpu) for k, v in keeps.items()}
         out = st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
@@ -120,7 +137,7 @@ def _run_steps(gpu, batch, steps, clip, n_steps=3, seed=3, lengths=None, golden=
             exp = min(1.0, clip / (st.eng.total_norm.item() + 1e-6))
             assert abs(coef - exp) <= 1e-6 * exp
         coefs.append(coef)
-        _check_adam(ours, opt, before, s + 1, coef if clip is not None else 1.0)
+        _check_adam(ours, opt, before, s + 1, coef if clip is not None else 1.0, cfg)
         print(f"[B={batch} T={steps} step {s + 1}] flips {rep} clip coef {coef:.4f}")
     print(tally)
     return ours, st, coefs
@@ -132,6 +149,48 @@ def test_fused_step_vs_golden_reference(gpu):
     import os
     g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "mosi_step_b4.npz"), allow_pickle=False))
     _run_steps(gpu, 4, 20, 1.0, seed=0, golden=g)
+
+
+def test_mosei_fused_step_vs_golden_reference(gpu):
+    """The MOSEI config (utt_fusion_train_mosei.yaml: 74/35-d inputs, "maxpool" LSTM embeddings,
+    FcClassifier with BatchNorm1d + dropout 0.66, clip 0.5) on the B=4 batch the real reference ran."""
+    import os
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "mosei_step_b4.npz"), allow_pickle=False))
+    _run_steps(gpu, 4, 20, 0.5, seed=0, golden=g, cfg=orc.MOSEI)
+
+
+@pytest.mark.parametrize("batch,steps", [(64, 50), (256, 50), (32, 23)])
+def test_mosei_fused_step_vs_oracle(gpu, batch, steps):
+    """MOSEI at its YAML batch (256) and smaller / odd lengths; clip 0.5 (active at these gradient norms)."""
+    lengths = [steps - (i * 7) % (steps // 2) for i in range(batch)]
+    _run_steps(gpu, batch, steps, 0.5, lengths=lengths, cfg=orc.MOSEI)
+
+
+def test_mosei_graph_replay_equals_eager_and_eval(gpu):
+    """Graph replay = eager bitwise (BN running statistics and num_batches_tracked included); then the
+    eval forward (running statistics, no dropout) against the fp64 oracle's validation_step."""
+    res = []
+    for use_graph in (False, True):
+        ours = _dropin(7, cfg=orc.MOSEI).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=orc.MOSEI.lr, weight_decay=orc.MOSEI.weight_decay)
+        st = M.FusedMosiStep(ours, opt, None, 64, 50, use_graph=use_graph)
+        A, V, T, y = orc.synthetic_batch(64, 50, seed=5, cfg=orc.MOSEI)
+        for s in range(4):
+            st.keep_override = {k: v.to(gpu) for k, v in orc.keep_masks(64, 90 + s, cfg=orc.MOSEI).items()}
+            st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
+        torch.cuda.synchronize()
+        res.append(torch.cat([t.detach().reshape(-1).double() for t in ours.state_dict().values()]).cpu())
+    assert torch.equal(res[0], res[1])
+    assert all(int(bn.num_batches_tracked) == 4 for bn in ours.netC.bns())
+    o = orc.build_oracle_utt(7, cfg=orc.MOSEI)
+    o.load_state_dict({k: v.cpu() for k, v in ours.state_dict().items()})
+    batch = {"audio": A, "video": V, "text": T, "label": y, "pattern_name": ["atv"] * 64}
+    v = ours.validation_step(batch, None, gpu, None)
+    r = orc.validation_step(o.double(), A.double(), V.double(), T.double(), y)
+    check_out("mosei eval logits", ours._engine(64, 50, gpu).logits, None, r["logits"])
+    assert abs(v["loss"] - r["loss"].item()) <= 1e-4 * abs(r["loss"].item())
+    emb = ours.netA(A.to(gpu))  # standalone "maxpool" encoder = the model's audio columns
+    assert rel_l2(emb, ours._engine(64, 50, gpu).fused[:, :64]) < 1e-6
 
 
 @pytest.mark.parametrize("batch,steps,clip", [(32, 50, 1.0), (128, 50, 1.0), (64, 37, 0.05)])

@@ -12,6 +12,7 @@ from oracle import mosi_ref as orc
 from tspm_amd import mosi as M
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "mosi_step_b4.npz")
+GOLDEN_MOSEI = os.path.join(os.path.dirname(__file__), "golden", "mosei_step_b4.npz")
 
 
 @pytest.fixture(scope="module")
@@ -19,13 +20,20 @@ def mg():
     return dict(np.load(GOLDEN, allow_pickle=False))
 
 
-def _dropin(seed=0, clip=1.0):
+@pytest.fixture(scope="module")
+def meg():
+    return dict(np.load(GOLDEN_MOSEI, allow_pickle=False))
+
+
+def _dropin(seed=0, clip=None, cfg=orc.MOSI):
     torch.manual_seed(seed)
-    a = M.LSTMEncoder(input_size=5, hidden_size=64, embd_method="last")
-    v = M.LSTMEncoder(input_size=20, hidden_size=64, embd_method="last")
-    t = M.TextCNN(input_size=768, embd_size=64, dropout=0.5, in_channels=1, out_channels=128, kernel_heights=[3, 4, 5])
-    c = M.FcClassifier(input_dim=192, layers=[192, 64, 32], output_dim=3, dropout=0.5)
-    return M.UttFusionModel(a, v, t, c, clip=clip)
+    a = M.LSTMEncoder(input_size=cfg.audio_dim, hidden_size=64, embd_method=cfg.embd_method)
+    v = M.LSTMEncoder(input_size=cfg.video_dim, hidden_size=64, embd_method=cfg.embd_method)
+    t = M.TextCNN(input_size=768, embd_size=64, dropout=cfg.text_dropout, in_channels=1, out_channels=128,
+                  kernel_heights=[3, 4, 5])
+    c = M.FcClassifier(input_dim=192, layers=list(cfg.cls_layers), output_dim=3, dropout=cfg.cls_dropout,
+                       use_bn=cfg.use_bn)
+    return M.UttFusionModel(a, v, t, c, clip=cfg.clip if clip is None else clip)
 
 
 def test_oracle_reproduces_reference_train_steps_bitwise(mg):
@@ -41,13 +49,27 @@ def test_oracle_reproduces_reference_train_steps_bitwise(mg):
         torch.set_num_threads(nt)
 
 
-def _replay(mg):
-    model = orc.build_oracle_utt(0)
+def test_oracle_reproduces_reference_mosei_train_steps_bitwise(meg):
+    """The MOSEI config (configs/mosei/centralised/utt_fusion_train_mosei.yaml: "maxpool" LSTM embeddings,
+    FcClassifier with BatchNorm1d, clip 0.5): 3 oracle train steps equal the real reference bit for bit,
+    incl. the BatchNorm1d running statistics and num_batches_tracked after every step."""
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    try:
+        _replay(meg, orc.MOSEI)
+    finally:
+        torch.set_num_threads(nt)
+
+
+def _replay(mg, cfg=orc.MOSI):
+    model = orc.build_oracle_utt(0, cfg=cfg)
     assert list(model.state_dict()) == list(mg["state_dict_keys"])
-    opt = orc.OracleAdam(list(model.parameters()), lr=1e-3, weight_decay=1e-3)
+    opt = orc.OracleAdam(list(model.parameters()), lr=cfg.lr, weight_decay=cfg.weight_decay)
     A, V, T, y = (torch.from_numpy(mg[k]) for k in ("audio", "video", "text", "labels"))
+    names = ["text"] + [f"cls{j}" for j in range(len(cfg.cls_layers))]
+    bns = [m for m in model.netC.module if isinstance(m, torch.nn.BatchNorm1d)]
     for s in range(3):
-        keeps = {k: torch.from_numpy(mg[f"keep_{k}"][s]) for k in ("text", "cls0", "cls1", "cls2")}
+        keeps = {k: torch.from_numpy(mg[f"keep_{k}"][s]) for k in names}
         r = orc.train_step(model, opt, A, V, T, y, keeps)
         assert torch.equal(r["logits"], torch.from_numpy(mg["logits"][s])), s
         assert r["loss"].item() == mg["losses"][s], s
@@ -57,19 +79,24 @@ def _replay(mg):
             np.testing.assert_array_equal(gn, mg["grad_norm_step1"])
         ps = np.array([p.detach().double().sum().item() for p in model.parameters()])
         np.testing.assert_array_equal(ps, mg["param_sums"][s])
+        if bns:
+            st = [float(t.double().sum()) for bn in bns for t in (bn.running_mean, bn.running_var)]
+            st += [int(bn.num_batches_tracked) for bn in bns]
+            np.testing.assert_array_equal(np.array(st), mg["bn_stat_sums"][s])
     model.eval()
     with torch.no_grad():
         ev = orc.forward(model, A, V, T, False)
     assert torch.equal(ev, torch.from_numpy(mg["eval_logits"]))
 
 
-def test_dropin_state_dict_and_seeded_init_equal_reference(mg):
-    ours, ref = _dropin(0), orc.build_oracle_utt(0)
-    sd, rsd = ours.state_dict(), ref.state_dict()
-    assert list(sd) == list(rsd) == list(mg["state_dict_keys"])
-    for k in sd:
-        assert torch.equal(sd[k], rsd[k]), k
-    assert [n for n, _ in ours.named_parameters()] == list(mg["param_names"])
+def test_dropin_state_dict_and_seeded_init_equal_reference(mg, meg):
+    for cfg, g in ((orc.MOSI, mg), (orc.MOSEI, meg)):
+        ours, ref = _dropin(0, cfg=cfg), orc.build_oracle_utt(0, cfg=cfg)
+        sd, rsd = ours.state_dict(), ref.state_dict()
+        assert list(sd) == list(rsd) == list(g["state_dict_keys"])
+        for k in sd:
+            assert torch.equal(sd[k], rsd[k]), k
+        assert [n for n, _ in ours.named_parameters()] == list(g["param_names"])
 
 
 def test_dropin_api_surface():
@@ -78,8 +105,8 @@ def test_dropin_api_surface():
     assert m.netA.hidden_size == 64 and m.netT.hidden_size == 64 and m.clip == 1.0
     with pytest.raises(NotImplementedError):
         M.LSTMEncoder(5, 64, embd_method="attention")
-    with pytest.raises(NotImplementedError):
-        M.FcClassifier(192, [64], 3, use_bn=True)
+    assert M.LSTMEncoder(74, 64, embd_method="maxpool").embd_method == "maxpool"
+    assert len(M.FcClassifier(192, [96, 48], 3, use_bn=True).bns()) == 2
     m.flatten_parameters()
     with pytest.raises(tspm_amd._lib.TspmError):  # no CPU fallback
         m.eval()
@@ -144,3 +171,17 @@ def test_mosi_dataset_loads_npz_and_refuses_pickles_by_default(tmp_path):
     pk.write_bytes(b"not read")
     with pytest.raises(ValueError):
         D.MOSI(str(pk), "train", device="cpu")
+
+
+def test_build_utt_fusion_matches_both_yamls(mg, meg):
+    """mosi.build_utt_fusion("mosi" / "mosei"): the YAML's modules in the YAML's order — state_dict keys and
+    seeded weights equal to the real reference's (the golden files' state_dict sha256)."""
+    import hashlib
+    for name, g in (("mosi", mg), ("mosei", meg)):
+        torch.manual_seed(0)
+        sd = M.build_utt_fusion(name).state_dict()
+        h = hashlib.sha256()
+        for k in sorted(sd):
+            h.update(k.encode())
+            h.update(sd[k].contiguous().numpy().tobytes())
+        assert list(sd) == list(g["state_dict_keys"]) and h.hexdigest() == str(g["state_dict_sha256"]), name
