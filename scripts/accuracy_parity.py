@@ -16,14 +16,16 @@ reference); batch 128 (last batch 64), Adam lr 5e-4 / wd 1e-4, dropout 0.5, E ep
 in how each implementation rounds in fp32, so the per-run difference of final test accuracies is the
 effect of the implementation; its mean over runs, with a t confidence interval, is the result.
 
-  reference — oracle/avmnist_ref.py on the CPU of the build container, i.e. the reference's
-              AVMNIST.train_step (bit-exact to it on CPU, tests/test_oracle_golden.py)
+  reference — oracle/avmnist_ref.py, i.e. the reference's AVMNIST.train_step (bit-exact to it on CPU,
+              tests/test_oracle_golden.py): on the CPU, or with --device cuda the same torch code through
+              ATen/MIOpen on the MI355X (what the reference itself runs on a GPU)
   ours      — tspm_amd.FusedTrainStep / FusedEvalStep on the MI355X
 
   python scripts/accuracy_parity.py prepare                               # here: files -> data_cache/
   python scripts/accuracy_parity.py reference --epochs 20 --seeds 0,1,... # here, CPU
+  python scripts/accuracy_parity.py reference --device cuda --epochs 20 --seeds 0,1,...  # GPU box (ATen)
   python scripts/accuracy_parity.py ours --epochs 20 --seeds 0,1,...      # GPU box
-  python scripts/accuracy_parity.py compare --out profiles/r2_accuracy_parity.json
+  python scripts/accuracy_parity.py compare [--device cuda] --out profiles/r2_accuracy_parity.json
 """
 from __future__ import annotations
 
