@@ -95,14 +95,25 @@ __global__ __launch_bounds__(256) void k_bn_stats_partial(long long M, int C, co
 // per-channel merge of G partial tiles: 4 channels x 64 tile groups per workgroup, double, fixed
 // order, 8 tile loads in flight per thread (bn_merge_block)
 constexpr int kFinChan = 4;
+template <int CH>
 __global__ __launch_bounds__(256) void k_bn_finalize(long long M, int C, int G, long long rows_per_tile,
                                                      const float* __restrict__ part, float* __restrict__ rmean,
                                                      float* __restrict__ rvar, float momentum, float eps,
                                                      float* __restrict__ smean, float* __restrict__ sinv) {
   __shared__ double red[256];
-  __shared__ double smu[kFinChan];
-  bn_merge_block(M, C, G, rows_per_tile, part, blockIdx.x * kFinChan, kFinChan, rmean, rvar, momentum, eps, smean,
+  __shared__ double smu[CH];
+  bn_merge_block(M, C, G, rows_per_tile, part, blockIdx.x * CH, CH, rmean, rvar, momentum, eps, smean,
                  sinv, red, smu);
+}
+
+// "Wide" BN launches for the few-channel layers (TSPM_BN_WIDE, default on; 0 = the previous shapes, read
+// per call): the statistics merge with fewer channels per workgroup (64 workgroups at C = 64 instead of
+// 16, each merging its tiles with all 256 threads) and the backward partial sums with more rows' loads
+// in flight per thread (the C = 64 layers' partial pass has only 64 workgroups: 1/4 of the CUs, so each
+// must keep more bytes in flight).  Both change only the (fixed) order of the double-precision sums.
+bool bn_wide() {
+  const char* e = getenv("TSPM_BN_WIDE");
+  return !(e && e[0] == '0');
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -230,7 +241,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_t(long long M, int C, const fl
 // tiles (rows in batches of 4 per thread so their loads are in flight together).  An in-launch
 // merge by the last workgroup was measured slower than the parallel pass 2 below (the merge of
 // >= 64 tiles per channel block serialises on one CU), so pass 2 stays a launch.
-template <bool HAS_OUT, bool TWO>
+template <bool HAS_OUT, bool TWO, int U>
 __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
                                                         const float* __restrict__ out, const float* __restrict__ y,
                                                         const float* __restrict__ mean, const float* __restrict__ y2,
@@ -247,7 +258,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
   if (cok) {
     const f32x4 mu = ld4(mean + 4 * c4);
     const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    constexpr int U = 4;  // rows per batch: all their loads in flight together
+    // U rows per batch: all their loads in flight together
     for (long long rb = r_begin + rg; rb < r_end; rb += U * kRowGroups) {
       f32x4 gv[U], yv[U], y2v[U];
 #pragma unroll
@@ -835,9 +846,15 @@ extern "C" int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t ro
   if (m <= 0 || c <= 0 || ntiles <= 0 || rows_per_tile <= 0 || !partial || !save_mean || !save_invstd)
     return TSPM_ERR_INVALID;
   if ((long long)ntiles * rows_per_tile < m || (long long)(ntiles - 1) * rows_per_tile >= m) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, kFinChan)), dim3(256), 0, static_cast<hipStream_t>(stream), (long long)m, c,
-                     ntiles, (long long)rows_per_tile, partial, running_mean, running_var, momentum, eps, save_mean,
-                     save_invstd);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const int ch = bn_wide() ? (c <= 64 ? 1 : c <= 128 ? 2 : kFinChan) : kFinChan;
+#define BN_FIN(CH)                                                                                               \
+  hipLaunchKernelGGL((k_bn_finalize<CH>), dim3(cdiv(c, CH)), dim3(256), 0, st, (long long)m, c, ntiles,          \
+                     (long long)rows_per_tile, partial, running_mean, running_var, momentum, eps, save_mean, save_invstd)
+  if (ch == 1) BN_FIN(1);
+  else if (ch == 2) BN_FIN(2);
+  else BN_FIN(kFinChan);
+#undef BN_FIN
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }
@@ -984,11 +1001,16 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   const int Greal = (int)cdiv64(m, rpb);
   float* coef = part + (size_t)3 * G * c;
   const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
-#define BNB_P(HO, TW)                                                                                     \
-  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
+  // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide)
+  const int pu = !bn_wide() ? 4 : rpb >= 64LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
+#define BNB_P(HO, TW, U)                                                                                     \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
                      y2, mean2, rpb, part)
-  if (ho) { if (two) BNB_P(true, true); else BNB_P(true, false); }
-  else { if (two) BNB_P(false, true); else BNB_P(false, false); }
+#define BNB_PU(HO, TW) \
+  if (pu == 16) BNB_P(HO, TW, 16); else if (pu == 8) BNB_P(HO, TW, 8); else BNB_P(HO, TW, 4);
+  if (ho) { if (two) { BNB_PU(true, true) } else { BNB_PU(true, false) } }
+  else { if (two) { BNB_PU(false, true) } else { BNB_PU(false, false) } }
+#undef BNB_PU
 #undef BNB_P
   TSPM_LAUNCH_CHECK();
   if (!dy_t) {

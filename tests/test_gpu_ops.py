@@ -239,7 +239,8 @@ def _bn_ref_block(y, y2, gamma, beta, gamma2, beta2, res, mode, relu):
     return out, [y, ga, be] + extra
 
 
-@pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (384, 512), (24576, 64), (1536, 256), (100, 8)])
+@pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (384, 512), (24576, 64), (1536, 256), (100, 8),
+                                 (96256, 64)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("fused", [True, False])
 def test_bn_block_fwd_bwd(gpu, m, c, mode, fused, monkeypatch):
