@@ -556,6 +556,54 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(long long count, int nslab
   }
 }
 
+// Many slabs of a small output (the 7x7 stem weight gradient: 64 x 49 floats split over 64 slabs): the
+// loop above would give each of a handful of workgroups a serial chain of nslab loads per element.  Here
+// Q slab groups x (256 / Q) elements per workgroup: group q sums slabs q, q+Q, q+2Q, ... in order (four
+// loads in flight), then the Q partial sums are added in group order — a fixed order, so deterministic.
+template <int Q>
+__global__ __launch_bounds__(256) void k_reduce_slabs_wide(long long count, int nslab, long long slab_stride,
+                                                           const float* __restrict__ slabs, float* __restrict__ out,
+                                                           int beta) {
+  constexpr int E = 256 / Q;
+  __shared__ float part[Q][E];
+  const int e = threadIdx.x % E, q = threadIdx.x / E;
+  const long long i = blockIdx.x * (long long)E + e;
+  float s = 0.f;
+  if (i < count) {
+    int z = q;
+    for (; z + 3 * Q < nslab; z += 4 * Q) {
+      const float a = slabs[z * slab_stride + i], b = slabs[(z + Q) * slab_stride + i];
+      const float c = slabs[(z + 2 * Q) * slab_stride + i], d = slabs[(z + 3 * Q) * slab_stride + i];
+      s += a;
+      s += b;
+      s += c;
+      s += d;
+    }
+    for (; z < nslab; z += Q) s += slabs[z * slab_stride + i];
+  }
+  part[q][e] = s;
+  __syncthreads();
+  if (q == 0 && i < count) {
+    float t = beta ? out[i] : 0.f;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) t += part[k][e];
+    out[i] = t;
+  }
+}
+
+void launch_reduce_slabs(long long count, int nslab, long long slab_stride, const float* slabs, float* out, int beta,
+                         hipStream_t st) {
+  constexpr int kQ = 8;
+  const char* e = getenv("TSPM_SLAB_WIDE");  // A/B switch (read per call): 0 = the element-parallel loop only
+  if (!(e && e[0] == '0') && nslab >= 2 * kQ && count <= (1LL << 18)) {
+    hipLaunchKernelGGL((k_reduce_slabs_wide<kQ>), dim3((unsigned)cdiv64(count, 256 / kQ)), dim3(256), 0, st, count,
+                       nslab, slab_stride, slabs, out, beta);
+    return;
+  }
+  const int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, count, nslab, slab_stride, slabs, out, beta);
+}
+
 // ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
@@ -845,10 +893,7 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   else TSPM_DISPATCH(k_conv_wgrad, false, g, x, dy, out, dw);
   TSPM_LAUNCH_CHECK();
   if (al.splits > 1 && !g.cnt) {  // separate slab reduction
-    long long count = g.slab;
-    int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, count, al.splits, g.slab,
-                       static_cast<const float*>(out), dw, 0);
+    launch_reduce_slabs(g.slab, al.splits, g.slab, static_cast<const float*>(out), dw, 0, st);
     TSPM_LAUNCH_CHECK();
   }
   return TSPM_OK;
@@ -940,10 +985,7 @@ extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo*
   TSPM_DISPATCH(k_conv_wgrad_t, false, g, x_t, (long long)ldx, dy_t, (long long)ldy, out, dw);
   TSPM_LAUNCH_CHECK();
   if (al.splits > 1 && !g.cnt) {
-    long long count = g.slab;
-    int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, st, count, al.splits, g.slab,
-                       static_cast<const float*>(out), dw, 0);
+    launch_reduce_slabs(g.slab, al.splits, g.slab, static_cast<const float*>(out), dw, 0, st);
     TSPM_LAUNCH_CHECK();
   }
   return TSPM_OK;
@@ -955,9 +997,7 @@ extern "C" int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stri
   if (count == 0) return TSPM_OK;
   if ((reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(out)) & 15) return TSPM_ERR_INVALID;
   if (nslab > 1 && (slab_stride & 3)) return TSPM_ERR_INVALID;
-  int blocks = (int)std::min<long long>(cdiv64(count / 4 + 1, 256), 2048);
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     (long long)count, nslab, (long long)slab_stride, slabs, out, 0);
+  launch_reduce_slabs(count, nslab, slab_stride, slabs, out, 0, static_cast<hipStream_t>(stream));
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }
