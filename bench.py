@@ -1009,6 +1009,26 @@ def main() -> None:
                 r34["what"] = ("ResNet34 (image encoder) 3x3 convs: fwd + dgrad + wgrad launches, valid-tap FLOPs / "
                                "their device time (north_star target >= 0.70)")
             rl["r34_3x3"] = r34
+            # the HBM-bound families: algorithmic bytes per step, PMC HBM bytes per step and the
+            # achieved rate over their device time (same replays as above)
+            bn_elems = 217728 * B  # BN(+ReLU/+add) elements per step (both encoders)
+            n_par = sum(p.numel() for p in model.parameters())
+            algo = {"bn": (8 + 12) * bn_elems, "pool": int(0.30e6 * B), "adam": 28 * n_par}
+            hbm = {}
+            for fam, abytes in algo.items():
+                ms = roof["families"].get(fam)
+                pb, _, psrc = pmc_traffic(fam)
+                if not ms:
+                    continue
+                hbm[fam] = {"algorithmic_bytes": abytes, "pmc_bytes": pb,
+                            "device_ms": round(ms, 4),
+                            "algorithmic_GBps": round(abytes / (ms * 1e-3) / 1e9, 1),
+                            "pmc_GBps": round(pb / (ms * 1e-3) / 1e9, 1) if pb else None,
+                            "frac_of_8TBps": round(abytes / (ms * 1e-3) / 8e12, 4)}
+            if hbm:
+                hbm["what"] = ("BN: 8 B/elem fwd + 12 B/elem bwd x 217,728 elems/sample; pool: 0.30 MB/sample; Adam: "
+                               "28 B/param; pmc_bytes from the same PMC summary as traffic_source")
+                rl["hbm_families"] = hbm
             rl["profiled_steps"] = roof["profiled_steps"]
             rl["incomplete_steps_dropped"] = roof["incomplete_steps_dropped"]
             if roof.get("attribution_failed"):
