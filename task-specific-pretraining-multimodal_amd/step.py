@@ -213,11 +213,17 @@ class FusedTrainStep:
         # stream may only join the origin (main) stream
         self.eng_i.fork_ds = False
         self.eng_i.join_aux = False
+        # TSPM_ENC_ORDER=ai: capture the audio encoder's launches before the image encoder's (A/B of the
+        # graph's node order for the two independent branches; default "ia")
+        audio_first = os.environ.get("TSPM_ENC_ORDER", "ia") == "ai"
         if phase in (0, 1):
             side.wait_stream(main)
+            if audio_first:
+                self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
             with torch.cuda.stream(side):
                 self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-            self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
+            if not audio_first:
+                self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
             main.wait_stream(side)
             sh = main.cuda_stream
             self._head_fwd(sh)
@@ -227,9 +233,12 @@ class FusedTrainStep:
             self._classify(sh)
             self._head_bwd(sh)
         side.wait_stream(main)
+        if audio_first:
+            self.eng_a.backward(self.dfused, self.F, phase=phase)
         with torch.cuda.stream(side):
             self.eng_i.backward(self.dfused[:, ea:], self.F, phase=phase)
-        self.eng_a.backward(self.dfused, self.F, phase=phase)
+        if not audio_first:
+            self.eng_a.backward(self.dfused, self.F, phase=phase)
         main.wait_stream(side)
         if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
             main.wait_stream(self.aux_a)
