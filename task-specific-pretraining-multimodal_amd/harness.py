@@ -186,10 +186,13 @@ def _epoch_block(loss: float, timing: float, n_batches: int, metrics: Dict[str, 
 def fit(model, optimizer, loss_functions, loaders: Dict[str, Any], epochs: int, *, metric_config=None,
         early_stopping: bool = True, patience: int = 10, min_delta: float = 1e-3, scheduler=None,
         checkpoint_dir=None, metrics_path=None, save_metric: str = "loss", mode: str = "minimize",
-        on_epoch=None) -> Dict[str, Any]:
+        on_epoch=None, fail_on_nonfinite: bool = True) -> Dict[str, Any]:
     """_train_loop + test (train_multimodal.py:554-917) for the AVMNIST late-fusion model.  ``loaders``:
     "train", "validation" and optionally "test" → iterables of device batches (a DeviceLoader is
-    re-iterated each epoch; call ``set_epoch`` in ``on_epoch`` for DistributedSampler order)."""
+    re-iterated each epoch; call ``set_epoch`` in ``on_epoch`` for DistributedSampler order).
+    ``fail_on_nonfinite``: raise FloatingPointError as soon as an epoch's mean training loss is NaN / inf
+    (checked at the epoch's one host synchronisation; SURVEY §5 — the reference only turns three numpy
+    RuntimeWarnings into errors, train_multimodal.py:46-60, and would keep training on NaN weights)."""
     runner = EpochRunner(model, optimizer, loss_functions, metric_config)
     ckpt = CheckpointManager(checkpoint_dir, save_metric, mode) if checkpoint_dir is not None else None
     history: Dict[str, Any] = {"train": [], "validation": [], "epoch_metrics": []}
@@ -201,6 +204,8 @@ def fit(model, optimizer, loss_functions, loaders: Dict[str, Any], epochs: int, 
         if on_epoch is not None:
             on_epoch(epoch)
         tr_loss, tr_time, tr_metrics, tr_n = runner.train_epoch(loaders["train"])
+        if fail_on_nonfinite and not np.isfinite(tr_loss):
+            raise FloatingPointError(f"non-finite mean training loss {tr_loss} at epoch {epoch}")
         tr_metrics = dict(tr_metrics, loss=tr_loss)
         va_loss, va_time, va_metrics, va_n = runner.validate_epoch(loaders["validation"])
         va_metrics = dict(va_metrics, loss=va_loss)

@@ -390,14 +390,13 @@ class MosiEngine:
             if train:  # num_batches_tracked += 1 of every classifier BatchNorm1d: one launch
                 from .step import shared_batches_tracked
                 L.counters_add(shared_batches_tracked(m, self.device, (nn.BatchNorm1d,)), 1, sh)
-        for j, (lin, hbuf) in enumerate(zip(c.linears(), self.h)):
-            if self.use_bn:
-                break
-            keep = self.keeps[1 + j].data_ptr() if (train and cp > 0) else None
-            L.check(lib.tspm_linear_fwd(B, fin, lin.out_features, x.data_ptr(), fin, lin.weight.data_ptr(),
-                                        lin.bias.data_ptr(), 1, keep, 1.0 / (1.0 - cp) if cp < 1 else 0.0,
-                                        hbuf.data_ptr(), lin.out_features, sh), f"classifier {j}")
-            x, fin = hbuf, lin.out_features
+        else:  # Linear + ReLU + Dropout in one launch per layer
+            for j, (lin, hbuf) in enumerate(zip(c.linears(), self.h)):
+                keep = self.keeps[1 + j].data_ptr() if (train and cp > 0) else None
+                L.check(lib.tspm_linear_fwd(B, fin, lin.out_features, x.data_ptr(), fin, lin.weight.data_ptr(),
+                                            lin.bias.data_ptr(), 1, keep, 1.0 / (1.0 - cp) if cp < 1 else 0.0,
+                                            hbuf.data_ptr(), lin.out_features, sh), f"classifier {j}")
+                x, fin = hbuf, lin.out_features
         fo = c.fc_out
         L.check(lib.tspm_linear_fwd(B, fin, fo.out_features, x.data_ptr(), fin, fo.weight.data_ptr(),
                                     fo.bias.data_ptr(), 0, None, 1.0, self.logits.data_ptr(), fo.out_features, sh),

@@ -176,3 +176,20 @@ def test_fit_writes_reference_files(gpu, tmp_path):
     assert os.path.exists(tmp_path / "models" / "epoch_1.pth")
     fresh, _ = _models(gpu)
     fresh.load_state_dict(ck["model_state_dict"])
+
+
+def test_fit_fails_fast_on_nonfinite_loss(gpu):
+    """A NaN in one training sample makes that batch's loss NaN: fit stops at the end of the epoch
+    with FloatingPointError instead of training on (checkpointing) NaN weights."""
+    import tspm_amd
+    from tspm_amd.data import AVMNIST, synthetic_corpus
+    from tspm_amd.harness import fit
+    c = synthetic_corpus(64, 5)
+    c.audio[3, 0, 0] = float("nan")
+    tr = AVMNIST(None, "train", "multimodal", selected_patterns=["ai"], corpus=c, device=gpu)
+    _, va = _loaders(gpu)
+    model, _ = _models(gpu)
+    opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
+    loaders = {"train": tr.device_loader(32, shuffle=False), "validation": va.device_loader(32)}
+    with pytest.raises(FloatingPointError):
+        fit(model, opt, None, loaders, epochs=2)
