@@ -179,7 +179,158 @@ def ours(epochs: int, seed: int) -> None:
         json.dump({"side": "ours (HIP path, MI355X)", "seed": seed, "curve": curve}, f, indent=1)
 
 
-def compare(out_path: str, ref_side: str = "reference") -> None:
+# ------------------------------------------------------------------------------------------------
+# pretrained-encoder variant (configs/avmnist/mono/train_{audio,image}_encoder_resnet.yaml, then
+# configs/avmnist/centralised/train_avmnist_resnet_pretrained.yaml): each encoder pre-trained alone
+# (MonomodalEncoder: encoder + Linear(hidden, 10), Adam 5e-4 / 1e-4, batch 128, seed s + 100), then the
+# fusion model (seed s) with the pre-trained encoder weights and two parameter groups — encoders
+# lr 1e-4 / wd 2e-4, the rest 5e-4 / 1e-4.  Fixed epoch counts on both sides (no early stopping).
+# ------------------------------------------------------------------------------------------------
+ENC_LR, ENC_WD = 1e-4, 2e-4
+
+
+def _mono_order(n, modality, epoch, seed):
+    return _order(n, 500 + epoch + (0 if modality == "audio" else 50), seed)
+
+
+def pretrained_reference(mono_epochs: int, epochs: int, seed: int, device: str = "cuda") -> None:
+    from oracle import avmnist_eval_ref as eref
+    from oracle import avmnist_ref as orc
+    from oracle import monomodal_ref as mref
+    tr, te = _load()
+    dev = torch.device(device)
+    lut = torch.from_numpy(_lut().astype(np.int64))
+
+    def tensors(c, rows):
+        a = torch.from_numpy(np.asarray(c.audio[rows]))
+        i = (lut[torch.from_numpy(np.asarray(c.image[rows])).long()].float() * (1.0 / 255.0)).unsqueeze(1)
+        return a.to(dev), i.to(dev), torch.from_numpy(np.asarray(c.labels[rows])).to(dev)
+    sds, mono_curve = {}, []
+    for modality in ("audio", "image"):
+        mm = mref.build_oracle_monomodal(modality, seed + 100).to(dev)
+        opt = orc.OracleAdam(list(mm.parameters()), lr=5e-4, weight_decay=1e-4)
+        for ep in range(mono_epochs):
+            order = _mono_order(len(tr), modality, ep, seed).numpy()
+            for b in range(0, len(order), BATCH):
+                a, i, lab = tensors(tr, order[b:b + BATCH])
+                mref.train_step(mm, opt, a if modality == "audio" else i, lab)
+        correct = 0
+        for b in range(0, len(te), BATCH):
+            a, i, lab = tensors(te, np.arange(b, min(len(te), b + BATCH)))
+            correct += int((mref.validation_step(mm, a if modality == "audio" else i, lab)["preds"] == lab).sum())
+        mono_curve.append({"modality": modality, "test_accuracy": correct / len(te)})
+        print(json.dumps(mono_curve[-1]), flush=True)
+        sds[modality] = {k: v.detach().clone() for k, v in mm.encoder.state_dict().items()}
+    model = orc.build_oracle_avmnist(seed).to(dev)
+    model.audio_encoder.load_state_dict(sds["audio"])
+    model.image_encoder.load_state_dict(sds["image"])
+    enc = list(model.audio_encoder.parameters()) + list(model.image_encoder.parameters())
+    encid = {id(p) for p in enc}
+    opts = [orc.OracleAdam(enc, lr=ENC_LR, weight_decay=ENC_WD),
+            orc.OracleAdam([p for p in model.parameters() if id(p) not in encid], lr=5e-4, weight_decay=1e-4)]
+
+    class _Both:
+        def step(self):
+            for o in opts:
+                o.step()
+    curve = []
+    for ep in range(epochs):
+        t0 = time.time()
+        order = _order(len(tr), ep, seed).numpy()
+        losses = []
+        model.train()
+        for b in range(0, len(order), BATCH):
+            a, i, lab = tensors(tr, order[b:b + BATCH])
+            keep = _keep(seed, ep, b // BATCH, lab.numel()).to(dev)
+            losses.append(orc.train_step(model, _Both(), a, i, lab, keep)["loss"].detach())
+        model.eval()
+        correct = 0
+        for b in range(0, len(te), BATCH):
+            a, i, lab = tensors(te, np.arange(b, min(len(te), b + BATCH)))
+            correct += int((eref.validation_step(model, a, i, lab)["preds"] == lab).sum())
+        curve.append({"epoch": ep + 1, "train_loss": float(np.mean([x.item() for x in losses])),
+                      "test_accuracy": correct / len(te), "seconds": round(time.time() - t0, 1)})
+        print(json.dumps(curve[-1]), flush=True)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f"accuracy_pt_reference_gpu_s{seed}.json"), "w") as f:
+        json.dump({"side": "reference (oracle = the reference's torch code, ATen/MIOpen on the MI355X), pretrained "
+                           "encoders", "seed": seed, "device": device, "mono": mono_curve, "curve": curve}, f, indent=1)
+
+
+def pretrained_ours(mono_epochs: int, epochs: int, seed: int) -> None:
+    import tspm_amd
+    from tspm_amd.data import DeviceCorpus
+    from tspm_amd.monomodal import FusedMonoEvalStep, FusedMonoStep, MonomodalEncoder
+    from tspm_amd.step import FusedEvalStep
+    dev = torch.device("cuda", 0)
+    tr, te = _load()
+    dtr, dte = DeviceCorpus(tr, dev), DeviceCorpus(te, dev)
+    sds, mono_curve = {}, []
+    for modality in ("audio", "image"):
+        torch.manual_seed(seed + 100)  # the reference side's build_oracle_monomodal(modality, seed + 100)
+        enc, dim = ((tspm_amd.ResNet18(1, 64), 64) if modality == "audio" else (tspm_amd.ResNet34(1, 128), 128))
+        mm = MonomodalEncoder(enc, dim, 10).to(dev)
+        opt = tspm_amd.FusedAdam(mm.parameters(), lr=5e-4, weight_decay=1e-4)
+        steps, evals = {}, {}
+        for ep in range(mono_epochs):
+            order = _mono_order(len(tr), modality, ep, seed).to(dev)
+            for b in range(0, len(tr), BATCH):
+                idx = order[b:b + BATCH].contiguous()
+                a, i, lab = dtr.gather(idx, want_audio=modality == "audio", want_image=modality == "image")
+                x = a if modality == "audio" else i
+                st = steps.get(x.shape[0]) or steps.setdefault(x.shape[0], FusedMonoStep(mm, opt, None, x.shape))
+                st.step(x, lab)
+        correct = torch.zeros((), dtype=torch.int64, device=dev)
+        for b in range(0, len(te), BATCH):
+            idx = torch.arange(b, min(len(te), b + BATCH), device=dev)
+            a, i, lab = dte.gather(idx, want_audio=modality == "audio", want_image=modality == "image")
+            x = a if modality == "audio" else i
+            ev = evals.get(x.shape[0]) or evals.setdefault(x.shape[0], FusedMonoEvalStep(mm, None, x.shape))
+            correct += (ev.step(x, lab)["preds"] == lab).sum()
+        mono_curve.append({"modality": modality, "test_accuracy": int(correct) / len(te)})
+        print(json.dumps(mono_curve[-1]), flush=True)
+        sds[modality] = {k: v.detach().clone() for k, v in mm.encoder.state_dict().items()}
+    torch.manual_seed(seed)
+    model = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
+    model.audio_encoder.load_state_dict(sds["audio"])
+    model.image_encoder.load_state_dict(sds["image"])
+    enc = list(model.audio_encoder.parameters()) + list(model.image_encoder.parameters())
+    encid = {id(p) for p in enc}
+    opt = tspm_amd.FusedAdam([{"params": enc, "lr": ENC_LR, "weight_decay": ENC_WD},
+                              {"params": [p for p in model.parameters() if id(p) not in encid]}],
+                             lr=5e-4, weight_decay=1e-4)
+    steps, evals, curve = {}, {}, []
+    for ep in range(epochs):
+        t0 = time.time()
+        order = _order(len(tr), ep, seed).to(dev)
+        losses = []
+        for b in range(0, len(tr), BATCH):
+            idx = order[b:b + BATCH].contiguous()
+            n = idx.numel()
+            st = steps.get(n) or steps.setdefault(n, tspm_amd.FusedTrainStep(model, opt, None, n))
+            dtr.gather(idx, out=(st.A, st.I, st.labels))
+            st.keep_override = _keep(seed, ep, b // BATCH, n).to(dev, non_blocking=True)
+            st.run()
+            losses.append(st.loss.clone())
+        correct = torch.zeros((), dtype=torch.int64, device=dev)
+        for b in range(0, len(te), BATCH):
+            idx = torch.arange(b, min(len(te), b + BATCH), device=dev)
+            n = idx.numel()
+            ev = evals.get(n) or evals.setdefault(n, FusedEvalStep(model, None, n))
+            dte.gather(idx, out=(ev.A, ev.I, ev.labels))
+            ev.run()
+            correct += (ev.preds == ev.labels).sum()
+        torch.cuda.synchronize()
+        curve.append({"epoch": ep + 1, "train_loss": float(np.mean([x.item() for x in losses])),
+                      "test_accuracy": int(correct) / len(te), "seconds": round(time.time() - t0, 2)})
+        print(json.dumps(curve[-1]), flush=True)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f"accuracy_pt_ours_s{seed}.json"), "w") as f:
+        json.dump({"side": "ours (HIP path, MI355X), pretrained encoders", "seed": seed, "mono": mono_curve,
+                   "curve": curve}, f, indent=1)
+
+
+def compare(out_path: str, ref_side: str = "reference", our_side: str = "ours", what: str = None) -> None:
     from scipy import stats
 
     def runs(side):
@@ -188,7 +339,7 @@ def compare(out_path: str, ref_side: str = "reference") -> None:
             d = json.load(open(p))
             out[d["seed"]] = d["curve"]
         return out
-    ref, our = runs(ref_side), runs("ours")
+    ref, our = runs(ref_side), runs(our_side)
     seeds = sorted(set(ref) & set(our))
     n = min(min(len(ref[s]) for s in seeds), min(len(our[s]) for s in seeds))
     rows = []
@@ -224,10 +375,10 @@ def compare(out_path: str, ref_side: str = "reference") -> None:
                                          "ours_mean": round(float(np.mean(o)), 5),
                                          "reference_std_pp": round(100 * float(np.std(r, ddof=1)), 3),
                                          "paired": {**paired(o, r), **paired90(o, r)}}
-    doc = {"what": "late-fusion AVMNIST on the reference's own sample files (24,000 train / 6,000 test pairs, "
-                   "speaker-disjoint test; own pairing — the reference's split CSVs are absent); paired runs: "
-                   "same initial weights (seed s), batch order and dropout masks on both sides; batch 128, "
-                   "Adam 5e-4 / 1e-4, dropout 0.5",
+    doc = {"what": what or ("late-fusion AVMNIST on the reference's own sample files (24,000 train / 6,000 test "
+                            "pairs, speaker-disjoint test; own pairing — the reference's split CSVs are absent); paired "
+                            "runs: same initial weights (seed s), batch order and dropout masks on both sides; batch "
+                            "128, Adam 5e-4 / 1e-4, dropout 0.5"),
            "reference_side": json.load(open(glob.glob(os.path.join(OUT, f"accuracy_{ref_side}_s*.json"))[0]))["side"],
            "seeds": seeds, "epochs_compared": n, "test_samples": TEST_PER_DIGIT * 10,
            "one_sample_pp": round(100 / (TEST_PER_DIGIT * 10), 4),
@@ -251,7 +402,8 @@ def compare(out_path: str, ref_side: str = "reference") -> None:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["prepare", "reference", "ours", "compare"])
+    ap.add_argument("what", choices=["prepare", "reference", "ours", "compare", "pt_reference", "pt_ours", "pt_compare"])
+    ap.add_argument("--mono-epochs", type=int, default=10, help="pretrained variant: encoder pre-training epochs")
     ap.add_argument("--epochs", type=int, default=6)
     ap.add_argument("--seeds", default="0", help="comma-separated dropout seeds (one run each)")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r2_accuracy_parity.json"))
@@ -268,6 +420,18 @@ def main() -> None:
     elif a.what == "ours":
         for sd in a.seeds.split(","):
             ours(a.epochs, int(sd))
+    elif a.what == "pt_reference":
+        for sd in a.seeds.split(","):
+            pretrained_reference(a.mono_epochs, a.epochs, int(sd), a.device)
+    elif a.what == "pt_ours":
+        for sd in a.seeds.split(","):
+            pretrained_ours(a.mono_epochs, a.epochs, int(sd))
+    elif a.what == "pt_compare":
+        compare(a.out, "pt_reference_gpu", "pt_ours",
+                "pretrained-encoder late fusion on the reference's AVMNIST files (same 24,000 / 6,000 split): each "
+                f"encoder pre-trained alone for {a.mono_epochs} epochs (MonomodalEncoder, Adam 5e-4 / 1e-4, seed s+100), "
+                "then the fusion model (seed s) with encoders at lr 1e-4 / wd 2e-4 and the head at 5e-4 / 1e-4 "
+                "(train_avmnist_resnet_pretrained.yaml param groups); same batch orders and dropout masks on both sides")
     else:
         compare(a.out, "reference_gpu" if a.device == "cuda" else "reference")
 

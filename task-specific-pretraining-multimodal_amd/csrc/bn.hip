@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
     }
     if (RELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+      for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
     }
     st4(out + 4 * i, o);
   }
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_t(long long M, int C, const fl
       }
       if (RELU) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+        for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
       }
       st4(out + off, o);
     }

@@ -39,6 +39,8 @@ TSPM_DEV bool tspm_dropout_keep(uint64_t base, long long i, float p) {
   return (float)(h >> 40) * (1.0f / 16777216.0f) >= p;
 }
 
+// nn.ReLU / F.relu: clamp_min(x, 0), which propagates NaN (fmaxf would return 0 for a NaN input)
+TSPM_DEV float relu_f(float v) { return v > 0.f ? v : (v != v ? v : 0.f); }
 TSPM_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 TSPM_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 

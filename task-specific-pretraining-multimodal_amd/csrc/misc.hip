@@ -180,8 +180,8 @@ TSPM_DEV void gemm_body(const GemmArgs& g, int bid, float* lds) {
       const int cm = row0 + acc_row(r, lane);
       if (cm >= g.M) continue;
       float v = acc[r] + bv;
-      if (g.relu) v = fmaxf(v, 0.f);
-      if (g.keep) v = g.keep[(long long)cm * g.N + ccol] ? v * g.kscale : 0.f;
+      if (g.relu) v = relu_f(v);
+      if (g.keep) v *= g.keep[(long long)cm * g.N + ccol] ? g.kscale : 0.f;  // x * mask (NaN stays NaN)
       g.C[(long long)cm * g.ldc + ccol] = v;
     }
   }
@@ -226,8 +226,8 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs g, int splits) {
 #pragma unroll 8
     for (int sidx = 0; sidx < splits; ++sidx) v += g.slab[(long long)sidx * total + t];  // loads in flight together
     if (g.bias) v += g.bias[ccol];
-    if (g.relu) v = fmaxf(v, 0.f);
-    if (g.keep) v = g.keep[t] ? v * g.kscale : 0.f;
+    if (g.relu) v = relu_f(v);
+    if (g.keep) v *= g.keep[t] ? g.kscale : 0.f;
     g.C[(long long)cm * g.ldc + ccol] = v;
   }
   if (g.rowsum && g.slab_rs) {
