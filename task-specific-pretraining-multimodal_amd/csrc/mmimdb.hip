@@ -236,11 +236,15 @@ struct Bn1dFwd {
   float keep_scale;
 };
 
+// DROP: the Dropout-after-BN variant (tspm_bn1d_fwd_drop) — a template parameter so the plain
+// BatchNorm1d launches compile exactly as before (a runtime branch in the row loop cost them 1-2 us).
+template <bool DROP = false>
 TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red);
 
+template <bool DROP>
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd(int m, Bn1dFwd p) {
   __shared__ double red[kBnCh * kBnGroups];
-  bn1d_fwd_body(m, p, blockIdx.x, red);
+  bn1d_fwd_body<DROP>(m, p, blockIdx.x, red);
 }
 
 // Two independent BatchNorm1d layers over the same rows (the MMIMDb image and text encoders' input
@@ -253,6 +257,7 @@ __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_fwd2(int m, Bn1dFwd 
     bn1d_fwd_body(m, p1, blockIdx.x - nb0, red);
 }
 
+template <bool DROP>
 TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red) {
   const int c = p.c;
   const float* __restrict__ x = p.x;
@@ -287,7 +292,7 @@ TSPM_DEV void bn1d_fwd_body(int m, const Bn1dFwd& p, int bid, double* red) {
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
     const float v = (x[i] - mean) * invstd * ga + be;
-    p.y[i] = p.keep ? v * (p.keep[i] ? p.keep_scale : 0.f) : v;
+    p.y[i] = (DROP && p.keep) ? v * (p.keep[i] ? p.keep_scale : 0.f) : v;
   }
 }
 
@@ -310,11 +315,14 @@ struct Bn1dBwd {
   int relu_x;
 };
 
+// DR: the Dropout-gradient-in / ReLU-mask-out variant (tspm_bn1d_bwd_drop_relu), compiled separately.
+template <bool DR = false>
 TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red);
 
+template <bool DR>
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd(int m, Bn1dBwd p) {
   __shared__ double red[kBnCh * kBnGroups];
-  bn1d_bwd_body(m, p, blockIdx.x, red);
+  bn1d_bwd_body<DR>(m, p, blockIdx.x, red);
 }
 
 __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd2(int m, Bn1dBwd p0, Bn1dBwd p1, int nb0) {
@@ -325,6 +333,7 @@ __global__ __launch_bounds__(kBnCh * kBnGroups) void k_bn1d_bwd2(int m, Bn1dBwd 
     bn1d_bwd_body(m, p1, blockIdx.x - nb0, red);
 }
 
+template <bool DR>
 TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   const int c = p.c;
   const float* __restrict__ g = p.g;
@@ -344,7 +353,7 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
   const uint8_t* __restrict__ gk = p.g_keep;
   const float gs = p.g_scale;
-  auto gval = [&](long long i) -> float { return gk ? g[i] * (gk[i] ? gs : 0.f) : g[i]; };
+  auto gval = [&](long long i) -> float { return (DR && gk) ? g[i] * (gk[i] ? gs : 0.f) : g[i]; };
   double sg = 0.0, sgx = 0.0;
   if (ok)
 #pragma unroll 4
@@ -366,7 +375,7 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
     float v = (float)(k * ((double)gval(i) - mg - ((double)x[i] - (double)mean) * (double)invstd * mgx));
-    if (p.relu_x && !(x[i] > 0.f)) v = 0.f;
+    if (DR && p.relu_x && !(x[i] > 0.f)) v = 0.f;
     if (dx) dx[i] = v;
     if (mo_da) {  // x was MaxOut(2)+Dropout of a[m, 2c]: route v as k_maxout_bwd does
       const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;
@@ -580,7 +589,7 @@ extern "C" int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* 
                              float* save_invstd, float* y, tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !x || !gamma || !beta || !save_mean || !save_invstd || !y) return TSPM_ERR_INVALID;
   const Bn1dFwd p{c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y};
-  hipLaunchKernelGGL(k_bn1d_fwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(k_bn1d_fwd<false>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -591,7 +600,7 @@ extern "C" int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* 
                              tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
   const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr};
-  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(k_bn1d_bwd<false>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -604,7 +613,7 @@ extern "C" int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const 
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta || !a || !da)
     return TSPM_ERR_INVALID;
   const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da};
-  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(k_bn1d_bwd<false>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -616,7 +625,7 @@ extern "C" int tspm_bn1d_fwd_drop(int32_t m, int32_t c, const float* x, const fl
                                   tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !x || !gamma || !beta || !save_mean || !save_invstd || !y) return TSPM_ERR_INVALID;
   const Bn1dFwd p{c, x, gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, y, keep, keep_scale};
-  hipLaunchKernelGGL(k_bn1d_fwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(k_bn1d_fwd<true>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -627,7 +636,7 @@ extern "C" int tspm_bn1d_bwd_drop_relu(int32_t m, int32_t c, const float* g, con
                                        float* dgamma, float* dbeta, float* dx, tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
   const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr, g_keep, g_scale, 1};
-  hipLaunchKernelGGL(k_bn1d_bwd, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(k_bn1d_bwd<true>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
