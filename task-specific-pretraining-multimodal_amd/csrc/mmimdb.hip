@@ -215,10 +215,16 @@ TSPM_DEV double bn_group_sum(double v, double* red) {
   __syncthreads();
   red[grp * kBnCh + ch] = v;
   __syncthreads();
-  double t = 0.0;
+  // one row group forms each channel's total (same order as before) and publishes it: every thread
+  // summing all kBnGroups doubles itself read 256 KB of LDS per call (≈ 1 µs at these sizes)
+  if (grp == 0) {
+    double t = 0.0;
 #pragma unroll
-  for (int q = 0; q < kBnGroups; ++q) t += red[q * kBnCh + ch];
-  return t;
+    for (int q = 0; q < kBnGroups; ++q) t += red[q * kBnCh + ch];
+    red[ch] = t;
+  }
+  __syncthreads();
+  return red[ch];
 }
 
 struct Bn1dFwd {
