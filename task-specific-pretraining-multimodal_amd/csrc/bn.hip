@@ -115,6 +115,11 @@ bool bn_wide() {
   const char* e = getenv("TSPM_BN_WIDE");
   return !(e && e[0] == '0');
 }
+// A/B switch read per call: unset = `dflt`, "0" = off, anything else = on
+bool getenv_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? e[0] != '0' : dflt;
+}
 
 // ------------------------------------------------------------------------------------------------
 // apply: out = act(y*scale + shift [+ res | + res*scale2 + shift2])
@@ -241,13 +246,15 @@ __global__ __launch_bounds__(256) void k_bn_apply_t(long long M, int C, const fl
 // tiles (rows in batches of 4 per thread so their loads are in flight together).  An in-launch
 // merge by the last workgroup was measured slower than the parallel pass 2 below (the merge of
 // >= 64 tiles per channel block serialises on one CU), so pass 2 stays a launch.
-template <bool HAS_OUT, bool TWO, int U>
-__global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
+// RG row groups of 16 lanes: 16 (256 threads), or 64 (1,024 threads) for the long tiles of the 64-channel
+// layers, whose partial pass has only 64 workgroups — four times the loads in flight per CU.
+template <bool HAS_OUT, bool TWO, int U, int RG = kRowGroups>
+__global__ __launch_bounds__(16 * RG) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
                                                         const float* __restrict__ out, const float* __restrict__ y,
                                                         const float* __restrict__ mean, const float* __restrict__ y2,
                                                         const float* __restrict__ mean2, long long rows_per_block,
                                                         float* __restrict__ part) {
-  __shared__ f32x4 sh[3][256];
+  __shared__ f32x4 sh[3][16 * RG];
   const int t = threadIdx.x;
   const int lane = t & 15, rg = t >> 4;
   const int c4 = blockIdx.y * 16 + lane;
@@ -259,11 +266,11 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
     const f32x4 mu = ld4(mean + 4 * c4);
     const f32x4 mu2 = TWO ? ld4(mean2 + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
     // U rows per batch: all their loads in flight together
-    for (long long rb = r_begin + rg; rb < r_end; rb += U * kRowGroups) {
+    for (long long rb = r_begin + rg; rb < r_end; rb += U * RG) {
       f32x4 gv[U], yv[U], y2v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long long row = rb + u * kRowGroups;
+        const long long row = rb + u * RG;
         if (row < r_end) {
           const long long off = row * C + 4 * c4;
           gv[u] = ld4(g + off);
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_partial(long long M, int C, cons
   __syncthreads();
   const long long plane = (long long)gridDim.x * C;
   if (rg == 0 && cok) {
-    for (int k = 1; k < kRowGroups; ++k) {
+    for (int k = 1; k < RG; ++k) {
       sg += sh[0][k * 16 + lane];
       sx += sh[1][k * 16 + lane];
       if (TWO) sx2 += sh[2][k * 16 + lane];
@@ -1003,11 +1010,19 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
   // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide)
   const int pu = !bn_wide() ? 4 : rpb >= 64LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
+  // 1,024-thread workgroups for the 64-channel layers' tiles (TSPM_BN_PART_RG64=1; off by default: measured
+  // BN device time 1.020 -> 0.972 ms per step but the step 2.778 -> 2.786 ms — the wider workgroups
+  // crowd the other encoder's stream)
+  const bool wide_rg = bn_wide() && c <= 64 && rpb >= 64 && getenv_flag("TSPM_BN_PART_RG64", false);
 #define BNB_P(HO, TW, U)                                                                                     \
-  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y, mean, \
-                     y2, mean2, rpb, part)
+  if (wide_rg)                                                                                               \
+    hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, (U > 4 ? U / 2 : 4), 64>), pgrid, dim3(1024), 0, st,        \
+                       (long long)m, c, g, out, y, mean, y2, mean2, rpb, part);                              \
+  else                                                                                                       \
+    hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y,   \
+                       mean, y2, mean2, rpb, part)
 #define BNB_PU(HO, TW) \
-  if (pu == 16) BNB_P(HO, TW, 16); else if (pu == 8) BNB_P(HO, TW, 8); else BNB_P(HO, TW, 4);
+  if (pu == 16) { BNB_P(HO, TW, 16); } else if (pu == 8) { BNB_P(HO, TW, 8); } else { BNB_P(HO, TW, 4); }
   if (ho) { if (two) { BNB_PU(true, true) } else { BNB_PU(true, false) } }
   else { if (two) { BNB_PU(false, true) } else { BNB_PU(false, false) } }
 #undef BNB_PU
