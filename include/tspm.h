@@ -535,7 +535,8 @@ int tspm_bce_logits(int32_t n, int32_t classes, const float* logits, const float
  * [T+1][B][H] (hs[0] = h0 = 0).  argmax NULL ("last"): h_T goes to h_out (row stride ld_out); argmax
  * non-NULL ("maxpool", ABI 14; lstm.py:47-52 F.max_pool1d over r_out): max over t of h_t goes to h_out
  * and its time index (first maximum, NaN wins) to argmax uint8 [batch][hidden] (steps <= 256).  hidden
- * must be 64 and batch even. */
+ * must be 64; any batch >= 1 (an odd batch leaves the last 2-row workgroup one ghost row, which reads the
+ * last real row and writes nothing). */
 typedef struct tspm_lstm_fwd_desc {
   int32_t batch, steps, hidden, ld_out;
   const float* xg;

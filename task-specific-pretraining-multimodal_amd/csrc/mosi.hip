@@ -50,19 +50,22 @@ TSPM_DEV void lstm_fwd_body(const LstmFwdDesc& d, int chunk) {
     w[k] = v[0]; w[k + 1] = v[1]; w[k + 2] = v[2]; w[k + 3] = v[3];
   }
   const float bh = d.bhh ? d.bhh[j] : 0.f;
-  const bool cell = j < RB * H;
+  // an odd batch leaves the last workgroup one row short: that ghost row reads the last real row's inputs
+  // (clamped index) and writes nothing
   const int cr = j / H, cu = j - (j / H) * H;
+  const bool cell = j < RB * H && b0 + cr < B;
   float c = 0.f, h = 0.f;
   float mx = -INFINITY;  // embd "maxpool": running max over t of h_t and its first index (NaN wins, as
   int am = 0;            // max_pool2d_with_indices: val > max || isnan(val))
-  if (cell) {
-    hsh[cr][cu] = 0.f;
-    d.hs[(long long)(b0 + cr) * H + cu] = 0.f;
-  }
+  if (j < RB * H) hsh[cr][cu] = 0.f;
+  if (cell) d.hs[(long long)(b0 + cr) * H + cu] = 0.f;
   const bool sig = j < 2 * H || j >= 3 * H;
+  int rowc[RB];  // clamped row of each of the workgroup's rows
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rowc[r] = min(b0 + r, B - 1);
   float xn[RB];
 #pragma unroll
-  for (int r = 0; r < RB; ++r) xn[r] = d.xg[((long long)b0 + r) * G + j];
+  for (int r = 0; r < RB; ++r) xn[r] = d.xg[(long long)rowc[r] * G + j];
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     float xc[RB];
@@ -70,7 +73,7 @@ TSPM_DEV void lstm_fwd_body(const LstmFwdDesc& d, int chunk) {
     for (int r = 0; r < RB; ++r) xc[r] = xn[r];
     if (t + 1 < T) {
 #pragma unroll
-      for (int r = 0; r < RB; ++r) xn[r] = d.xg[((long long)(t + 1) * B + b0 + r) * G + j];
+      for (int r = 0; r < RB; ++r) xn[r] = d.xg[((long long)(t + 1) * B + rowc[r]) * G + j];
     }
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
@@ -86,17 +89,19 @@ TSPM_DEV void lstm_fwd_body(const LstmFwdDesc& d, int chunk) {
       const float pre = (acc + bh) + xc[r];
       const float a = sig ? sigmoidf_(pre) : tanhf(pre);
       gsh[r][j] = a;
-      d.gates[((long long)t * B + b0 + r) * G + j] = a;
+      if (b0 + r < B) d.gates[((long long)t * B + b0 + r) * G + j] = a;
     }
     __syncthreads();
-    if (cell) {
+    if (j < RB * H) {
       const float ig = gsh[cr][cu], fg = gsh[cr][H + cu], gg = gsh[cr][2 * H + cu], og = gsh[cr][3 * H + cu];
       c = fg * c + ig * gg;
       h = og * tanhf(c);
+      hsh[cr][cu] = h;
+    }
+    if (cell) {
       const long long o = ((long long)t * B + b0 + cr) * H + cu;
       d.cs[o] = c;
       d.hs[o + (long long)B * H] = h;
-      hsh[cr][cu] = h;
       if (d.arg && (h > mx || h != h)) {
         mx = h;
         am = t;
@@ -147,13 +152,16 @@ TSPM_DEV void lstm_bwd_body(const LstmBwdDesc& d, int chunk) {
   float wc[H];
 #pragma unroll
   for (int jj = 0; jj < H; ++jj) wc[jj] = d.whh[(long long)(q * H + jj) * H + k];
-  const bool cell = tid < RB * H;
   const int cr = tid / H, cu = tid - (tid / H) * H;
+  const bool cell = tid < RB * H && b0 + cr < B;  // a ghost row (odd batch) computes zeros, writes nothing
   float dc = 0.f, dh = 0.f, gin = 0.f;
   int am = T - 1;  // the step whose h received the embedding gradient
   if (cell) {
     gin = d.dh[(long long)(b0 + cr) * d.lddh + cu];
     if (d.arg) am = d.arg[(long long)(b0 + cr) * H + cu];
+  }
+  if (tid < RB * H && !cell) {
+    dgs[cr][cu] = 0.f; dgs[cr][H + cu] = 0.f; dgs[cr][2 * H + cu] = 0.f; dgs[cr][3 * H + cu] = 0.f;
   }
   for (int t = T - 1; t >= 0; --t) {
     if (cell) {
@@ -450,7 +458,7 @@ int grid_for(long long work) {
 
 template <int H, int RB>
 int launch_lstm_fwd(const LstmFwdDesc& a, const LstmFwdDesc* b, hipStream_t st) {
-  const int na = a.B / RB, nbb = b ? b->B / RB : 0;
+  const int na = (a.B + RB - 1) / RB, nbb = b ? (b->B + RB - 1) / RB : 0;
   hipLaunchKernelGGL((k_lstm_fwd<H, RB>), dim3(na + nbb), dim3(4 * H), 0, st, a, b ? *b : a, na);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -458,7 +466,7 @@ int launch_lstm_fwd(const LstmFwdDesc& a, const LstmFwdDesc* b, hipStream_t st) 
 
 template <int H, int RB>
 int launch_lstm_bwd(const LstmBwdDesc& a, const LstmBwdDesc* b, hipStream_t st) {
-  const int na = a.B / RB, nbb = b ? b->B / RB : 0;
+  const int na = (a.B + RB - 1) / RB, nbb = b ? (b->B + RB - 1) / RB : 0;
   hipLaunchKernelGGL((k_lstm_bwd<H, RB>), dim3(na + nbb), dim3(4 * H), 0, st, a, b ? *b : a, na);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -467,7 +475,7 @@ int launch_lstm_bwd(const LstmBwdDesc& a, const LstmBwdDesc* b, hipStream_t st) 
 constexpr int kLstmRB = 2;  // batch rows per workgroup (B = 128: 64 workgroups per LSTM)
 
 bool lstm_ok(int B, int T, int H, const void* p0, const void* p1, const void* p2, const void* p3) {
-  return B > 0 && T > 0 && H == 64 && B % kLstmRB == 0 && p0 && p1 && p2 && p3;
+  return B > 0 && T > 0 && H == 64 && p0 && p1 && p2 && p3;
 }
 
 }  // namespace

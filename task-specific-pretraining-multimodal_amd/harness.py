@@ -50,6 +50,17 @@ AVMNIST_METRICS = {
 }
 
 
+# the MOSI / MOSEI UTT-Fusion YAMLs' metric block (configs/mosi/centralised/utt_fusion_base_training.yaml:151-162)
+MOSI_METRICS = {
+    "metrics": {
+        "MSA": {"function": "metrics.msa_binary_classification", "kwargs": {}, "level": "epoch"},
+        "ConfusionMatrix": {"function": "sklearn.metrics.confusion_matrix", "kwargs": {"labels": [0, 1, 2]},
+                            "level": "epoch"},
+    },
+    "groups": {"classification": ["MSA", "ConfusionMatrix"]},
+}
+
+
 def check_early_stopping(val_metrics: Dict[str, Any], best_metrics: Optional[Dict[str, Any]], patience: int,
                          min_delta: float, wait: int, mode: str = "minimize",
                          target_metric: str = "loss") -> Tuple[bool, bool, int]:
@@ -166,6 +177,96 @@ class EpochRunner:
         return self._finish(t0)
 
 
+class MosiEpochRunner:
+    """train_epoch / validate_epoch (train_multimodal.py:438-541) for UttFusionModel on the fused steps, over the
+    seven missing-modality patterns (data/mosi.py:61-69).  A batch is a collate_fn-style dict — batch-first
+    tensors, or the time-major buffers of this runner's own steps when the loader gathered into them
+    (``MosiDeviceLoader`` with ``step_for`` pointed here by ``loader_for``) — or, for valid / test, the
+    pattern-grouped ``{pattern: sub-batch}`` of data/mosi.py:236-251; each group is one ``validation_step`` (one
+    ``FusedMosiEvalStep`` replay: its loss is one entry of the epoch's loss log, its rows go to the confusion
+    counts of their pattern).  Per-pattern metrics come from ``DeviceMetricRecorder`` with the YAML's MSA and
+    confusion-matrix functions (keys ``MSA_Has0_Accuracy_ATV`` ...; metric_recorder.py:147-209)."""
+
+    def __init__(self, model, optimizer, loss_functions, metric_config=None, device=None, log_capacity: int = 1 << 16):
+        from .mosi_data import PATTERNS
+        self.model, self.optimizer, self.loss_functions = model, optimizer, loss_functions
+        self.device = device or next(model.parameters()).device
+        self.log = ClassificationLog(self.device, groups=PATTERNS, classes=3, capacity=log_capacity)
+        self.recorder = DeviceMetricRecorder(metric_config or MOSI_METRICS, self.log)
+        self.eval_steps: Dict[Tuple[int, int], Any] = {}
+
+    def train_step_for(self, b: int, t: int):
+        st = self.model.fused_step(self.optimizer, self.loss_functions, b, t)
+        if st.log is not self.log:
+            st.log, st.graph = self.log, None  # the captured graph must record into this log
+        return st
+
+    def eval_step_for(self, b: int, t: int):
+        from .mosi import FusedMosiEvalStep
+        st = self.eval_steps.get((b, t))
+        if st is None:
+            st = FusedMosiEvalStep(self.model, self.loss_functions, b, t, self.log)
+            self.eval_steps[(b, t)] = st
+        return st
+
+    def loader_for(self, loader, train: bool):
+        """Point a ``MosiDeviceLoader`` at this runner's steps (batches gathered straight into their inputs)."""
+        if hasattr(loader, "step_for"):
+            loader.step_for = self.train_step_for if train else self.eval_step_for
+        return loader
+
+    def _run(self, st, b: Dict[str, Any]) -> None:
+        st.eng.groups.copy_(self.log.group_ids(b.get("pattern_name") or b["pattern_names"]), non_blocking=True)
+        if b.get("time_major") and b["audio"] is st.eng.A:
+            st.run()
+        else:
+            st.step(b["audio"], b["video"], b["text"], b["label"])
+
+    @staticmethod
+    def _shape(b: Dict[str, Any]) -> Tuple[int, int]:
+        return int(b["label"].numel()), int(b.get("steps") or b["audio"].shape[1])
+
+    @staticmethod
+    def _groups(b: Dict[str, Any]):
+        if "label" in b:
+            return [b]
+        return list(b.values())  # {pattern: sub-batch}
+
+    def _finish(self, t0: float):
+        conf, losses, _ = self.log.fetch()  # the epoch's only host synchronisation
+        mean = ClassificationLog.mean_loss(losses)
+        metrics = self.recorder.calculate_metrics_for_group("classification", loss=mean, conf=conf)
+        return mean, time.time() - t0, metrics, len(losses)
+
+    def train_epoch(self, loader: Iterable[Dict[str, Any]]):
+        """→ (mean batch loss, seconds, metrics dict, batches)."""
+        self.log.reset()
+        t0 = time.time()
+        for b in self.loader_for(loader, True):
+            for g in self._groups(b):
+                self._run(self.train_step_for(*self._shape(g)), g)
+        return self._finish(t0)
+
+    @torch.no_grad()
+    def validate_epoch(self, loader: Iterable[Dict[str, Any]]):
+        self.log.reset()
+        t0 = time.time()
+        self.model.eval()
+        for b in self.loader_for(loader, False):
+            for g in self._groups(b):
+                self._run(self.eval_step_for(*self._shape(g)), g)
+        self.model.train()
+        return self._finish(t0)
+
+
+def runner_for(model, optimizer, loss_functions, metric_config=None):
+    """The epoch runner of the model family: AVMNIST late fusion, or MOSI / MOSEI UTT-Fusion."""
+    from .mosi import UttFusionModel
+    if isinstance(model, UttFusionModel):
+        return MosiEpochRunner(model, optimizer, loss_functions, metric_config)
+    return EpochRunner(model, optimizer, loss_functions, metric_config)
+
+
 def _epoch_block(loss: float, timing: float, n_batches: int, metrics: Dict[str, Any]) -> Dict[str, Any]:
     """One split's entry of epoch_metrics.json (train_multimodal.py:627-718)."""
     out: Dict[str, Any] = {"loss": loss, "timing": {"total_time": timing,
@@ -187,13 +288,14 @@ def fit(model, optimizer, loss_functions, loaders: Dict[str, Any], epochs: int, 
         early_stopping: bool = True, patience: int = 10, min_delta: float = 1e-3, scheduler=None,
         checkpoint_dir=None, metrics_path=None, save_metric: str = "loss", mode: str = "minimize",
         on_epoch=None, fail_on_nonfinite: bool = True) -> Dict[str, Any]:
-    """_train_loop + test (train_multimodal.py:554-917) for the AVMNIST late-fusion model.  ``loaders``:
+    """_train_loop + test (train_multimodal.py:554-917) for the AVMNIST late-fusion model and the MOSI / MOSEI
+    UTT-Fusion model (``runner_for``; its loaders: ``mosi_data.MOSI.loader(...)``).  ``loaders``:
     "train", "validation" and optionally "test" → iterables of device batches (a DeviceLoader is
     re-iterated each epoch; call ``set_epoch`` in ``on_epoch`` for DistributedSampler order).
     ``fail_on_nonfinite``: raise FloatingPointError as soon as an epoch's mean training loss is NaN / inf
     (checked at the epoch's one host synchronisation; SURVEY §5 — the reference only turns three numpy
     RuntimeWarnings into errors, train_multimodal.py:46-60, and would keep training on NaN weights)."""
-    runner = EpochRunner(model, optimizer, loss_functions, metric_config)
+    runner = runner_for(model, optimizer, loss_functions, metric_config)
     ckpt = CheckpointManager(checkpoint_dir, save_metric, mode) if checkpoint_dir is not None else None
     history: Dict[str, Any] = {"train": [], "validation": [], "epoch_metrics": []}
     best, wait = None, 0

@@ -88,7 +88,20 @@ class ClassificationLog:
         return float(np.mean([float(x) for x in losses])) if len(losses) else float("nan")
 
 
+# metric functions the reference's YAMLs name from its own ``metrics`` package (MML_Suite/metrics/__init__.py),
+# restated in this package (the reference is not importable on the GPU box)
+REFERENCE_METRICS = {
+    "metrics.msa_binary_classification": ("msa_metrics", "msa_binary_classification"),   # metrics/msa.py:44-92
+    "metrics.msa.msa_binary_classification": ("msa_metrics", "msa_binary_classification"),
+}
+
+
 def _resolve(path: str) -> Callable:
+    if path in REFERENCE_METRICS:
+        mod, fn = REFERENCE_METRICS[path]
+        return getattr(importlib.import_module(f"{__package__}.{mod}"), fn)
+    if path in ("metrics.confusion_matrix_from_logits", "metrics.msa.confusion_matrix_from_logits"):
+        path = "sklearn.metrics.confusion_matrix"  # metrics/msa.py:40-41: the same call
     mod, fn = path.rsplit(".", 1)
     return getattr(importlib.import_module(mod), fn)
 
@@ -103,6 +116,8 @@ def evaluate(fn_path: str, kwargs: Dict[str, Any], conf: np.ndarray):
     """Value of metric ``fn_path(y_true, y_pred, **kwargs)`` over the samples counted in ``conf``."""
     fn = _resolve(fn_path)
     t, p, w = compressed(conf)
+    if fn_path in REFERENCE_METRICS:  # not sklearn: the expanded arrays
+        return fn(np.repeat(t, w), np.repeat(p, w), **kwargs)
     if fn_path.rsplit(".", 1)[1] in CONFUSION_ONLY and "sample_weight" not in kwargs:
         return fn(t, p, sample_weight=w, **kwargs)
     return fn(np.repeat(t, w), np.repeat(p, w), **kwargs)
@@ -144,7 +159,12 @@ class DeviceMetricRecorder:
                 if name not in self.metrics:
                     continue
                 path, kw = self.metrics[name]
-                value = evaluate(path, kw, c)
+                try:
+                    value = evaluate(path, kw, c)
+                except (ImportError, AttributeError):
+                    raise
+                except Exception:  # metric_recorder.py:199-201: a failing metric is reported and skipped
+                    continue
                 if isinstance(value, dict):
                     for k, v in value.items():
                         results[f"{name}_{k}_{tag}"] = v

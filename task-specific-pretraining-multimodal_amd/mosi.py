@@ -43,6 +43,7 @@ from .linear import linear_bwd
 from .optim import FusedAdam
 
 NUM_CLASSES = 3  # data/mosi.py:26 (classification_labels)
+_CLS_SEED_SALT = 0x6A09E667F3BCC909  # the classifier masks' seed = model seed ^ salt (independent of the text masks)
 PATTERNS = {"atv": (1.0, 1.0, 1.0), "at": (1.0, 1.0, 0.0), "av": (1.0, 0.0, 1.0), "tv": (0.0, 1.0, 1.0),
             "a": (1.0, 0.0, 0.0), "t": (0.0, 1.0, 0.0), "v": (0.0, 0.0, 1.0)}  # (audio, text, video) data/mosi.py:60-68
 
@@ -136,9 +137,25 @@ class FcClassifier(nn.Module):
             input_dim = layers[i]
         self.module = nn.Sequential(*self.all_layers)
         self.fc_out = nn.Linear(layers[-1], output_dim)
-        self.dropout_p = float(dropout)
         self.widths = [int(w) for w in layers]
         self.use_bn = bool(use_bn)
+
+    @property
+    def dropout_p(self) -> float:
+        """The rate the kernels use, read from the nn.Dropout modules each time (one rate per classifier,
+        classifier.py:104-105; 0 when the classifier was built without dropout)."""
+        ps = {float(m.p) for m in self.module if isinstance(m, nn.Dropout)}
+        if len(ps) > 1:
+            raise L.TspmError(f"FcClassifier HIP path: one dropout rate for every layer (found {sorted(ps)})")
+        return ps.pop() if ps else 0.0
+
+    @dropout_p.setter
+    def dropout_p(self, p: float) -> None:
+        drops = [m for m in self.module if isinstance(m, nn.Dropout)]
+        if not drops and p > 0:
+            raise L.TspmError("FcClassifier was built without dropout layers")
+        for m in drops:
+            m.p = float(p)
 
     def linears(self):
         return [m for m in self.module if isinstance(m, nn.Linear)]
@@ -167,8 +184,6 @@ class MosiEngine:
         a, v, t, c = model.netA, model.netV, model.netT, model.netC
         if a.hidden_size != 64 or v.hidden_size != 64:
             raise NotImplementedError("MOSI HIP path: LSTM hidden size 64 (tspm_lstm_fwd)")
-        if batch % 2:
-            raise L.TspmError("MOSI HIP path: the batch must be even (2 rows per LSTM workgroup)")
         if steps > 255 or min(t.heights) > steps or max(t.heights) > 5:
             raise L.TspmError("MOSI HIP path: 1 <= kernel heights <= min(5, steps) and steps <= 255")
         f = dict(device=device, dtype=torch.float32)
@@ -281,14 +296,25 @@ class MosiEngine:
             dst.copy_(self.keep_override[k].reshape(dst.shape).to(torch.uint8), non_blocking=True)
 
     def _keep_masks(self, train: bool, sh: int) -> None:
-        p = self.m.netC.dropout_p
-        if not train or p <= 0 or self.keep_override is not None:
+        """Fresh keep masks for one training forward: the TextCNN slice (keeps[0]) at the TextCNN's own rate
+        (textcnn.py:45, netT.dropout.p), the classifier slices at the classifier's (classifier.py:104-105);
+        two independent draws (the classifier's under a derived seed) on the same step counter."""
+        pt, pc = float(self.m.netT.dropout.p), float(self.m.netC.dropout_p)
+        if not train or (pt <= 0 and pc <= 0) or self.keep_override is not None:
             return
         if self.rng_ctr_ptr is None:
             self._host_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
             self.rng_ctr_ptr = self._host_ctr.data_ptr()
-        L.check(L.lib().tspm_dropout_mask(self.keep_all.numel(), p, self.m._rng_seed, self.rng_ctr_ptr,
-                                          self.keep_all.data_ptr(), sh), "dropout_mask")
+        lib, seed = L.lib(), self.m._rng_seed
+        nt = self.keeps[0].numel()
+        if pt > 0:
+            L.check(lib.tspm_dropout_mask(nt, pt, seed, self.rng_ctr_ptr, self.keep_all.data_ptr(), sh),
+                    "dropout_mask (text)")
+        if pc > 0:
+            L.check(lib.tspm_dropout_mask(self.keep_all.numel() - nt, pc, seed ^ _CLS_SEED_SALT, self.rng_ctr_ptr,
+                                          self.keep_all.data_ptr() + nt, sh), "dropout_mask (classifier)")
+        if self._host_ctr is not None and self.rng_ctr_ptr == self._host_ctr.data_ptr():
+            self._host_ctr.add_(1)  # outside FusedMosiStep nothing else advances the counter: fresh masks per step
 
     def _fork(self):
         """Side stream for the LSTM half of the step (it shares no buffer with the TextCNN half until the
@@ -596,6 +622,52 @@ class FusedMosiStep:
         self.calls += 1
 
 
+class FusedMosiEvalStep:
+    """``validation_step``'s device work (utt_fusion.py:202-244) for one (batch, steps) shape as one HIP graph:
+    eval-mode forward (no dropout; running statistics in the MOSEI classifier BatchNorm1d), the loss group's
+    cross-entropy, and ``tspm_classify_update`` (softmax argmax, per-pattern confusion counts, the batch loss
+    appended to the epoch's log) — no host synchronisation.  Inputs are the engine's time-major buffers
+    (``mosi_data.MOSI.device_loader(step_for=...)`` gathers into them) or a batch-first batch via ``step``."""
+
+    def __init__(self, model: "UttFusionModel", loss_functions, batch: int, steps: int, log, use_graph: bool = True):
+        dev = next(model.parameters()).device
+        self.model, self.N, self.T, self.log = model, batch, steps, log
+        self.weight = _ce_weight(loss_functions)
+        if self.weight is None:
+            raise L.TspmError("FusedMosiEvalStep: the loss group must be a single cross-entropy term")
+        self.eng = model._engine(batch, steps, dev)
+        self.use_graph = use_graph and not os.environ.get("TSPM_NO_GRAPH")
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.calls = 0
+
+    def _all(self) -> None:
+        sh, e, lg = L.stream_handle(), self.eng, self.log
+        e.forward(sh, False)
+        e.loss_fn(sh, self.weight, False)
+        L.check(L.lib().tspm_classify_update(self.N, e.logits.shape[1], e.logits.data_ptr(), e.labels.data_ptr(),
+                                             e.groups.data_ptr(), len(lg.groups), lg.conf.data_ptr(), None,
+                                             e.loss.data_ptr(), lg.loss_log.data_ptr(), lg.counters.data_ptr(),
+                                             lg.capacity, sh), "classify_update")
+
+    def step(self, A, V, T, labels) -> None:
+        self.eng.load(A, V, T, labels)
+        self.run()
+
+    def run(self) -> None:
+        self.model.eval()
+        if not self.use_graph or self.calls == 0:
+            self._all()
+        else:
+            if self.graph is None:
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._all()
+                self.graph = g
+            self.graph.replay()
+        self.calls += 1
+
+
 # ------------------------------------------------------------------------------------------------
 # the model
 # ------------------------------------------------------------------------------------------------
@@ -811,8 +883,6 @@ def _encode_lstm(enc: LSTMEncoder, x: torch.Tensor) -> torch.Tensor:
     """Standalone LSTMEncoder embedding (inference): projection GEMM + one-problem tspm_lstm_fwd."""
     L.require_cuda_f32(x, "LSTMEncoder input")
     B, T, F = x.shape
-    if B % 2:
-        raise L.TspmError("LSTMEncoder HIP path: even batch")
     dev, H = x.device, enc.hidden_size
     f = dict(device=dev, dtype=torch.float32)
     xt = x.transpose(0, 1).contiguous() if T > 1 else x.reshape(1, B, F).contiguous()

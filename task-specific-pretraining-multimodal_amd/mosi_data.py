@@ -206,11 +206,13 @@ class MOSI(torch.utils.data.Dataset):
             split = raw[self.split]
         if self.labels_key not in split:
             raise KeyError(f"Labels key '{self.labels_key}' not found in data")
-        lengths = None
+        # The reference keeps the dense [N, T, F] arrays even for unaligned files and never trims them to
+        # audio_lengths / vision_lengths (data/mosi.py:134-152: lengths are metadata only); so here.
+        corpus = MosiCorpus.from_split(split, self.labels_key, None)
         if not self.aligned and "audio_lengths" in split:
-            lengths = {"audio": np.asarray(split["audio_lengths"]).astype(np.int64),
-                       "video": np.asarray(split["vision_lengths"]).astype(np.int64)}
-        return MosiCorpus.from_split(split, self.labels_key, lengths)
+            corpus.true_lengths = {"audio": np.asarray(split["audio_lengths"]).astype(np.int64),
+                                   "video": np.asarray(split["vision_lengths"]).astype(np.int64)}
+        return corpus
 
     # -- reference Dataset API ----------------------------------------------------------------------
     def __len__(self) -> int:
@@ -275,23 +277,41 @@ class MOSI(torch.utils.data.Dataset):
 
     def device_loader(self, batch_size: int, shuffle: bool = False, drop_last: bool = False,
                       generator: Optional[torch.Generator] = None, step_for=None,
-                      pad_to: int = 0) -> Iterator[Dict[str, Any]]:
-        """One epoch of batches gathered on device.  ``step_for(B, T) -> FusedMosiStep``: gather each batch
-        time-major straight into that step's input buffers.  ``pad_to``: pad every batch to at least this
-        many steps (the aligned length, e.g. 50 for aligned_50: one captured step shape for the whole
-        epoch; pad_sequence pads to the batch maximum, which equals it on the reference's dense data)."""
+                      pad_to: int = 0, group_patterns: Optional[bool] = None) -> Iterator[Dict[str, Any]]:
+        """One epoch of batches gathered on device.  ``step_for(B, T) -> FusedMosiStep`` (or
+        ``FusedMosiEvalStep``): gather each batch time-major straight into that step's input buffers.
+        ``pad_to``: pad every batch to at least this many steps (the aligned length, e.g. 50 for aligned_50:
+        one captured step shape for the whole epoch; pad_sequence pads to the batch maximum, which equals it
+        on the reference's dense data).  ``group_patterns`` (default: valid / test splits, as collate_fn):
+        each batch is ``{pattern: sub-batch}`` in first-seen order (data/mosi.py:236-251)."""
         n = len(self)
+        grouped = (self.split != "train") if group_patterns is None else bool(group_patterns)
         order = torch.randperm(n, generator=generator).numpy() if shuffle else np.arange(n)
         for s in range(0, n, batch_size):
             items = order[s:s + batch_size]
             if drop_last and len(items) < batch_size:
                 break
             rows, pid = self._resolve(items)
-            if step_for is not None:
-                t = self.device_corpus.steps_for(rows, pad_to)
-                yield self._collate(rows, pid, step_for(len(rows), t), pad_to)
-            else:
-                yield self._collate(rows, pid, None, pad_to)
+            parts = ([(self.selected_patterns[p], pid == p) for p in dict.fromkeys(pid.tolist())] if grouped
+                     else [(None, slice(None))])
+            out = {}
+            for name, sel in parts:
+                r, q = rows[sel], pid[sel]
+                if step_for is not None:
+                    t = self.device_corpus.steps_for(r, pad_to)
+                    out[name] = self._collate(r, q, step_for(len(r), t), pad_to)
+                    if grouped:
+                        yield {name: out[name]}  # the step's buffers are reused: hand each group over at once
+                        out = {}
+                else:
+                    out[name] = self._collate(r, q, None, pad_to)
+            if out:
+                yield out if grouped else out[None]
+
+    def loader(self, batch_size: int, shuffle: bool = False, drop_last: bool = False, seed: Optional[int] = None,
+               step_for=None, pad_to: int = 0, group_patterns: Optional[bool] = None) -> "MosiDeviceLoader":
+        """A re-iterable epoch loader (one ``device_loader`` pass per ``iter``), as a DataLoader is."""
+        return MosiDeviceLoader(self, batch_size, shuffle, drop_last, seed, step_for, pad_to, group_patterns)
 
     def get_split(self) -> str:
         return self.split
@@ -310,3 +330,28 @@ class MOSI(torch.utils.data.Dataset):
 class MOSEI(MOSI):
     """data/mosi.py:270-283 (CMU-MOSEI: the same MultimodalSentimentDataset, 3 classes) — the dataset of
     configs/mosei/centralised/utt_fusion_train_mosei.yaml (74-d audio, 35-d video, 768-d text)."""
+
+
+class MosiDeviceLoader:
+    """Re-iterable wrapper of ``MOSI.device_loader`` (a DataLoader is iterated once per epoch): epoch e draws
+    its shuffle from ``torch.Generator().manual_seed(seed + e)``; ``step_for`` may be replaced before an epoch
+    (the harness points it at its own train / eval steps)."""
+
+    def __init__(self, ds: MOSI, batch_size: int, shuffle: bool, drop_last: bool, seed: Optional[int], step_for,
+                 pad_to: int, group_patterns: Optional[bool]):
+        self.ds, self.batch_size, self.shuffle, self.drop_last = ds, batch_size, shuffle, drop_last
+        self.seed, self.step_for, self.pad_to, self.group_patterns = seed, step_for, pad_to, group_patterns
+        self.epoch = 0
+
+    def __len__(self) -> int:
+        n = len(self.ds)
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        gen = None
+        if self.shuffle:
+            gen = torch.Generator()
+            gen.manual_seed((self.seed if self.seed is not None else 0) + self.epoch)
+        self.epoch += 1
+        return self.ds.device_loader(self.batch_size, self.shuffle, self.drop_last, gen, self.step_for, self.pad_to,
+                                     self.group_patterns)

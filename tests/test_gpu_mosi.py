@@ -230,20 +230,52 @@ def test_lstm_bias_gradients_identical(gpu):
         assert torch.equal(enc.rnn.bias_ih_l0.grad, enc.rnn.bias_hh_l0.grad)
 
 
-def test_device_dropout_masks(gpu):
-    """Without keep_override the step draws fresh masks on the device every step (rate ~0.5)."""
-    ours = _dropin(2).to(gpu)
+@pytest.mark.parametrize("cfg_name", ["mosi", "mosei"])
+def test_device_dropout_masks(gpu, cfg_name):
+    """Without keep_override the step draws fresh masks on the device every step: the TextCNN slice at the
+    TextCNN's rate (MOSI 0.5, MOSEI 0.7 → ~30 % kept), the classifier slices at the classifier's (0.5 /
+    0.66 → ~34 % kept), the two draws independent."""
+    torch.manual_seed(2)
+    ours = M.build_utt_fusion(cfg_name).to(gpu)
+    cfg = orc.MOSI if cfg_name == "mosi" else orc.MOSEI
     opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
     st = M.FusedMosiStep(ours, opt, None, 64, 20)
-    A, V, T, y = orc.synthetic_batch(64, 20, seed=11)
+    A, V, T, y = orc.synthetic_batch(64, 20, seed=11, cfg=cfg)
     masks = []
     for _ in range(3):
         st.step(A.to(gpu), V.to(gpu), T.to(gpu), y.to(gpu))
-        masks.append(st.eng.keep_all.clone())
+        masks.append([k.clone() for k in st.eng.keeps])
     torch.cuda.synchronize()
-    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    pt, pc = ours.netT.dropout.p, ours.netC.dropout_p
+    for j in range(len(masks[0])):
+        assert not torch.equal(masks[0][j], masks[1][j]) and not torch.equal(masks[1][j], masks[2][j])
     for m in masks:
-        assert abs(m.float().mean().item() - 0.5) < 0.02
+        assert abs(m[0].float().mean().item() - (1 - pt)) < 0.02, "text slice rate"
+        cls = torch.cat([k.reshape(-1) for k in m[1:]]).float()
+        assert abs(cls.mean().item() - (1 - pc)) < 0.02, "classifier slice rate"
+        # independent draws: the text slice does not repeat the classifier bits at the same index
+        n = min(m[0].numel(), cls.numel())
+        agree = (m[0].reshape(-1)[:n].float() == cls[:n]).float().mean().item()
+        expect = (1 - pt) * (1 - pc) + pt * pc
+        assert abs(agree - expect) < 0.03
+
+
+def test_autograd_path_fresh_masks(gpu):
+    """The autograd-node path (torch optimizer / non-CE loss) advances its own counter: two training forwards
+    draw different masks (the host counter was never incremented)."""
+    ours = _dropin(2).to(gpu)
+    ours.train()
+    A, V, T, _ = orc.synthetic_batch(16, 12, seed=5)
+    A, V, T = (x.to(gpu) for x in (A, V, T))
+    got = []
+    for _ in range(2):
+        out = ours(A, V, T)
+        out.sum().backward()
+        eng = ours._engine(16, 12, A.device)
+        got.append([k.clone() for k in eng.keeps])
+    torch.cuda.synchronize()
+    for a, b in zip(*got):
+        assert not torch.equal(a, b)
 
 
 def test_train_step_api_fused_and_autograd(gpu):
@@ -262,10 +294,8 @@ def test_train_step_api_fused_and_autograd(gpu):
     for kind in ("fused", "autograd"):
         ours = _dropin(4).to(gpu)
         ours.netT.dropout.p = 0.0
-        for mm in ours.netC.module:
-            if isinstance(mm, torch.nn.Dropout):
-                mm.p = 0.0
-        ours.netC.dropout_p = 0.0
+        ours.netC.dropout_p = 0.0  # the property sets every classifier nn.Dropout
+        assert all(mm.p == 0.0 for mm in ours.netC.module if isinstance(mm, torch.nn.Dropout))
         opt = (tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD) if kind == "fused"
                else torch.optim.Adam(ours.parameters(), lr=LR, weight_decay=WD))
         r = ours.train_step(batch, opt, None if kind == "fused" else Group(), gpu, None)
@@ -410,3 +440,158 @@ def test_textcnn_wgrad_slab_equals_rows_kernel(gpu, B, T):
             rowsx = xx[a + dt, torch.arange(B)[:, None]]  # [B, C, F]
             ref[:, dt] += (gw[:, i * C:(i + 1) * C, None] * rowsx).sum(0)
         assert rel_l2(slab[i], ref) < 1e-6
+
+
+# ------------------------------------------------------------------------------------------------
+# BASELINE configs[4]: the seven missing-modality patterns (data/mosi.py:61-69; the YAML's validation / test
+# splits select all seven, utt_fusion_base_training.yaml:99,118) through the HIP step and validation_step
+# ------------------------------------------------------------------------------------------------
+def _corpus_from(A, V, T, y):
+    from tspm_amd.mosi_data import MosiCorpus
+    return MosiCorpus({"audio": list(A.numpy()), "video": list(V.numpy()), "text": list(T.numpy())}, y.numpy())
+
+
+def _masked(A, V, T, pattern):
+    from tspm_amd.mosi_data import pattern_keep
+    k = pattern_keep(pattern)
+    return A * k["audio"], V * k["video"], T * k["text"]
+
+
+@pytest.mark.parametrize("pattern", ["atv", "at", "av", "tv", "a", "t", "v"])
+def test_missing_pattern_step_and_eval_vs_oracle(gpu, pattern):
+    """One fused train step and one validation_step at the config's batch (128, aligned_50) with every row under
+    ``pattern``: the batch is gathered on the device with the pattern's modality mask (tspm_seq_gather, straight
+    into the step's inputs) and must equal the host-masked batch bitwise; the step is then held to the §8(c)
+    criterion against the forced-decision fp64 oracle fed the same zeroed modalities (a zeroed text makes every
+    TextCNN time-max an exact tie; a zeroed audio / video drives the LSTM by its biases alone) and Adam is checked
+    exactly; the eval logits and loss of validation_step against the fp64 oracle's validation_step."""
+    from tspm_amd.mosi_data import MOSI
+    B, S = 128, 50
+    A, V, T, y = orc.synthetic_batch(B, S, seed=777)
+    Am, Vm, Tm = _masked(A, V, T, pattern)
+    corpus = _corpus_from(A, V, T, y)
+    ours = _dropin(3).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    ds = MOSI(split="train", corpus=corpus, device=gpu, selected_patterns=[pattern])
+    b = next(iter(ds.device_loader(B, shuffle=False, step_for=lambda n, t: ours.fused_step(opt, None, n, t))))
+    st = ours.fused_step(opt, None, B, S)
+    assert b["audio"] is st.eng.A and b["pattern_name"] == [pattern] * B
+    for buf, ref in ((st.eng.A, Am), (st.eng.V, Vm), (st.eng.X, Tm)):
+        assert torch.equal(buf.transpose(0, 1).cpu(), ref)
+    keeps = orc.keep_masks(B, 61)
+    o32, o64 = pair_from(ours, lambda: orc.build_oracle_utt(3))
+    before = snapshot(ours)
+    st.keep_override = {k: v.to(gpu) for k, v in keeps.items()}
+    st.run()
+    torch.cuda.synchronize()
+    tally = Tally()
+    rep = _check_step(ours, st, o32, o64, Am, Vm, Tm, y, keeps, {"loss": st.eng.loss, "logits": st.eng.logits}, tally)
+    coef = float(st.eng.clip_coef.item())
+    _check_adam(ours, opt, before, 1, coef)
+    # validation_step on the pattern-grouped eval collate of the same rows
+    ev = MOSI(split="valid", corpus=corpus, device=gpu, selected_patterns=[pattern])
+    grouped = ev.collate_fn(ev.__getitems__(list(range(B))))
+    assert list(grouped) == [pattern]
+    v = ours.validation_step(grouped[pattern], None, gpu, None)
+    o = orc.build_oracle_utt(3)
+    o.load_state_dict({k: x.cpu() for k, x in ours.state_dict().items()})
+    r = orc.validation_step(o.double(), Am.double(), Vm.double(), Tm.double(), y)
+    check_out(f"eval logits [{pattern}]", ours._engine(B, S, gpu).logits, None, r["logits"], tally)
+    assert abs(v["loss"] - r["loss"].item()) <= 1e-4 * abs(r["loss"].item())
+    print(f"[pattern {pattern}] flips {rep} clip coef {coef:.4f}; {tally}")
+
+
+def test_mixed_pattern_eval_batch_grouped(gpu):
+    """A shuffled validation batch mixing all seven patterns: collate groups it by pattern (first-seen order,
+    data/mosi.py:236-251); every group's validation_step logits match the fp64 oracle on its masked rows, and
+    the device loader's grouped batches (gathered into FusedMosiEvalStep buffers) give the same logits."""
+    from tspm_amd.mosi_data import MOSI, PATTERNS
+    from tspm_amd.metrics import ClassificationLog
+    n = 40
+    A, V, T, y = orc.synthetic_batch(n, 30, seed=91)
+    corpus = _corpus_from(A, V, T, y)
+    ours = _dropin(5).to(gpu)
+    o = orc.build_oracle_utt(5).double()
+    ev = MOSI(split="valid", corpus=corpus, device=gpu)
+    items = torch.randperm(len(ev), generator=torch.Generator().manual_seed(3))[:128].tolist()
+    grouped = ev.collate_fn(ev.__getitems__(items))
+    seen = [PATTERNS[i // n] for i in items]
+    assert list(grouped) == list(dict.fromkeys(seen))
+    ref_logits = {}
+    for p, sub in grouped.items():
+        rows = [i % n for i in items if PATTERNS[i // n] == p]
+        Am, Vm, Tm = _masked(A[rows], V[rows], T[rows], p)
+        ours.validation_step(sub, None, gpu, None)
+        r = orc.validation_step(o, Am.double(), Vm.double(), Tm.double(), y[rows])
+        check_out(f"grouped eval [{p}]", ours._engine(len(rows), 30, gpu).logits, None, r["logits"])
+        ref_logits[p] = ours._engine(len(rows), 30, gpu).logits.clone()
+    # the same batch through the device loader into the harness's eval steps
+    from tspm_amd.harness import MosiEpochRunner
+    runner = MosiEpochRunner(ours, None, None)
+    order_ds = MOSI(split="valid", corpus=corpus, device=gpu)
+    got = {}
+    sub_items = items
+    rows_all, pid = order_ds._resolve(np.asarray(sub_items))
+    for p in dict.fromkeys(pid.tolist()):
+        sel = pid == p
+        st = runner.eval_step_for(int(sel.sum()), 30)
+        b = order_ds._collate(rows_all[sel], pid[sel], st)
+        runner._run(st, b)
+        got[PATTERNS[p]] = st.eng.logits.clone()
+    torch.cuda.synchronize()
+    for p in ref_logits:
+        assert torch.equal(got[p], ref_logits[p]), p
+    assert isinstance(runner.log, ClassificationLog)
+
+
+def test_odd_batch_step_vs_oracle(gpu):
+    """Odd batch (the last workgroup of each LSTM kernel carries one ghost row) and a short odd length."""
+    lengths = [17 - (i * 5) % 8 for i in range(33)]
+    _run_steps(gpu, 33, 17, 1.0, n_steps=2, lengths=lengths)
+
+
+def test_mosi_epoch_harness_per_pattern_metrics(gpu, tmp_path):
+    """harness.fit on UttFusionModel: training batches drawn over all seven patterns, validation / test on the
+    pattern-grouped eval loader (every group one FusedMosiEvalStep replay), metrics per pattern from device
+    confusion counts with the YAML's MSA + confusion-matrix functions.  Checked against a host replay of the
+    validation epoch through validation_step (per-group losses, softmax-argmax predictions): the epoch loss is
+    the mean of the group losses and every per-pattern metric equals the metric functions on the raw arrays."""
+    from tspm_amd import harness
+    from tspm_amd.metrics import evaluate
+    from tspm_amd.mosi_data import MOSI, PATTERNS, synthetic_mosi_corpus
+    from tspm_amd.msa_metrics import msa_binary_classification
+    from sklearn.metrics import confusion_matrix
+    ours = _dropin(8).to(gpu)
+    opt = tspm_amd.FusedAdam(ours.parameters(), lr=LR, weight_decay=WD)
+    tr = MOSI(split="train", corpus=synthetic_mosi_corpus(192, seed=1, steps=20), device=gpu, seed=4)
+    va = MOSI(split="valid", corpus=synthetic_mosi_corpus(36, seed=2, steps=20), device=gpu)
+    loaders = {"train": tr.loader(32, shuffle=True, seed=1), "validation": va.loader(32, shuffle=True, seed=9),
+               "test": va.loader(32)}
+    hist = harness.fit(ours, opt, None, loaders, epochs=2, early_stopping=False, checkpoint_dir=tmp_path / "ck",
+                       metrics_path=tmp_path / "m")
+    vm = hist["validation"][-1]
+    for p in PATTERNS:
+        assert f"MSA_Has0_Accuracy_{p.upper()}" in vm and f"ConfusionMatrix_{p.upper()}" in vm, p
+    assert np.isfinite(hist["train"][-1]["loss"]) and (tmp_path / "m" / "epoch_metrics.json").exists()
+    # host replay of the test epoch (fit loads best.pth before it): validation_step per pattern group
+    losses, preds, labels = [], {p: [] for p in PATTERNS}, {p: [] for p in PATTERNS}
+
+    class Rec:
+        def update_group_all(self, group, predictions, targets, m_types):
+            for pr, t, m in zip(predictions, targets, m_types):
+                preds[m].append(int(pr))
+                labels[m].append(int(t))
+    for b in va.device_loader(32):
+        for p, sub in b.items():
+            losses.append(ours.validation_step(sub, None, gpu, Rec())["loss"])
+    te = hist["test"]
+    assert abs(te["loss"] - float(np.mean(losses))) <= 1e-6 * abs(te["loss"])
+    for p in PATTERNS:
+        t, pr = np.asarray(labels[p]), np.asarray(preds[p])
+        conf = confusion_matrix(t, pr, labels=[0, 1, 2])
+        assert np.array_equal(np.asarray(te[f"ConfusionMatrix_{p.upper()}"]), conf), p
+        for k, val in msa_binary_classification(t, pr).items():
+            got = te[f"MSA_{k}_{p.upper()}"]
+            assert (np.isnan(val) and np.isnan(got)) or got == val, (p, k, got, val)
+        assert evaluate("metrics.msa_binary_classification", {}, conf) == msa_binary_classification(t, pr)
+    print({p: te[f"MSA_Has0_Accuracy_{p.upper()}"] for p in PATTERNS})

@@ -98,3 +98,39 @@ def test_mean_loss_is_numpy_mean_of_python_floats():
     from tspm_amd.metrics import ClassificationLog
     xs = np.random.default_rng(0).random(1000).astype(np.float32)
     assert ClassificationLog.mean_loss(xs) == np.mean([float(x) for x in xs])
+
+
+def test_mosi_recorder_matches_reference_metric_recorder():
+    """MOSI's YAML metrics (MSA = metrics.msa_binary_classification restated in tspm_amd.msa_metrics, and the
+    3-class confusion matrix) over the seven missing-modality patterns, from per-pattern confusion counts, against
+    the REAL reference MetricRecorder fed the pattern-grouped batches (tests/golden/make_mosi_metrics_golden.py)
+    — bit-exact, NaN where the reference gives NaN (a pattern with no non-neutral sample)."""
+    import math
+    from tspm_amd.metrics import DeviceMetricRecorder
+    with open(os.path.join(REPO, "tests", "golden", "mosi_metrics.json")) as f:
+        g = json.load(f)
+    pats = tuple(g["patterns"])
+    rec = DeviceMetricRecorder(g["metric_config"], _Log(confusion_by_pattern(g["batches"], pats, k=3), pats))
+    res = rec.calculate_all_groups(epoch=1, loss=0.5)["classification"]
+    assert set(res.keys()) == set(g["results"].keys())
+    for k, v in g["results"].items():
+        got = res[k]
+        if isinstance(v, list):
+            assert np.array_equal(np.asarray(got), np.asarray(v)), k
+        elif isinstance(v, float) and math.isnan(v):
+            assert math.isnan(float(got)), k
+        else:
+            assert float(got) == v, (k, got, v)
+
+
+def test_msa_metric_equals_reference_formula_on_raw_arrays():
+    """msa_binary_classification from expanded confusion counts equals the call on the raw (unsorted) arrays."""
+    from tspm_amd.metrics import evaluate
+    from tspm_amd.msa_metrics import msa_binary_classification
+    rng = np.random.default_rng(7)
+    for _ in range(8):
+        n = int(rng.integers(5, 300))
+        t, p = rng.integers(0, 3, size=n), rng.integers(0, 3, size=n)
+        conf = np.zeros((3, 3), np.int64)
+        np.add.at(conf, (t, p), 1)
+        assert evaluate("metrics.msa_binary_classification", {}, conf) == msa_binary_classification(t, p)
