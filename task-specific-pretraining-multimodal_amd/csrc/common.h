@@ -147,12 +147,15 @@ TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag, bool acquir
 // returns (in the threads with t < CB) the range's mean and sum of squared deviations in double.
 template <bool SC1 = false>  // SC1: the partials are an in-launch hand-off read with ld_sc1
 TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
-                             int c0, int CB, double* red, double* smu, double& mean_out, double& m2_out) {
+                             int c0, int CB, double* red, double* smu, double& mean_out, double& m2_out,
+                             int nthreads = 0) {
   auto ld = [](const float* p) -> float {
     if constexpr (SC1) return ld_sc1(p);
     else return *p;
   };
-  const int t = threadIdx.x, T = blockDim.x;
+  // nthreads: the threads taking part (0 = the whole workgroup); the LDS conv kernels' loader waves
+  // have left by the time their compute threads merge
+  const int t = threadIdx.x, T = nthreads > 0 ? nthreads : (int)blockDim.x;
   const int GG = T / CB, cl = t % CB, gg = t / CB;
   const int c = c0 + cl;
   const bool cok = c < C;
@@ -218,9 +221,10 @@ TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const
 // mean-K carries the rounding residual), written through (sc1) for the second-level merger.
 template <bool SC1 = false>
 TSPM_DEV void bn_merge_level1(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
-                              int c0, int CB, float* part1, int G1, int g_out, double* red, double* smu) {
+                              int c0, int CB, float* part1, int G1, int g_out, double* red, double* smu,
+                              int nthreads = 0) {
   double mean, m2;
-  bn_merge_range<SC1>(M, C, G_all, rpt, part, g_lo, g_hi, c0, CB, red, smu, mean, m2);
+  bn_merge_range<SC1>(M, C, G_all, rpt, part, g_lo, g_hi, c0, CB, red, smu, mean, m2, nthreads);
   const int t = threadIdx.x, c = c0 + t;
   if (t < CB && c < C) {
     const long long plane1 = (long long)G1 * C, o = (long long)g_out * C + c;
@@ -234,9 +238,9 @@ TSPM_DEV void bn_merge_level1(long long M, int C, int G_all, long long rpt, cons
 template <bool SC1 = false>
 TSPM_DEV void bn_merge_block(long long M, int C, int G, long long rpt, const float* part, int c0, int CB,
                              float* rmean, float* rvar, float momentum, float eps, float* smean, float* sinv,
-                             double* red, double* smu) {
+                             double* red, double* smu, int nthreads = 0) {
   double mean, m2;
-  bn_merge_range<SC1>(M, C, G, rpt, part, 0, G, c0, CB, red, smu, mean, m2);
+  bn_merge_range<SC1>(M, C, G, rpt, part, 0, G, c0, CB, red, smu, mean, m2, nthreads);
   const int cl = threadIdx.x, c = c0 + cl;
   if (cl < CB && c < C) {
     const double n = (double)M;

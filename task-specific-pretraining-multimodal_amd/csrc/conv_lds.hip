@@ -40,7 +40,40 @@ extern "C" int tspm_debug_stamps_lds_clear(void) {
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;  // compute (MFMA) threads: 4 waves, one per SIMD
+
+// Loader waves (TSPM_LOADER_WAVES, default on): 4 more waves per workgroup that only issue the LDS-DMA
+// of the operand ring.  Measured on MI355X (stamped builds, round 2): a global_load_lds blocks its wave
+// ~170 cycles at issue, and with one wave per SIMD doing both, the DMA issue path and the MFMA path of a
+// stage added up (one stage of a 32x64 tile: 0.36 + 0.45 us).  With a loader wave beside each compute
+// wave on the same SIMD, the compute wave's MFMA stream no longer stops at the DMA issues.  The loader
+// waves leave after the ring loop (s_barrier then counts only the surviving waves, as the ISA defines),
+// so the epilogues, split-K hand-offs and BN merges run on the 256 compute threads as before: results
+// are bitwise those of the single-role kernel (same MFMA order).
+// TSPM_LOADER_WAVES=2 (default): the loader waves stage through registers — full-line 16-B global loads two
+// stages ahead, then ds_write_b128 to the same LDS image the LDS-DMA would write (lane-linear per
+// 1-KiB piece) — instead of global_load_lds; =1: loader waves issuing global_load_lds; =0: one role.
+#ifndef TSPM_LOADER_WAVES
+#define TSPM_LOADER_WAVES 2
+#endif
+constexpr int kLoaderThreads = (TSPM_LOADER_WAVES == 1 || TSPM_LOADER_WAVES == 2) ? 256 : 0;
+// TSPM_LOADER_WAVES=3: no loader waves; the four compute waves stage through registers themselves (global
+// loads two stages ahead, ds_write, barrier, MFMAs): 256-thread workgroups, two LDS slots
+constexpr bool kRegStage = TSPM_LOADER_WAVES == 2 || TSPM_LOADER_WAVES == 3;
+// minimum waves per SIMD the register allocation must allow (__launch_bounds__ second argument): with
+// loader waves, 4 (two 512-thread workgroups per CU, so the two encoder streams' conv launches can share
+// CUs) for the one-block-per-wave tiles, 2 for the larger wave tiles (128 VGPRs would spill them)
+#ifndef TSPM_LDS_WAVES_SMALL
+#define TSPM_LDS_WAVES_SMALL (TSPM_LOADER_WAVES == 3 ? 2 : TSPM_LOADER_WAVES ? 4 : 1)
+#endif
+template <class C>
+constexpr int min_waves() { return C::TM * C::TN == 1 ? TSPM_LDS_WAVES_SMALL : (kLoaderThreads ? 2 : 1); }
+template <class C1, class C2>
+constexpr int min_waves2() { return min_waves<C1>() < min_waves<C2>() ? min_waves<C1>() : min_waves<C2>(); }
+constexpr int kBlock = kThreads + kLoaderThreads;
+TSPM_DEV bool is_loader_wave() {
+  return kLoaderThreads > 0 && __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= kThreads;
+}
 
 TSPM_DEV int swz(int row) { return (row >> 1) & 7; }
 
@@ -88,6 +121,7 @@ TSPM_DEV void glds16(const float* src, float* dst) {
 #endif
 template <int STAGE>
 constexpr int ring_depth() {
+  if (kRegStage) return 2;  // register staging: the loads in flight sit in registers
   int d = TSPM_RING_MAX;
   while (d > 2 && STAGE * 4 * d > TSPM_RING_BYTES) --d;
   return d;
@@ -162,6 +196,19 @@ TSPM_DEV void mma_interleaved(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C
   }
 }
 
+// One stage's MFMAs without DMA issues (compute waves when loader waves carry the DMA); same MFMA order.
+template <class C>
+TSPM_DEV void mma_plain(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM], const f32x4 (&B)[C::KGW][C::TN]) {
+#pragma unroll
+  for (int kk = 0; kk < C::KGW; ++kk)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::TN; ++b) acc.v[a][b] = mfma32(A[kk][a][j], B[kk][b][j], acc.v[a][b]);
+}
+
 // LDS-DMA ring over stages [st0, st1): C::D stage slots of C::STAGE floats.  prep(st) returns the
 // operand offsets of stage st, issue_i(off, slot, i) issues this thread's i-th of C::NI
 // global_load_lds (16 B per lane, lane-linear destination) of that stage into the slot,
@@ -172,12 +219,122 @@ TSPM_DEV void mma_interleaved(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C
 // st1-1 into slots that are never read again, so the vmcnt count is the same in every iteration.
 // Raw s_barrier, not __syncthreads(): the latter waits vmcnt(0) and would drain the ring.  Every
 // thread of the workgroup must call this with the same st0/st1; the ring is drained on return.
-template <class C, class Prep, class IssueI, class Frags>
-TSPM_DEV void ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, IssueI&& issue_i,
+// Returns true in loader waves, which must then leave the kernel (they take no part in what follows).
+// With loader waves the roles split: the loaders issue every DMA and wait for it (counted vmcnt) before
+// each stage barrier; the compute waves only pass the barriers, read fragments and multiply.
+template <class C, class Prep, class Src, class Dst, class Frags>
+TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags) {
   constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
   const int n = st1 - st0;
-  if (n <= 0) return;
+  const bool loader = is_loader_wave();
+  if (n <= 0) return loader;
+  // this thread's i-th 16-B piece of a stage: global source src_i(off, i), LDS destination dst_i(slot, i) + 4*lane
+  // (the lane-linear image one global_load_lds of the wave writes)
+  auto issue_i = [&](const Off& off, float* slot, int i) { glds16(src_i(off, i), dst_i(slot, i)); };
+  if constexpr (TSPM_LOADER_WAVES == 3) {
+    const int lane4 = (threadIdx.x & 63) * 4;
+    f32x4 R0[NI], R1[NI];
+    f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
+    auto load = [&](int st, f32x4 (&R)[NI]) {
+      const Off off = prep(st);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) R[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+    };
+    // stage it: registers -> LDS slot it % 2, barrier, fragments, MFMAs.  Slot it % 2 last held stage it-2,
+    // whose fragments every wave read before barrier it-1 (the MFMAs of it-2 consumed them).
+    auto stage = [&](int it, const f32x4 (&R)[NI]) {
+      float* slot = lds + (it & 1) * SF;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(slot, i) + lane4) = R[i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
+      frags(slot, A, B);
+    };
+    load(st0, R0);
+    if (n > 1) load(st0 + 1, R1);
+    for (int it = 0; it < n; it += 2) {
+      stage(it, R0);
+      if (it + 2 < n) load(st0 + it + 2, R0);
+      mma_plain<C>(acc, A, B);
+      if (it + 1 >= n) break;
+      stage(it + 1, R1);
+      if (it + 3 < n) load(st0 + it + 3, R1);
+      mma_plain<C>(acc, A, B);
+    }
+    __syncthreads();
+    return false;
+  }
+  if constexpr (kLoaderThreads > 0 && TSPM_LOADER_WAVES == 2) {
+    if (loader) {
+      const int lane4 = (threadIdx.x & 63) * 4;
+      f32x4 R0[NI], R1[NI];
+      auto load = [&](int st, f32x4 (&R)[NI]) {
+        const Off off = prep(st);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) R[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+      };
+      auto store = [&](int slot, const f32x4 (&R)[NI]) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + slot * SF, i) + lane4) = R[i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage is in LDS before the barrier
+        __builtin_amdgcn_s_barrier();
+      };
+      load(st0, R0);
+      if (n > 1) load(st0 + 1, R1);
+      for (int it = 0; it < n; it += 2) {  // two stages per trip: R0 / R1 indexed statically
+        store(it & 1, R0);                 // (D = 2: slot it % 2 was last read before barrier it-1)
+        if (it + 2 < n) load(st0 + it + 2, R0);
+        if (it + 1 >= n) break;
+        store((it + 1) & 1, R1);
+        if (it + 3 < n) load(st0 + it + 3, R1);
+      }
+      __builtin_amdgcn_s_barrier();
+      return true;
+    }
+    f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
+    for (int it = 0; it < n; ++it) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
+      frags(lds + (it % D) * SF, A, B);
+      mma_plain<C>(acc, A, B);
+    }
+    __builtin_amdgcn_s_barrier();
+    return false;
+  }
+  if constexpr (kLoaderThreads > 0 && TSPM_LOADER_WAVES == 1) {
+    if (loader) {
+#pragma unroll
+      for (int d = 0; d < D - 1; ++d) {
+        const Off off = prep(min(st0 + d, st1 - 1));
+#pragma unroll
+        for (int i = 0; i < NI; ++i) issue_i(off, lds + d * SF, i);
+      }
+      for (int it = 0; it < n; ++it) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * NI) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const Off off = prep(min(st0 + it + D - 1, st1 - 1));
+        float* nslot = lds + ((it + D - 1) % D) * SF;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) issue_i(off, nslot, i);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // the ring's last (re-)loads have landed: LDS is free for the epilogue
+      return true;
+    }
+    f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
+    for (int it = 0; it < n; ++it) {
+      __builtin_amdgcn_s_barrier();
+      if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
+      frags(lds + (it % D) * SF, A, B);
+      mma_plain<C>(acc, A, B);
+    }
+    __builtin_amdgcn_s_barrier();
+    return false;
+  }
 #pragma unroll
   for (int d = 0; d < D - 1; ++d) {
     const Off off = prep(min(st0 + d, st1 - 1));
@@ -196,6 +353,7 @@ TSPM_DEV void ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  return false;
 }
 
 // Combine the WK k-slices of each (wm, wn) tile through LDS, in k-slice order (deterministic).
@@ -282,7 +440,7 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 // A image: BM rows (n) x 32 channels (swizzled); B image: BN rows (output channel) x 32 channels.
 // =============================================================================================
 template <class C>
-__global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
+__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y,
                                                      tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
   extern __shared__ float lds[];
@@ -303,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   const int st0 = split_lo(T, bk.z, g.splits), st1 = split_lo(T, bk.z + 1, g.splits);
 
   constexpr int NA = C::BM / 32, NB = C::BN / 32;
-  const int wv = tid >> 6;
+  const int wv = (tid >> 6) & 3;
   const float* xa[NA];
   const float* wb[NB];
 #pragma unroll
@@ -318,7 +476,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  ring_loop<C>(
+  if (ring_loop<C>(
       acc, lds, st0, st1,
       [&](int st) -> Off {
         const int tap = st / cb, cc = (st - tap * cb) << 5;
@@ -326,9 +484,9 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
         const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
         return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
       },
-      [&](const Off& off, float* slot, int i) {
-        if (i < NA) glds16(xa[i] + off.a, slot + (i * 4 + wv) * 256);
-        else glds16(wb[i - NA] + off.b, slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256);
+      [&](const Off& off, int i) -> const float* { return i < NA ? xa[i] + off.a : wb[i - NA] + off.b; },
+      [&](float* slot, int i) -> float* {
+        return i < NA ? slot + (i * 4 + wv) * 256 : slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256;
       },
       [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
 #pragma unroll
@@ -340,7 +498,8 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
           for (int b = 0; b < C::TN; ++b)
             B[kk][b] = frag_row(img + C::BM * 32, (id.wn * C::TN + b) * 32 + (lane & 31), q);
         }
-      });
+      }))
+    return;
   TSPM_STAMP(tspm_g_stamps_lds, 2);
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
@@ -371,7 +530,8 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
       const int x0 = grp * gw, x1 = min((int)gridDim.x, x0 + gw);
       if (!last_arriver(bf.counters + gridDim.y + bk.y * ng + grp, (unsigned)(x1 - x0), flag, g.acq != 0)) return;
       float* part1 = bf.partial + 3LL * T * K;
-      bn_merge_level1<true>(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu);
+      bn_merge_level1<true>(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu,
+                            kThreads);
       if (!last_arriver(bf.counters + bk.y, (unsigned)ng, flag, g.acq != 0)) return;
       part = part1;
       G = ng;
@@ -380,7 +540,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_lds(ConvArgs g, const float* _
       return;
     }
     bn_merge_block<true>(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
-                   bf.save_mean, bf.save_invstd, red, smu);
+                   bf.save_mean, bf.save_invstd, red, smu, kThreads);
   }
 }
 
@@ -415,7 +575,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   constexpr int NA = C::BM / 32;
   constexpr int BCH = C::BN / 4;            // 16-B chunks per B row
   constexpr int NB = C::BN / 32;            // = 32 rows * BCH chunks / 256 threads
-  const int wv = tid >> 6;
+  const int wv = (tid >> 6) & 3;
   const float* da[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
@@ -431,7 +591,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  ring_loop<C>(
+  if (ring_loop<C>(
       acc, lds, st0, st1,
       [&](int st) -> Off {
         const int t = st / kb, k0 = (st - t * kb) << 5;
@@ -443,9 +603,9 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
         const int pp = (hi + g.pad - r) / g.st, qq = (wi + g.pad - s) / g.st;
         return Off{((long long)pp * g.q + qq) * N * K + k0, (long long)k0 * RSC + (r * g.s + s) * Cc};
       },
-      [&](const Off& off, float* slot, int i) {
-        if (i < NA) glds16(da[i] + off.a, slot + (i * 4 + wv) * 256);
-        else glds16(wb[i - NA] + off.b, slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256);
+      [&](const Off& off, int i) -> const float* { return i < NA ? da[i] + off.a : wb[i - NA] + off.b; },
+      [&](float* slot, int i) -> float* {
+        return i < NA ? slot + (i * 4 + wv) * 256 : slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256;
       },
       [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
 #pragma unroll
@@ -457,7 +617,8 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
           for (int b = 0; b < C::TN; ++b)
             B[kk][b] = frag_col(img + C::BM * 32, C::BN, q * 4, (id.wn * C::TN + b) * 32 + (lane & 31));
         }
-      });
+      }))
+    return;
   TSPM_STAMP(tspm_g_stamps_lds, 2);
   combine_k<C>(acc, lds, id, lane);
   TSPM_STAMP(tspm_g_stamps_lds, 3);
@@ -477,7 +638,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   TSPM_STAMP(tspm_g_stamps_lds, 5);
 }
 template <class C>
-__global__ __launch_bounds__(kThreads) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
+__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
                                                        const float* __restrict__ w, float* __restrict__ dx,
                                                        float* __restrict__ slabs) {
   extern __shared__ float lds[];
@@ -506,7 +667,7 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
 
   constexpr int ACH = C::BM / 4, BCH = C::BN / 4;
   constexpr int NA = C::BM / 32, NB = C::BN / 32;
-  const int wv = tid >> 6;
+  const int wv = (tid >> 6) & 3;
   const float* ap[NA];
   const float* bp[NB];
 #pragma unroll
@@ -523,7 +684,7 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  ring_loop<C>(
+  if (ring_loop<C>(
       acc, lds, st0, st1,
       [&](int st) -> Off {
         const int pc = st / n32, nc = st - pc * n32;
@@ -533,9 +694,9 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
         const long long xrow = ((long long)(pp * g.st - g.pad + r) * g.w + (qq * g.st - g.pad + s)) * N + nc * 32;
         return Off{mrow * K, xrow * Cc};
       },
-      [&](const Off& off, float* slot, int i) {
-        if (i < NA) glds16(ap[i] + off.a, slot + (i * 4 + wv) * 256);
-        else glds16(bp[i - NA] + off.b, slot + 32 * C::BM + ((i - NA) * 4 + wv) * 256);
+      [&](const Off& off, int i) -> const float* { return i < NA ? ap[i] + off.a : bp[i - NA] + off.b; },
+      [&](float* slot, int i) -> float* {
+        return i < NA ? slot + (i * 4 + wv) * 256 : slot + 32 * C::BM + ((i - NA) * 4 + wv) * 256;
       },
       [&](const float* img, f32x4 (&A)[C::KGW][C::TM], f32x4 (&B)[C::KGW][C::TN]) {
 #pragma unroll
@@ -547,7 +708,8 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
           for (int b = 0; b < C::TN; ++b)
             B[kk][b] = frag_col(img + 32 * C::BM, C::BN, k0, (id.wn * C::TN + b) * 32 + (lane & 31));
         }
-      });
+      }))
+    return;
   combine_k<C>(acc, lds, id, lane);
   const int row0 = co0 + id.wm * C::TM * 32, col0 = col0b + id.wn * C::TN * 32;
   if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)K * RSC, g.splits, g.cnt, row0, col0, K, RSC, RSC, lds, bk, g.acq != 0))
@@ -555,7 +717,7 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
   if (id.wk == 0 && row0 < K) acc.store(dw, row0, col0, K, RSC, RSC, lane, false);
 }
 template <class C>
-__global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float* __restrict__ x,
+__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_wgrad_lds(ConvArgs g, const float* __restrict__ x,
                                                        const float* __restrict__ dy, float* __restrict__ dw,
                                                        float* __restrict__ slabs) {
   extern __shared__ float lds[];
@@ -570,7 +732,7 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_lds(ConvArgs g, const float*
 // body is the standalone kernel's, so results are bitwise those of the two separate launches.
 // =============================================================================================
 template <class CD, class CW>
-__global__ __launch_bounds__(kThreads) void k_bwd_lds(ConvArgs gd, const float* __restrict__ dy,
+__global__ __launch_bounds__(kBlock, (min_waves2<CD, CW>())) void k_bwd_lds(ConvArgs gd, const float* __restrict__ dy,
                                                      const float* __restrict__ w, float* __restrict__ dx,
                                                      float* __restrict__ slabs_d, int dgx, int dgy, ConvArgs gw,
                                                      const float* __restrict__ x, float* __restrict__ dw,
@@ -607,7 +769,7 @@ int bn_of(const LdsAlgo& a) { return a.wn * a.tn * 32; }
 
 size_t lds_bytes(const LdsAlgo& a, bool bn_tail) {
   const size_t st1 = (size_t)(bm_of(a) + bn_of(a)) * 32 * sizeof(float);
-  int depth = TSPM_RING_MAX;  // = ring_depth<>
+  int depth = kRegStage ? 2 : TSPM_RING_MAX;  // = ring_depth<>
   while (depth > 2 && st1 * depth > TSPM_RING_BYTES) --depth;
   const size_t stage = depth * st1;
   const size_t comb = (size_t)(a.wk - 1) * a.wm * a.wn * a.tm * a.tn * 16 * 64 * sizeof(float);
@@ -754,7 +916,7 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
   }
   const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
   const size_t lds = lds_bytes(a, bf.counters != nullptr);
-#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, w, y, bf, slabs, gw, ng)
+#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;
@@ -783,7 +945,7 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
   const dim3 grid(g.m / bm_of(a), cdiv(s->c, bn_of(a)), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
   const size_t lds = lds_bytes(a, false);
-#define TSPM_DG(CFG) hipLaunchKernelGGL(k_dgrad_lds<CFG>, grid, dim3(kThreads), lds, st, g, dy, w, dx, slabs)
+#define TSPM_DG(CFG) hipLaunchKernelGGL(k_dgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, dy, w, dx, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_DG) }();
 #undef TSPM_DG
   if (rc != TSPM_OK) return rc;
@@ -806,7 +968,7 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
   const dim3 grid(cdiv(s->k, bm_of(a)), RSC / bn_of(a), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
   const size_t lds = lds_bytes(a, false);
-#define TSPM_WG(CFG) hipLaunchKernelGGL(k_wgrad_lds<CFG>, grid, dim3(kThreads), lds, st, g, x, dy, dw, slabs)
+#define TSPM_WG(CFG) hipLaunchKernelGGL(k_wgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, dy, dw, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_WG) }();
 #undef TSPM_WG
   if (rc != TSPM_OK) return rc;
@@ -827,7 +989,7 @@ struct BwdLaunch {
 template <class CD, class CW>
 void bwd_go(const BwdLaunch& L) {
   const int nblk = L.wgx * L.wgy * L.gw.splits + L.dgx * L.dgy * L.gd.splits;
-  hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kThreads), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
+  hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kBlock), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
                      L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy);
 }
 bool is_cfg(const LdsAlgo& a, int tm, int wm, int wn, int wk) {

@@ -320,7 +320,7 @@ class MosiEngine:
         """Side stream for the LSTM half of the step (it shares no buffer with the TextCNN half until the
         classifier): returns (side torch stream, its handle) after making it wait for the main stream."""
         if self.side is None:
-            self.side = torch.cuda.Stream(device=self.device)
+            self.side = L.shared_streams(self.device, 1)[0]
             self._ev = [torch.cuda.Event() for _ in range(4)]
         main = torch.cuda.current_stream(self.device)
         self._ev[0].record(main)

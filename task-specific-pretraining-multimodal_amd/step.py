@@ -128,11 +128,10 @@ class FusedTrainStep:
         self.stats = torch.zeros(4, **f32)  # loss*n, correct, n (accumulated on device)
         self.keep_override: Optional[torch.Tensor] = None
         self.nbt = shared_batches_tracked(model, dev)
-        self.side = torch.cuda.Stream(device=dev)
-        # per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in all,
-        # matching the 4 hardware queues HIP gives a process by default
-        self.aux_a = torch.cuda.Stream(device=dev)
-        self.aux_i = torch.cuda.Stream(device=dev)
+        # side stream + per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in
+        # all with the main one, matching the 4 hardware queues HIP gives a process by default; one set
+        # per process, shared by every step build (L.shared_streams)
+        self.side, self.aux_a, self.aux_i = L.shared_streams(dev, 3)
         self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
         # Off by default: measured on MI355X (ROCm 7), an eager step gains ~3 % from the auxiliary
         # streams but a replayed HIP graph with their ~50 cross-stream edges runs ~30 % SLOWER than
@@ -528,7 +527,7 @@ class FusedEvalStep:
         self.logits = torch.empty(batch, NUM_CLASSES, **f32)
         self.loss = torch.zeros(1, **f32)
         self.preds = torch.zeros(batch, dtype=torch.int64, device=dev)
-        self.side = torch.cuda.Stream(device=dev)
+        self.side = L.shared_streams(dev, 1)[0]
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self._graph_log = None
         self.calls = 0
