@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 14
+#define TSPM_ABI_VERSION 15
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -111,6 +111,24 @@ typedef struct tspm_bn_fuse {
 int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
                   const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
                   void* workspace, size_t workspace_bytes, tspm_stream_t stream);
+/* ABI 15: tspm_conv_fwd whose input is the PRE-BatchNorm output of the previous conv (BasicBlock's
+ * conv1 -> bn1 -> relu -> conv2, resnet.py:41-45): the operand loader applies relu(x * scale + shift) with
+ * scale = gamma * invstd, shift = beta - mean * scale per input channel (train-mode batch statistics —
+ * exactly tspm_bn_apply's arithmetic, so the results are bitwise those of tspm_bn_apply + tspm_conv_fwd),
+ * and writes the activation it formed to x_out (same HWNC layout as x; each element once, by the
+ * workgroups that load it as the centre tap of the first output-channel block).  Replaces one
+ * tspm_bn_apply launch and its pass over the activation.  Variant 1 (LDS-staged), stride 1, square
+ * odd kernel with pad = r / 2 only; otherwise TSPM_ERR_INVALID (the caller keeps tspm_bn_apply). */
+typedef struct tspm_bn_input {
+  const float* mean;    /* save_mean of the BatchNorm over x */
+  const float* invstd;  /* save_invstd */
+  const float* gamma;
+  const float* beta;
+  float* x_out;         /* relu(bn(x)), HWNC like x */
+} tspm_bn_input;
+int tspm_conv_fwd_bnin(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
+                       const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
+                       const tspm_bn_input* bn_in, void* workspace, size_t workspace_bytes, tspm_stream_t stream);
 int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 /* Buffer sizes that enable the two-level in-launch BN merge (tspm_bn_fuse.counters_len /
@@ -367,6 +385,16 @@ int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream);
 /* counters[i] += value for i < count (ABI 13): every BatchNorm's num_batches_tracked (one shared
  * int64 vector) advanced once per training step inside the captured step. */
 int tspm_counters_add(int64_t* counters, int64_t count, int64_t value, tspm_stream_t stream);
+
+/* Graph-external events (ABI 15) for the DP step's exchange ordering: inside a stream capture,
+ * tspm_event_record_external records `event` as an event-record NODE of the graph (hipEventRecordWithFlags
+ * with hipEventRecordExternal), so a stream outside the graph can wait (tspm_stream_wait_event) for the
+ * part of each replay before that node; outside a capture it is a plain record.  PyTorch's ROCm build
+ * refuses torch.cuda.Event(external=True), hence these four entry points.  Events: hipEventDisableTiming. */
+int tspm_event_create(void** event);
+int tspm_event_destroy(void* event);
+int tspm_event_record_external(void* event, tspm_stream_t stream);
+int tspm_stream_wait_event(tspm_stream_t stream, void* event);
 /* One fused Adam update over `count` contiguous fp32 elements (the flat parameter buffer). */
 int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    const tspm_adam_hyper* hyper, tspm_stream_t stream);

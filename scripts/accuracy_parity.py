@@ -103,6 +103,8 @@ def reference(epochs: int, seed: int, device: str = "cpu") -> None:
     tr, te = _load()
     dev = torch.device(device)
     lut = torch.from_numpy(_lut().astype(np.int64))
+    if os.environ.get("ACC_CUDNN_BENCHMARK") == "1":  # MIOpen picks kernels by timing (same math, fp32)
+        torch.backends.cudnn.benchmark = True
 
     def tensors(c, rows):
         a = torch.from_numpy(np.asarray(c.audio[rows]))
@@ -183,10 +185,16 @@ def ours(epochs: int, seed: int) -> None:
 # pretrained-encoder variant (configs/avmnist/mono/train_{audio,image}_encoder_resnet.yaml, then
 # configs/avmnist/centralised/train_avmnist_resnet_pretrained.yaml): each encoder pre-trained alone
 # (MonomodalEncoder: encoder + Linear(hidden, 10), Adam 5e-4 / 1e-4, batch 128, seed s + 100), then the
-# fusion model (seed s) with the pre-trained encoder weights and two parameter groups — encoders
-# lr 1e-4 / wd 2e-4, the rest 5e-4 / 1e-4.  Fixed epoch counts on both sides (no early stopping).
+# fusion model (seed s) with the pre-trained encoder weights.  Optimizer as the reference BUILDS it for
+# AVMNIST (``--pt-groups one``, default): train_multimodal.py:216-304 collects encoder parameters only
+# from ``image_model`` / ``audio_model`` / ``netA`` ... attributes, which AVMNIST does not have, so the
+# reference makes ONE group of all 178 parameters at lr 5e-4 / wd 1e-4 (tests/golden/plugin_resolution.json
+# records exactly that for the pretrained YAML).  ``--pt-groups two`` keeps round 2's variant (encoders
+# lr 1e-4 / wd 2e-4, the rest 5e-4 / 1e-4), which the reference never builds.  Fixed epoch counts on both
+# sides (no early stopping).
 # ------------------------------------------------------------------------------------------------
 ENC_LR, ENC_WD = 1e-4, 2e-4
+PT_GROUPS = "one"
 
 
 def _mono_order(n, modality, epoch, seed):
@@ -226,8 +234,11 @@ def pretrained_reference(mono_epochs: int, epochs: int, seed: int, device: str =
     model.image_encoder.load_state_dict(sds["image"])
     enc = list(model.audio_encoder.parameters()) + list(model.image_encoder.parameters())
     encid = {id(p) for p in enc}
-    opts = [orc.OracleAdam(enc, lr=ENC_LR, weight_decay=ENC_WD),
-            orc.OracleAdam([p for p in model.parameters() if id(p) not in encid], lr=5e-4, weight_decay=1e-4)]
+    if PT_GROUPS == "two":
+        opts = [orc.OracleAdam(enc, lr=ENC_LR, weight_decay=ENC_WD),
+                orc.OracleAdam([p for p in model.parameters() if id(p) not in encid], lr=5e-4, weight_decay=1e-4)]
+    else:  # the reference's real optimizer for AVMNIST: one group, all parameters
+        opts = [orc.OracleAdam(list(model.parameters()), lr=5e-4, weight_decay=1e-4)]
 
     class _Both:
         def step(self):
@@ -296,9 +307,12 @@ def pretrained_ours(mono_epochs: int, epochs: int, seed: int) -> None:
     model.image_encoder.load_state_dict(sds["image"])
     enc = list(model.audio_encoder.parameters()) + list(model.image_encoder.parameters())
     encid = {id(p) for p in enc}
-    opt = tspm_amd.FusedAdam([{"params": enc, "lr": ENC_LR, "weight_decay": ENC_WD},
-                              {"params": [p for p in model.parameters() if id(p) not in encid]}],
-                             lr=5e-4, weight_decay=1e-4)
+    if PT_GROUPS == "two":
+        opt = tspm_amd.FusedAdam([{"params": enc, "lr": ENC_LR, "weight_decay": ENC_WD},
+                                  {"params": [p for p in model.parameters() if id(p) not in encid]}],
+                                 lr=5e-4, weight_decay=1e-4)
+    else:
+        opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
     steps, evals, curve = {}, {}, []
     for ep in range(epochs):
         t0 = time.time()
@@ -409,7 +423,11 @@ def main() -> None:
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r2_accuracy_parity.json"))
     ap.add_argument("--threads", type=int, default=0, help="reference side: torch threads (0 = all)")
     ap.add_argument("--device", default="cpu", help="reference side: cpu (bit-exact oracle) or cuda (ATen)")
+    ap.add_argument("--pt-groups", default="one", choices=["one", "two"],
+                    help="pretrained variant: optimizer groups (one = what the reference builds for AVMNIST)")
     a = ap.parse_args()
+    global PT_GROUPS
+    PT_GROUPS = a.pt_groups
     if a.what == "prepare":
         prepare()
     elif a.what == "reference":
@@ -430,8 +448,11 @@ def main() -> None:
         compare(a.out, "pt_reference_gpu", "pt_ours",
                 "pretrained-encoder late fusion on the reference's AVMNIST files (same 24,000 / 6,000 split): each "
                 f"encoder pre-trained alone for {a.mono_epochs} epochs (MonomodalEncoder, Adam 5e-4 / 1e-4, seed s+100), "
-                "then the fusion model (seed s) with encoders at lr 1e-4 / wd 2e-4 and the head at 5e-4 / 1e-4 "
-                "(train_avmnist_resnet_pretrained.yaml param groups); same batch orders and dropout masks on both sides")
+                + ("then the fusion model (seed s) with ONE Adam group of all 178 parameters at lr 5e-4 / wd 1e-4 — the "
+                   "optimizer train_multimodal.py:216-304 builds for AVMNIST (no image_model/audio_model attributes; "
+                   "tests/golden/plugin_resolution.json)" if PT_GROUPS == "one" else
+                   "then the fusion model (seed s) with encoders at lr 1e-4 / wd 2e-4 and the head at 5e-4 / 1e-4")
+                + f" for {a.epochs} epochs; same batch orders and dropout masks on both sides")
     else:
         compare(a.out, "reference_gpu" if a.device == "cuda" else "reference")
 

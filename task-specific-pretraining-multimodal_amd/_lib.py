@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -56,6 +56,12 @@ class BnFuse(Structure):
                 ("partial_floats", c_int64)]
 
 
+class BnInput(Structure):
+    """tspm_bn_input (ABI 15): the BatchNorm + ReLU a tspm_conv_fwd_bnin applies to its input operand."""
+    _fields_ = [("mean", c_void_p), ("invstd", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
+                ("x_out", c_void_p)]
+
+
 class AdamHyper(Structure):
     _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("grad_scale", ctypes.c_double),
@@ -89,6 +95,8 @@ _SIGS = {
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
     "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, POINTER(BnFuse),
                                 _P, c_size_t, _P]),
+    "tspm_conv_fwd_bnin": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P,
+                                     POINTER(BnFuse), POINTER(BnInput), _P, c_size_t, _P]),
     "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_bn_counters": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
@@ -141,6 +149,11 @@ _SIGS = {
     "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
     "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_counters_add": (c_int32, [_P, c_int64, c_int64, _P]),
+    # ABI 15: graph-external events (the DP step's exchange ordering)
+    "tspm_event_create": (c_int32, [POINTER(c_void_p)]),
+    "tspm_event_destroy": (c_int32, [_P]),
+    "tspm_event_record_external": (c_int32, [_P, _P]),
+    "tspm_stream_wait_event": (c_int32, [_P, _P]),
     "tspm_adam_begin": (c_int32, [_P, _P]),
     "tspm_adam_step": (c_int32, [c_int64, _P, _P, _P, _P, _P, _P]),
     "tspm_image_lut": (c_int32, [c_int64, _P, _P, _P, _P]),
@@ -272,3 +285,29 @@ def counters_add(t: torch.Tensor, value: int = 1, stream: Optional[int] = None) 
         raise TspmError("counters_add: contiguous int64 device tensor")
     check(lib().tspm_counters_add(t.data_ptr(), t.numel(), int(value), stream_handle() if stream is None else stream),
           "counters_add")
+
+
+class ExternalEvent:
+    """A HIP event whose record inside a stream capture becomes an event-record NODE of the graph
+    (hipEventRecordExternal, ``tspm_event_record_external``): a stream outside the graph can wait for the
+    part of each replay that precedes the node.  (PyTorch's ROCm build refuses
+    ``torch.cuda.Event(external=True)``.)  Outside a capture, record/wait are plain event operations."""
+
+    def __init__(self):
+        h = c_void_p()
+        check(lib().tspm_event_create(ctypes.byref(h)), "event_create")
+        self.handle = h.value
+
+    def record(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        sh = stream_handle() if stream is None else stream.cuda_stream
+        check(lib().tspm_event_record_external(self.handle, sh), "event_record_external")
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Make ``stream`` (default: the current stream) wait for the last record."""
+        sh = stream_handle() if stream is None else stream.cuda_stream
+        check(lib().tspm_stream_wait_event(sh, self.handle), "stream_wait_event")
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h and _lib is not None:
+            _lib.tspm_event_destroy(h)

@@ -823,6 +823,22 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   return TSPM_OK;
 }
 
+extern "C" int tspm_conv_fwd_bnin(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
+                                  const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn,
+                                  const tspm_bn_input* bi, void* ws, size_t ws_bytes, tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !w || !y || !bi) return TSPM_ERR_INVALID;
+  if (!is_lds(user) || !tspm_detail::lds_fwd_bnin_supported(s)) return TSPM_ERR_INVALID;
+  tspm_bn_fuse bf{};
+  if (bn) {
+    bf = *bn;
+    if (!bf.partial && bf.counters) return TSPM_ERR_INVALID;
+    if (bf.counters && (!bf.save_mean || !bf.save_invstd)) return TSPM_ERR_INVALID;
+  }
+  const tspm_detail::LdsAlgo la = lds_algo(user);
+  if (!tspm_detail::lds_fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
+  return tspm_detail::lds_fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), bi);
+}
+
 extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user)) return 0;
   return tspm_detail::lds_dgrad_workspace(s, lds_algo(user));

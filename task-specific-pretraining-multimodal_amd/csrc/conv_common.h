@@ -303,7 +303,8 @@ long long lds_fwd_bn_partial_floats(const tspm_conv_shape* s, const LdsAlgo& a);
 size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
 size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st);
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi = nullptr);
+bool lds_fwd_bnin_supported(const tspm_conv_shape* s);
 int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
               void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb = nullptr);
 int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,

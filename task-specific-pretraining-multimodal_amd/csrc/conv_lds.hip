@@ -222,9 +222,31 @@ TSPM_DEV void mma_plain(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM],
 // Returns true in loader waves, which must then leave the kernel (they take no part in what follows).
 // With loader waves the roles split: the loaders issue every DMA and wait for it (counted vmcnt) before
 // each stage barrier; the compute waves only pass the barriers, read fragments and multiply.
+// Optional operand hooks (register-staging loader waves only, TSPM_LOADER_WAVES == 2; the forward's
+// BatchNorm-input prologue, tspm_conv_fwd_bnin): when `hooks` is true, the loader waves call pro() after
+// issuing the first two stages' loads and every wave passes one extra barrier before the first stage
+// (pro's LDS writes are then visible to every loader wave), and xf(st, i, v) transforms each loaded
+// 16-B piece i of stage st in registers before it is written to LDS.
+struct NoPro {
+  TSPM_DEV void operator()() const {}
+};
+struct NoXf {
+  TSPM_DEV void operator()(int, int, f32x4&) const {}
+};
+template <class C, class Prep, class Src, class Dst, class Frags>
+TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
+                        Frags&& frags);
+template <class C, class Prep, class Src, class Dst, class Frags, class Pro, class Xf>
+TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
+                          Frags&& frags, bool hooks, Pro&& pro, Xf&& xf);
 template <class C, class Prep, class Src, class Dst, class Frags>
 TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags) {
+  return ring_loop_x<C>(acc, lds, st0, st1, prep, src_i, dst_i, frags, false, NoPro{}, NoXf{});
+}
+template <class C, class Prep, class Src, class Dst, class Frags, class Pro, class Xf>
+TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
+                          Frags&& frags, bool hooks, Pro&& pro, Xf&& xf) {
   constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
   const int n = st1 - st0;
   const bool loader = is_loader_wave();
@@ -276,25 +298,35 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
 #pragma unroll
         for (int i = 0; i < NI; ++i) R[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
       };
-      auto store = [&](int slot, const f32x4 (&R)[NI]) {
+      auto store = [&](int it, f32x4 (&R)[NI]) {
+        if (hooks) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + slot * SF, i) + lane4) = R[i];
+          for (int i = 0; i < NI; ++i) xf(st0 + it, i, R[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + (it & 1) * SF, i) + lane4) = R[i];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage is in LDS before the barrier
         __builtin_amdgcn_s_barrier();
       };
       load(st0, R0);
       if (n > 1) load(st0 + 1, R1);
+      if (hooks) {
+        pro();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
       for (int it = 0; it < n; it += 2) {  // two stages per trip: R0 / R1 indexed statically
-        store(it & 1, R0);                 // (D = 2: slot it % 2 was last read before barrier it-1)
+        store(it, R0);                     // (D = 2: slot it % 2 was last read before barrier it-1)
         if (it + 2 < n) load(st0 + it + 2, R0);
         if (it + 1 >= n) break;
-        store((it + 1) & 1, R1);
+        store(it + 1, R1);
         if (it + 3 < n) load(st0 + it + 3, R1);
       }
       __builtin_amdgcn_s_barrier();
       return true;
     }
     f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
+    if (hooks) __builtin_amdgcn_s_barrier();  // the loaders' prologue barrier
     for (int it = 0; it < n; ++it) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -442,7 +474,8 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 template <class C>
 __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y,
-                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
+                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng,
+                                                     tspm_bn_input bi) {
   extern __shared__ float lds[];
   TSPM_STAMP(tspm_g_stamps_lds, 0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -476,14 +509,21 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  if (ring_loop<C>(
-      acc, lds, st0, st1,
-      [&](int st) -> Off {
-        const int tap = st / cb, cc = (st - tap * cb) << 5;
-        const int tr = tap / ns;
-        const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
-        return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
-      },
+  auto prep = [&](int st) -> Off {
+    const int tap = st / cb, cc = (st - tap * cb) << 5;
+    const int tr = tap / ns;
+    const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
+    return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
+  };
+  // BatchNorm-input prologue (tspm_conv_fwd_bnin): the loader waves form scale / shift for all Cc input
+  // channels in LDS behind the ring (tspm_bn_apply's arithmetic), then transform every activation piece
+  // in registers; the workgroups of the first output-channel block also store the centre tap's pieces
+  // (input position == output position at stride 1: every activation element exactly once) to x_out.
+  const bool bnin = bi.mean != nullptr;
+  float* tab = lds + C::D * C::STAGE;
+  const int ltid = tid - kThreads;
+  if (ring_loop_x<C>(
+      acc, lds, st0, st1, prep,
       [&](const Off& off, int i) -> const float* { return i < NA ? xa[i] + off.a : wb[i - NA] + off.b; },
       [&](float* slot, int i) -> float* {
         return i < NA ? slot + (i * 4 + wv) * 256 : slot + C::BM * 32 + ((i - NA) * 4 + wv) * 256;
@@ -498,6 +538,28 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
           for (int b = 0; b < C::TN; ++b)
             B[kk][b] = frag_row(img + C::BM * 32, (id.wn * C::TN + b) * 32 + (lane & 31), q);
         }
+      },
+      bnin,
+      [&]() {
+        for (int c4 = ltid; c4 < (Cc >> 2); c4 += kLoaderThreads) {
+          const f32x4 mu = ld4(bi.mean + 4 * c4), iv = ld4(bi.invstd + 4 * c4);
+          const f32x4 sc = ld4(bi.gamma + 4 * c4) * iv;
+          const f32x4 sf = ld4(bi.beta + 4 * c4) - mu * sc;
+          *reinterpret_cast<f32x4*>(tab + 4 * c4) = sc;
+          *reinterpret_cast<f32x4*>(tab + Cc + 4 * c4) = sf;
+        }
+      },
+      [&](int st, int i, f32x4& v) {
+        if (i >= NA) return;  // weight pieces
+        const int tap = st / cb, cc = (st - tap * cb) << 5;
+        const int row = (i * 4 + wv) * 8 + (lane >> 3);
+        const int ch = cc + (((lane & 7) ^ swz(row)) << 2);
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(tab + ch), sf = *reinterpret_cast<const f32x4*>(tab + Cc + ch);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], sc[j], sf[j]));
+        const int tr = tap / ns;
+        if (bk.y == 0 && r_lo + tr == g.pad && s_lo + (tap - tr * ns) == g.pad)
+          *reinterpret_cast<f32x4*>(bi.x_out + (xa[i] - x) + prep(st).a) = v;
       }))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 2);
@@ -888,8 +950,19 @@ size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, s->k, (long long)s->r * s->s * s->c);
 }
 
+bool lds_fwd_bnin_supported(const tspm_conv_shape* s) {
+  return TSPM_LOADER_WAVES == 2 && s->stride == 1 && s->r == s->s && (s->r & 1) && s->pad == s->r / 2 &&
+         s->p == s->h && s->q == s->w && s->c % 4 == 0;
+}
+
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi) {
+  tspm_bn_input bin{};
+  if (bi) {
+    if (!lds_fwd_bnin_supported(s) || !bi->mean || !bi->invstd || !bi->gamma || !bi->beta || !bi->x_out)
+      return TSPM_ERR_INVALID;
+    bin = *bi;
+  }
   ConvArgs g = args_of(s);
   g.m = s->p * s->q * s->n;
   g.splits = a.splits;
@@ -915,8 +988,14 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
     if (!room) bf.counters = nullptr;
   }
   const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
-  const size_t lds = lds_bytes(a, bf.counters != nullptr);
-#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
+  size_t lds = lds_bytes(a, bf.counters != nullptr);
+  if (bi) {  // scale / shift table behind the two register-staging ring slots
+    const size_t ring = (size_t)2 * (bm_of(a) + bn_of(a)) * 32 * sizeof(float);
+    lds = std::max(lds, ring + (size_t)2 * s->c * sizeof(float));
+    if (lds > 160 * 1024) return TSPM_ERR_INVALID;
+  }
+#define TSPM_FWD(CFG) \
+  hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;

@@ -676,6 +676,31 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
+extern "C" int tspm_event_create(void** event) {
+  if (!event) return TSPM_ERR_INVALID;
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return TSPM_ERR_LAUNCH;
+  *event = e;
+  return TSPM_OK;
+}
+extern "C" int tspm_event_destroy(void* event) {
+  if (!event) return TSPM_ERR_INVALID;
+  return hipEventDestroy(static_cast<hipEvent_t>(event)) == hipSuccess ? TSPM_OK : TSPM_ERR_LAUNCH;
+}
+extern "C" int tspm_event_record_external(void* event, tspm_stream_t stream) {
+  if (!event) return TSPM_ERR_INVALID;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return TSPM_ERR_LAUNCH;
+  const unsigned flags = cs == hipStreamCaptureStatusActive ? hipEventRecordExternal : 0u;
+  return hipEventRecordWithFlags(static_cast<hipEvent_t>(event), st, flags) == hipSuccess ? TSPM_OK : TSPM_ERR_LAUNCH;
+}
+extern "C" int tspm_stream_wait_event(tspm_stream_t stream, void* event) {
+  if (!event) return TSPM_ERR_INVALID;
+  return hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0) == hipSuccess
+             ? TSPM_OK : TSPM_ERR_LAUNCH;
+}
+
 extern "C" int tspm_abi_version(void) { return TSPM_ABI_VERSION; }
 
 extern "C" const char* tspm_status_string(int status) {

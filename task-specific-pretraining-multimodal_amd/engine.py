@@ -160,6 +160,11 @@ class EncoderEngine:
         # by ~5 us each (the epilogue's operand round trips sit in the split-K tail): conv 2.59 -> 2.77
         # ms, ResNet34 3x3 at 0.133 instead of 0.149 of peak, step time unchanged (2.82 ms)
         self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "0") == "1"
+        # bn1 + ReLU of every BasicBlock applied by conv2's operand loader (tspm_conv_fwd_bnin, ABI 15), which
+        # also writes the activation a1 the backward reads: one tspm_bn_apply launch (and its pass over the
+        # activation) fewer per block in the training forward; bitwise the same y2 and a1.
+        # TSPM_BN_FOLD=0 keeps the separate apply launch (A/B switch)
+        self.bn_fold = os.environ.get("TSPM_BN_FOLD", "1") != "0"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -332,17 +337,41 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
+    def _bnf(self, bn: BNOp, aux: bool = False) -> L.BnFuse:
+        m = bn.module
+        part, cnt = (self.bn_part_aux, self.bn_cnt_aux) if aux else (self.bn_part, self.bn_cnt)
+        return L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
+                        BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
+                        bn.invstd.data_ptr(), cnt.numel() if self.bn_two_level else 0, 0,
+                        part.numel() if self.bn_two_level else 0)
+
     def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
                  aux: bool = False) -> None:
         """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
         per channel block, merges them (save_mean/invstd + running statistics): one launch."""
-        m = bn.module
-        part, cnt = (self.bn_part_aux, self.bn_cnt_aux) if aux else (self.bn_part, self.bn_cnt)
-        bnf = L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
-                       BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                       bn.invstd.data_ptr(), cnt.numel() if self.bn_two_level else 0, 0,
-                       part.numel() if self.bn_two_level else 0)
-        self._conv_fwd(op, x_ptr, strides, y, sh, bnf, aux)
+        self._conv_fwd(op, x_ptr, strides, y, sh, self._bnf(bn, aux), aux)
+
+    def _can_fold(self, op: ConvOp) -> bool:
+        """conv2 of a block may take bn1 + ReLU in its operand loader (tspm_conv_fwd_bnin)."""
+        s = op.shape
+        return (self.bn_fold and not self.use_t and op.algo_fwd.variant == 1 and s.stride == 1
+                and s.r == s.s == 3 and s.pad == 1)
+
+    def _conv_bn_in(self, op: ConvOp, bn: BNOp, bn_in: BNOp, y_in: torch.Tensor, a_out: torch.Tensor,
+                    strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
+        """_conv_bn whose input operand is relu(bn_in(y_in)), formed by the loader; a_out receives it."""
+        m = bn_in.module
+        bi = L.BnInput(bn_in.mean.data_ptr(), bn_in.invstd.data_ptr(), m.weight.data_ptr(), m.bias.data_ptr(),
+                       a_out.data_ptr())
+        bnf = self._bnf(bn)
+        s, a = op.shape, op.algo_fwd
+        if self.conv_timer:
+            self.conv_timer.begin(op, "fwd")
+        L.check(L.lib().tspm_conv_fwd_bnin(ctypes.byref(s), ctypes.byref(a), y_in.data_ptr(), ctypes.byref(strides),
+                                           self._w(op).data_ptr(), y.data_ptr(), ctypes.byref(bnf), ctypes.byref(bi),
+                                           self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_fwd_bnin")
+        if self.conv_timer:
+            self.conv_timer.end()
 
     def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
                out_t: Optional[torch.Tensor] = None):
@@ -428,12 +457,15 @@ class EncoderEngine:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
                 self._conv_fwd_eval(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
-            self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train, out_t=bp.a1_t if train else None)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
-            if train:
+            if train and self._can_fold(bp.conv2):
+                self._conv_bn_in(bp.conv2, bp.bn2, bp.bn1, bp.y1, bp.a1, xs_a1, bp.y2, sh)
+            elif train:
+                self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train, out_t=bp.a1_t)
                 self._conv_bn(bp.conv2, bp.bn2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             else:
+                self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
                 self._conv_fwd_eval(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             if bp.ds_conv is not None:
                 if fork:

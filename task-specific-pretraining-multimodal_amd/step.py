@@ -198,11 +198,13 @@ class FusedTrainStep:
         linear_bwd(n, F, hd, self.fused.data_ptr(), F, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
                    g(net[0].weight).data_ptr(), g(net[0].bias).data_ptr(), self.dfused.data_ptr(), F, sh)
 
-    def _fwd_bwd(self, phase: int = 0) -> None:
+    def _fwd_bwd(self, phase: int = 0, marks=None) -> None:
         """Enqueue forward + loss + backward on the current stream (+ the side stream).  phase 0:
         everything; 1: forward, loss, head backward and the encoders' backward phase 1 (fc,
         layer4, layer3); 2: the encoders' backward phase 2 (layer2, layer1, stem) — see
-        EncoderEngine.backward and ddp.PhasedGradAllReduce."""
+        EncoderEngine.backward and ddp.PhasedGradAllReduce.  ``marks`` (phase 0 only): two external
+        events recorded after the audio / image encoder's backward phase 1 (the same launches, split
+        at the phase boundary), which the DP exchange waits on outside the graph (_run_phased)."""
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
@@ -232,12 +234,23 @@ class FusedTrainStep:
             self._classify(sh)
             self._head_bwd(sh)
         side.wait_stream(main)
-        if audio_first:
-            self.eng_a.backward(self.dfused, self.F, phase=phase)
-        with torch.cuda.stream(side):
-            self.eng_i.backward(self.dfused[:, ea:], self.F, phase=phase)
-        if not audio_first:
-            self.eng_a.backward(self.dfused, self.F, phase=phase)
+        if marks is not None:
+            ev_a, ev_i = marks
+            self.eng_a.backward(self.dfused, self.F, phase=1)
+            ev_a.record(main)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(self.dfused[:, ea:], self.F, phase=1)
+                ev_i.record(side)
+            self.eng_a.backward(None, self.F, phase=2)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(None, self.F, phase=2)
+        else:
+            if audio_first:
+                self.eng_a.backward(self.dfused, self.F, phase=phase)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(self.dfused[:, ea:], self.F, phase=phase)
+            if not audio_first:
+                self.eng_a.backward(self.dfused, self.F, phase=phase)
         main.wait_stream(side)
         if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
             main.wait_stream(self.aux_a)
@@ -285,6 +298,56 @@ class FusedTrainStep:
         L.counters_add(self.nbt)
 
     def _run_phased(self) -> None:
+        """DP step with the RCCL exchange overlapped with backward, the whole forward + backward as ONE
+        HIP graph (the plain step's two-stream schedule):
+             main (graph): [fwd both + head + head bwd + audio bwd late ─●─ audio bwd early] ─┐
+             side (graph):                               [image bwd late ─●─ image bwd early] ─┴─ wait ─ [Adam graph]
+             RCCL:                                      all-reduce(head+audio late) · (image late) · (both early)
+        ● = an external event (``_lib.ExternalEvent``: an event-record node of the graph that streams outside
+        it can wait on); the collectives run outside the graph, on RCCL's stream, each
+        after the event of the backward part that writes its gradients.  ``TSPM_PHASED=split`` keeps the
+        round-2 schedule (one graph per phase and encoder, _run_phased_split)."""
+        if os.environ.get("TSPM_PHASED", "one") == "split":
+            self._run_phased_split()
+            return
+        ar = self.allreduce
+        main = torch.cuda.current_stream()
+        comm = self.aux_a  # free in this schedule (the auxiliary conv streams are off)
+        eager = not self.use_graph or self.calls == 0
+        if getattr(self, "_marks", None) is None:
+            self._marks = (L.ExternalEvent(), L.ExternalEvent())
+        self.eng_i.fork_ds = self.eng_a.fork_ds = False
+        if eager:
+            self._fwd_bwd(marks=self._marks)
+        else:
+            if self.graph is None:
+                torch.cuda.synchronize(self.device)
+                g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._fwd_bwd(marks=self._marks)
+                with torch.cuda.graph(go):
+                    self._opt()
+                self.graph, self.graph_opt = g, go
+            self.graph.replay()
+        # the first event follows, in graph order, everything main ran before this step (batch upload,
+        # the previous step's Adam reading the gradients) — comm waits on nothing else before it
+        self._marks[0].wait(comm)
+        with torch.cuda.stream(comm):
+            w_a = ar.launch(0)
+        self._marks[1].wait(comm)
+        with torch.cuda.stream(comm):
+            w_i = ar.launch(1)
+        comm.wait_stream(main)
+        with torch.cuda.stream(comm):
+            w_e = ar.launch(2)
+        ar.wait(w_a + w_i + w_e)
+        main.wait_stream(comm)
+        if eager:
+            self._opt()
+        else:
+            self.graph_opt.replay()
+
+    def _run_phased_split(self) -> None:
         """DP step with the RCCL exchange overlapped with backward:
              main:   [fwd both + head + head bwd] ──────────────────────────── wait ─ [Adam]
              s_a:        └ [audio bwd late] ─ [audio bwd early] ─┤

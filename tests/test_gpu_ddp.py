@@ -2,15 +2,17 @@
 
 Two processes share cuda:0 and a gloo process group (gloo all-reduces device tensors through host
 copies; the driver's 8-GPU runs use RCCL with the same calls).  Each rank runs FusedTrainStep with
-``ddp.PhasedGradAllReduce`` — the overlapped exchange path bench.py uses at N > 1: per-phase HIP graphs,
-the phase-1 gradients all-reduced while phase 2 computes — on its half of a 64-sample batch, with
-FusedAdam(grad_scale = 1/2).  Checked:
+``ddp.PhasedGradAllReduce`` — the overlapped exchange path bench.py uses at N > 1: forward + backward as
+one HIP graph whose external events release the phase-1 gradients to the exchange while phase 2
+computes — on its half of a 64-sample batch, with FusedAdam(grad_scale = 1/2).  Checked:
 
 * the summed gradient buffer equals g_0 + g_1 bitwise, where g_r is rank r's gradient from a plain
   (no exchange) fused step on the same half batch;
 * fp64 Adam applied to the averaged gradient (g_0 + g_1) / 2 reproduces every rank's update;
 * both ranks hold bitwise identical parameters and Adam moments after 1 and after 4 steps (eager
-  first step, then the captured phase graphs).
+  first step, then the captured graphs);
+* on each REPLAYED step too, the exchanged gradient equals the sum of both ranks' plain-step gradients
+  for the same weights and half batches (the exchange read what this step's backward wrote).
 """
 import os
 import socket
@@ -77,18 +79,33 @@ def _worker(rank, world, port, q):
         got = fg.param.detach().cpu().double()
         ok_adam = bool(((got - exp).abs() <= 1e-6 * exp.abs() + 2e-9).all())
         state1 = torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).clone()
-        for s in range(3):  # eager done; capture + replays of the phase graphs
+        fl = o_loc.flat_groups()[0]
+        replay_sums = []
+        for s in range(3):  # eager done; capture + replays of the step graph
             a, i, lab, _ = orc.synthetic_batch(64, seed=3000 + s)
             st.keep_override = keep_full[half].to(dev)
+            p_before = fg.param.detach().clone()
             st.step(a[half].to(dev), i[half].to(dev), lab[half].to(dev))
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            # the exchanged gradient of this REPLAYED step against the two ranks' local gradients of the same
+            # weights and half batches (plain fused step): catches an exchange that ran before the graph's
+            # backward had written the gradients it reads (the external events' ordering)
+            with torch.no_grad():
+                fl.param.copy_(p_before)
+            s_loc.keep_override = keep_full[half].to(dev)
+            s_loc.step(a[half].to(dev), i[half].to(dev), lab[half].to(dev))
+            torch.cuda.synchronize()
+            gs = [torch.empty_like(fl.grad) for _ in range(world)]
+            dist.all_gather(gs, fl.grad.clone())
+            replay_sums.append(bool(torch.equal(fg.grad, gs[0] + gs[1])))
+        ok_sum = ok_sum and all(replay_sums)
         state4 = torch.cat([fg.param, fg.exp_avg, fg.exp_avg_sq]).clone()
         same = []
         for t in (state1, state4):
             other = [torch.empty_like(t) for _ in range(world)]
             dist.all_gather(other, t)
             same.append(bool(torch.equal(other[0], other[1])))
-        q.put((rank, ok_sum, ok_adam, same, st.graph is not None))
+        q.put((rank, (ok_sum, replay_sums), ok_adam, same, st.graph is not None))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - surfaced by the parent
         import traceback
@@ -110,7 +127,7 @@ def test_two_rank_phased_dp_step_on_one_gpu():
             if p.is_alive():
                 p.kill()
     for rank, ok_sum, ok_adam, same, captured in res:
-        assert ok_sum is True, (rank, ok_sum)
+        assert isinstance(ok_sum, tuple) and ok_sum[0] is True, (rank, ok_sum)
         assert ok_adam is True, rank
         assert same == [True, True], (rank, same)
         assert captured, rank

@@ -171,8 +171,8 @@ def test_graph_replay_equals_eager(gpu):
 
 
 def test_phased_allreduce_step_equals_plain_step(gpu):
-    """The DP step path — backward split in two phases, graph 1 | RCCL all-reduce of phase-1
-    gradients overlapping graph 2 | RCCL of the rest | Adam graph — under a 1-rank RCCL group
+    """The DP step path — forward + backward as one graph whose external events release the phase-1
+    gradients to the RCCL all-reduce while phase 2 runs | RCCL of the rest | Adam graph — under a 1-rank RCCL group
     (all-reduce = identity) gives bitwise the parameters of the plain fused step, eager and
     graph-replayed, and covers every parameter exactly once."""
     import os
@@ -203,6 +203,8 @@ def test_phased_allreduce_step_equals_plain_step(gpu):
                 audio, image, labels, _ = orc.synthetic_batch(32, seed=50 + i)
                 st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
             torch.cuda.synchronize()
+            if phased and os.environ.get("TSPM_PHASED", "one") != "split":  # one fwd+bwd graph + the Adam graph
+                assert isinstance(st.graph, torch.cuda.CUDAGraph) and isinstance(st.graph_opt, torch.cuda.CUDAGraph)
             bufs = [m.running_var.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)]
             results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs).cpu())
         bad = (results[0] != results[1]).nonzero().reshape(-1)
