@@ -386,15 +386,18 @@ int tspm_adam_begin(tspm_adam_hyper* hyper, tspm_stream_t stream);
  * int64 vector) advanced once per training step inside the captured step. */
 int tspm_counters_add(int64_t* counters, int64_t count, int64_t value, tspm_stream_t stream);
 
-/* Graph-external events (ABI 15) for the DP step's exchange ordering: inside a stream capture,
- * tspm_event_record_external records `event` as an event-record NODE of the graph (hipEventRecordWithFlags
- * with hipEventRecordExternal), so a stream outside the graph can wait (tspm_stream_wait_event) for the
- * part of each replay before that node; outside a capture it is a plain record.  PyTorch's ROCm build
- * refuses torch.cuda.Event(external=True), hence these four entry points.  Events: hipEventDisableTiming. */
-int tspm_event_create(void** event);
-int tspm_event_destroy(void* event);
-int tspm_event_record_external(void* event, tspm_stream_t stream);
-int tspm_stream_wait_event(tspm_stream_t stream, void* event);
+/* Step flags (ABI 15) for the DP step's exchange ordering across a graph boundary.  A flag is a device
+ * counter plus a word of coherent pinned host memory.  tspm_flag_bump enqueues a one-thread kernel that
+ * increments the counter and stores the new value to the host word (system-scope release) — capturable, so
+ * it marks a point INSIDE a captured step graph; tspm_flag_host_wait spins on the host until the word is
+ * >= value (0 = TSPM_OK; TSPM_ERR_LAUNCH after timeout_ms).  The host then launches work that depends on
+ * that point.  (ROCm 7 refuses graph-external event records; a hipStreamWaitValue64 on another stream
+ * cost 0.21 ms per step — the waiting queue stalls the graph's.) */
+typedef struct tspm_flag tspm_flag;
+int tspm_flag_create(tspm_flag** flag);
+int tspm_flag_destroy(tspm_flag* flag);
+int tspm_flag_bump(tspm_flag* flag, tspm_stream_t stream);
+int tspm_flag_host_wait(tspm_flag* flag, uint64_t value, int32_t timeout_ms);
 /* One fused Adam update over `count` contiguous fp32 elements (the flat parameter buffer). */
 int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    const tspm_adam_hyper* hyper, tspm_stream_t stream);

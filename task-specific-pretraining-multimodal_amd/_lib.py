@@ -149,11 +149,11 @@ _SIGS = {
     "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
     "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_counters_add": (c_int32, [_P, c_int64, c_int64, _P]),
-    # ABI 15: graph-external events (the DP step's exchange ordering)
-    "tspm_event_create": (c_int32, [POINTER(c_void_p)]),
-    "tspm_event_destroy": (c_int32, [_P]),
-    "tspm_event_record_external": (c_int32, [_P, _P]),
-    "tspm_stream_wait_event": (c_int32, [_P, _P]),
+    # ABI 15: step flags (the DP step's exchange ordering across the graph boundary)
+    "tspm_flag_create": (c_int32, [POINTER(c_void_p)]),
+    "tspm_flag_destroy": (c_int32, [_P]),
+    "tspm_flag_bump": (c_int32, [_P, _P]),
+    "tspm_flag_host_wait": (c_int32, [_P, ctypes.c_uint64, c_int32]),
     "tspm_adam_begin": (c_int32, [_P, _P]),
     "tspm_adam_step": (c_int32, [c_int64, _P, _P, _P, _P, _P, _P]),
     "tspm_image_lut": (c_int32, [c_int64, _P, _P, _P, _P]),
@@ -287,27 +287,26 @@ def counters_add(t: torch.Tensor, value: int = 1, stream: Optional[int] = None) 
           "counters_add")
 
 
-class ExternalEvent:
-    """A HIP event whose record inside a stream capture becomes an event-record NODE of the graph
-    (hipEventRecordExternal, ``tspm_event_record_external``): a stream outside the graph can wait for the
-    part of each replay that precedes the node.  (PyTorch's ROCm build refuses
-    ``torch.cuda.Event(external=True)``.)  Outside a capture, record/wait are plain event operations."""
+class DeviceFlag:
+    """A point inside a captured step graph the HOST can wait for: ``bump`` enqueues a one-thread kernel
+    (+1 on a device counter, the new value stored to a coherent pinned host word); ``host_wait(v)`` spins
+    (GIL released, in C) until the word reaches ``v``.  ROCm 7 refuses graph-external event records, the
+    CUDA idiom, and a stream waiting on the word (hipStreamWaitValue64) stalled the graph's queues."""
 
     def __init__(self):
         h = c_void_p()
-        check(lib().tspm_event_create(ctypes.byref(h)), "event_create")
+        check(lib().tspm_flag_create(ctypes.byref(h)), "flag_create")
         self.handle = h.value
+        self.count = 0  # executions of the bump enqueued so far (host bookkeeping)
 
-    def record(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+    def bump(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         sh = stream_handle() if stream is None else stream.cuda_stream
-        check(lib().tspm_event_record_external(self.handle, sh), "event_record_external")
+        check(lib().tspm_flag_bump(self.handle, sh), "flag_bump")
 
-    def wait(self, stream: Optional[torch.cuda.Stream] = None) -> None:
-        """Make ``stream`` (default: the current stream) wait for the last record."""
-        sh = stream_handle() if stream is None else stream.cuda_stream
-        check(lib().tspm_stream_wait_event(sh, self.handle), "stream_wait_event")
+    def host_wait(self, value: int, timeout_ms: int = 60000) -> None:
+        check(lib().tspm_flag_host_wait(self.handle, int(value), int(timeout_ms)), "flag_host_wait (timeout)")
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
         if h and _lib is not None:
-            _lib.tspm_event_destroy(h)
+            _lib.tspm_flag_destroy(h)

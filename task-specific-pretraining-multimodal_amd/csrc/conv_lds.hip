@@ -119,6 +119,18 @@ TSPM_DEV void glds16(const float* src, float* dst) {
 #ifndef TSPM_RING_BYTES
 #define TSPM_RING_BYTES (64 * 1024)
 #endif
+// register-staged operand stages in flight per loader thread (TSPM_LOADER_WAVES == 2).  Measured in the
+// batch-128 step (A/B, 2 runs each, same box): 2 stages 2.684-2.691 ms (2.697-2.706 with the previous loop,
+// which drained every load at each trip), 3 stages 2.677-2.681, 4 stages (3 for the large tiles)
+// 2.705-2.707; TSPM_REG_STAGES overrides (A/B builds)
+template <int NI>
+constexpr int reg_stages() {
+#ifdef TSPM_REG_STAGES
+  return TSPM_REG_STAGES;
+#else
+  return 3;
+#endif
+}
 template <int STAGE>
 constexpr int ring_depth() {
   if (kRegStage) return 2;  // register staging: the loads in flight sit in registers
@@ -223,30 +235,35 @@ TSPM_DEV void mma_plain(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM],
 // With loader waves the roles split: the loaders issue every DMA and wait for it (counted vmcnt) before
 // each stage barrier; the compute waves only pass the barriers, read fragments and multiply.
 // Optional operand hooks (register-staging loader waves only, TSPM_LOADER_WAVES == 2; the forward's
-// BatchNorm-input prologue, tspm_conv_fwd_bnin): when `hooks` is true, the loader waves call pro() after
-// issuing the first two stages' loads and every wave passes one extra barrier before the first stage
-// (pro's LDS writes are then visible to every loader wave), and xf(st, i, v) transforms each loaded
-// 16-B piece i of stage st in registers before it is written to LDS.
-struct NoPro {
+// BatchNorm-input prologue, tspm_conv_fwd_bnin).  With HOOKS the loader waves call pro_issue() before
+// the first two stages' loads (its global loads are then ahead of them in the vmcnt order), pro_finish()
+// after them (it waits only for its own loads) and every wave passes one extra barrier before the first
+// stage (pro_finish's LDS writes are then visible to every loader wave); xfp(st, i, S, H) reads piece i's
+// per-stage constants from LDS when the stage's loads are issued, and xfa(st, i, v, S, H) transforms the
+// first NXF loaded 16-B pieces of stage st in registers before they are written to LDS — so neither adds
+// a memory or LDS round trip to the loader's store of a stage.
+struct NoHook {
   TSPM_DEV void operator()() const {}
-};
-struct NoXf {
-  TSPM_DEV void operator()(int, int, f32x4&) const {}
+  TSPM_DEV void operator()(int, int, f32x4&, f32x4&) const {}
+  TSPM_DEV void operator()(int, int, f32x4&, const f32x4&, const f32x4&) const {}
 };
 template <class C, class Prep, class Src, class Dst, class Frags>
 TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags);
-template <class C, class Prep, class Src, class Dst, class Frags, class Pro, class Xf>
+template <class C, bool HOOKS, int NXF, class Prep, class Src, class Dst, class Frags, class PI, class PF, class XP,
+          class XA>
 TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
-                          Frags&& frags, bool hooks, Pro&& pro, Xf&& xf);
+                          Frags&& frags, PI&& pro_issue, PF&& pro_finish, XP&& xfp, XA&& xfa);
 template <class C, class Prep, class Src, class Dst, class Frags>
 TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags) {
-  return ring_loop_x<C>(acc, lds, st0, st1, prep, src_i, dst_i, frags, false, NoPro{}, NoXf{});
+  return ring_loop_x<C, false, 0>(acc, lds, st0, st1, prep, src_i, dst_i, frags, NoHook{}, NoHook{}, NoHook{},
+                                  NoHook{});
 }
-template <class C, class Prep, class Src, class Dst, class Frags, class Pro, class Xf>
+template <class C, bool HOOKS, int NXF, class Prep, class Src, class Dst, class Frags, class PI, class PF, class XP,
+          class XA>
 TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
-                          Frags&& frags, bool hooks, Pro&& pro, Xf&& xf) {
+                          Frags&& frags, PI&& pro_issue, PF&& pro_finish, XP&& xfp, XA&& xfa) {
   constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
   const int n = st1 - st0;
   const bool loader = is_loader_wave();
@@ -292,41 +309,71 @@ TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, 
   if constexpr (kLoaderThreads > 0 && TSPM_LOADER_WAVES == 2) {
     if (loader) {
       const int lane4 = (threadIdx.x & 63) * 4;
-      f32x4 R0[NI], R1[NI];
-      auto load = [&](int st, f32x4 (&R)[NI]) {
+      // RS stages of operand loads in flight in registers (two LDS slots): a stage's loads are issued RS
+      // stages before its LDS write, which covers more of the memory latency than two stages of MFMA work
+      constexpr int RS = reg_stages<NI>();
+      f32x4 R[RS][NI];
+      constexpr int NX = NXF > 0 ? NXF : 1;
+      f32x4 S[RS][NX], H[RS][NX];  // per-piece transform constants (HOOKS only)
+      auto load = [&](int st, f32x4 (&Rb)[NI]) {
         const Off off = prep(st);
 #pragma unroll
-        for (int i = 0; i < NI; ++i) R[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+        for (int i = 0; i < NI; ++i) Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
       };
-      auto store = [&](int it, f32x4 (&R)[NI]) {
-        if (hooks) {
+      auto consts = [&](int st, f32x4 (&Sb)[NX], f32x4 (&Hb)[NX]) {
+        if constexpr (HOOKS) {
 #pragma unroll
-          for (int i = 0; i < NI; ++i) xf(st0 + it, i, R[i]);
+          for (int i = 0; i < NXF; ++i) xfp(st, i, Sb[i], Hb[i]);
+        }
+      };
+      auto store = [&](int it, f32x4 (&Rb)[NI], const f32x4 (&Sb)[NX], const f32x4 (&Hb)[NX]) {
+        if constexpr (HOOKS) {
+#pragma unroll
+          for (int i = 0; i < NXF; ++i) xfa(st0 + it, i, Rb[i], Sb[i], Hb[i]);
         }
 #pragma unroll
-        for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + (it & 1) * SF, i) + lane4) = R[i];
+        for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + (it & 1) * SF, i) + lane4) = Rb[i];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage is in LDS before the barrier
         __builtin_amdgcn_s_barrier();
       };
-      load(st0, R0);
-      if (n > 1) load(st0 + 1, R1);
-      if (hooks) {
-        pro();
+      // Every load group is issued unconditionally (past the end the loader re-loads stage st1-1 into
+      // buffers that are never stored), so the vmcnt scoreboard is the same on every path through the
+      // loop: the compiler's wait before a stage's LDS write is then vmcnt((RS-1)*NI) — the RS-1 later
+      // stages stay in flight.  (With the loads conditional it merged the paths conservatively and
+      // drained ALL loads at every trip: one exposed memory latency per trip.)
+      const int last = st1 - 1;
+      if constexpr (HOOKS) pro_issue();
+#pragma unroll
+      for (int j = 0; j < RS; ++j) load(min(st0 + j, last), R[j]);
+      if constexpr (HOOKS) {
+        pro_finish();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int j = 0; j < RS; ++j) consts(min(st0 + j, last), S[j], H[j]);
       }
-      for (int it = 0; it < n; it += 2) {  // two stages per trip: R0 / R1 indexed statically
-        store(it, R0);                     // (D = 2: slot it % 2 was last read before barrier it-1)
-        if (it + 2 < n) load(st0 + it + 2, R0);
-        if (it + 1 >= n) break;
-        store(it + 1, R1);
-        if (it + 3 < n) load(st0 + it + 3, R1);
+      // RS stages per trip, buffers indexed statically; (D = 2: slot it % 2 was last read before barrier it-1).
+      // Full trips are one basic block (each buffer keeps its registers across the back-edge — a copy of a
+      // buffer whose loads are in flight would force a wait for them), the last partial trip stores only.
+      int it = 0;
+      for (; it + RS <= n; it += RS) {
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          store(it + j, R[j], S[j], H[j]);
+          const int nx = min(st0 + it + j + RS, last);
+          load(nx, R[j]);
+          consts(nx, S[j], H[j]);
+        }
       }
+#pragma unroll
+      for (int j = 0; j < RS - 1; ++j)
+        if (it + j < n) store(it + j, R[j], S[j], H[j]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       return true;
     }
     f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
-    if (hooks) __builtin_amdgcn_s_barrier();  // the loaders' prologue barrier
+    if constexpr (HOOKS) __builtin_amdgcn_s_barrier();  // the loaders' prologue barrier
     for (int it = 0; it < n; ++it) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -471,7 +518,7 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 // Forward: y[(p,q,n), k] = sum_{valid (r,s), c} x[(p*st-pad+r, q*st-pad+s, n), c] w[k, r, s, c]
 // A image: BM rows (n) x 32 channels (swizzled); B image: BN rows (output channel) x 32 channels.
 // =============================================================================================
-template <class C>
+template <class C, bool BNIN = false>
 __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y,
                                                      tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng,
@@ -515,14 +562,15 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
     const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
     return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
   };
-  // BatchNorm-input prologue (tspm_conv_fwd_bnin): the loader waves form scale / shift for all Cc input
-  // channels in LDS behind the ring (tspm_bn_apply's arithmetic), then transform every activation piece
-  // in registers; the workgroups of the first output-channel block also store the centre tap's pieces
-  // (input position == output position at stride 1: every activation element exactly once) to x_out.
-  const bool bnin = bi.mean != nullptr;
+  // BatchNorm-input prologue (tspm_conv_fwd_bnin, BNIN): the loader waves form scale / shift for all Cc
+  // input channels in LDS behind the ring (tspm_bn_apply's arithmetic: one loader thread per 4 channels),
+  // then transform every activation piece in registers; the workgroups of the first output-channel block
+  // also store the centre tap's pieces (input position == output position at stride 1: every activation
+  // element exactly once) to x_out.
   float* tab = lds + C::D * C::STAGE;
-  const int ltid = tid - kThreads;
-  if (ring_loop_x<C>(
+  const int c4 = tid - kThreads;
+  f32x4 t_mu, t_iv, t_g, t_b;
+  if (ring_loop_x<C, BNIN, NA>(
       acc, lds, st0, st1, prep,
       [&](const Off& off, int i) -> const float* { return i < NA ? xa[i] + off.a : wb[i - NA] + off.b; },
       [&](float* slot, int i) -> float* {
@@ -539,25 +587,42 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
             B[kk][b] = frag_row(img + C::BM * 32, (id.wn * C::TN + b) * 32 + (lane & 31), q);
         }
       },
-      bnin,
       [&]() {
-        for (int c4 = ltid; c4 < (Cc >> 2); c4 += kLoaderThreads) {
-          const f32x4 mu = ld4(bi.mean + 4 * c4), iv = ld4(bi.invstd + 4 * c4);
-          const f32x4 sc = ld4(bi.gamma + 4 * c4) * iv;
-          const f32x4 sf = ld4(bi.beta + 4 * c4) - mu * sc;
+        if (c4 < (Cc >> 2)) {
+          t_mu = ld4(bi.mean + 4 * c4);
+          t_iv = ld4(bi.invstd + 4 * c4);
+          t_g = ld4(bi.gamma + 4 * c4);
+          t_b = ld4(bi.beta + 4 * c4);
+        }
+      },
+      [&]() {
+        if (c4 < (Cc >> 2)) {
+          const f32x4 sc = t_g * t_iv;
+          const f32x4 sf = t_b - t_mu * sc;
           *reinterpret_cast<f32x4*>(tab + 4 * c4) = sc;
           *reinterpret_cast<f32x4*>(tab + Cc + 4 * c4) = sf;
         }
       },
-      [&](int st, int i, f32x4& v) {
-        if (i >= NA) return;  // weight pieces
-        const int tap = st / cb, cc = (st - tap * cb) << 5;
+      [&](int st, int i, f32x4& S, f32x4& H) {
+#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 3  // diagnostic builds only: which part of the hook costs
+        return;
+#endif
+        const int cc = (st % cb) << 5;
         const int row = (i * 4 + wv) * 8 + (lane >> 3);
         const int ch = cc + (((lane & 7) ^ swz(row)) << 2);
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(tab + ch), sf = *reinterpret_cast<const f32x4*>(tab + Cc + ch);
+        S = *reinterpret_cast<const f32x4*>(tab + ch);
+        H = *reinterpret_cast<const f32x4*>(tab + Cc + ch);
+      },
+      [&](int st, int i, f32x4& v, const f32x4& S, const f32x4& H) {
+#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 2
+        return;
+#endif
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], sc[j], sf[j]));
-        const int tr = tap / ns;
+        for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], S[j], H[j]));
+#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 1
+        return;
+#endif
+        const int tap = st / cb, tr = tap / ns;
         if (bk.y == 0 && r_lo + tr == g.pad && s_lo + (tap - tr * ns) == g.pad)
           *reinterpret_cast<f32x4*>(bi.x_out + (xa[i] - x) + prep(st).a) = v;
       }))
@@ -952,7 +1017,7 @@ size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
 
 bool lds_fwd_bnin_supported(const tspm_conv_shape* s) {
   return TSPM_LOADER_WAVES == 2 && s->stride == 1 && s->r == s->s && (s->r & 1) && s->pad == s->r / 2 &&
-         s->p == s->h && s->q == s->w && s->c % 4 == 0;
+         s->p == s->h && s->q == s->w && s->c % 4 == 0 && s->c <= 4 * kLoaderThreads;
 }
 
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
@@ -994,8 +1059,9 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
     lds = std::max(lds, ring + (size_t)2 * s->c * sizeof(float));
     if (lds > 160 * 1024) return TSPM_ERR_INVALID;
   }
-#define TSPM_FWD(CFG) \
-  hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin)
+#define TSPM_FWD(CFG)                                                                                         \
+  if (bi) hipLaunchKernelGGL((k_fwd_lds<CFG, true>), grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin); \
+  else hipLaunchKernelGGL((k_fwd_lds<CFG, false>), grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;

@@ -1,3 +1,5 @@
+#include <chrono>
+#include <cstdio>
 // Fusion head (Linear/ReLU/Dropout, MML_Suite/models/avmnist.py:219-230,267), encoder fc
 // (resnet.py:150,217), cross-entropy (experiment_utils/loss.py:123-148), Adam (torch.optim.Adam as
 // built at config/optimizer_config.py:199-226) and the image colormap LUT (data/avmnist.py:186-191).
@@ -676,29 +678,56 @@ extern "C" int tspm_image_lut(int64_t count, const uint8_t* u8, const uint8_t* l
   return TSPM_OK;
 }
 
-extern "C" int tspm_event_create(void** event) {
-  if (!event) return TSPM_ERR_INVALID;
-  hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return TSPM_ERR_LAUNCH;
-  *event = e;
+struct tspm_flag {
+  unsigned long long* dev;   // device counter (only the bump kernel touches it)
+  unsigned long long* host;  // coherent pinned host word the bump kernel publishes to
+};
+namespace {
+__global__ void k_flag_bump(unsigned long long* dev, unsigned long long* host) {
+  const unsigned long long v = dev[0] + 1;
+  dev[0] = v;
+  __hip_atomic_store(host, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+extern "C" int tspm_flag_create(tspm_flag** flag) {
+  if (!flag) return TSPM_ERR_INVALID;
+  tspm_flag* f = new tspm_flag{nullptr, nullptr};
+  if (hipMalloc(&f->dev, 64) != hipSuccess || hipMemset(f->dev, 0, 64) != hipSuccess ||
+      hipHostMalloc(&f->host, 64, hipHostMallocCoherent) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    if (f->dev) (void)hipFree(f->dev);
+    if (f->host) (void)hipHostFree(f->host);
+    delete f;
+    return TSPM_ERR_LAUNCH;
+  }
+  __atomic_store_n(f->host, 0ull, __ATOMIC_SEQ_CST);
+  *flag = f;
   return TSPM_OK;
 }
-extern "C" int tspm_event_destroy(void* event) {
-  if (!event) return TSPM_ERR_INVALID;
-  return hipEventDestroy(static_cast<hipEvent_t>(event)) == hipSuccess ? TSPM_OK : TSPM_ERR_LAUNCH;
+extern "C" int tspm_flag_destroy(tspm_flag* f) {
+  if (!f) return TSPM_ERR_INVALID;
+  (void)hipFree(f->dev);
+  (void)hipHostFree(f->host);
+  delete f;
+  return TSPM_OK;
 }
-extern "C" int tspm_event_record_external(void* event, tspm_stream_t stream) {
-  if (!event) return TSPM_ERR_INVALID;
-  const hipStream_t st = static_cast<hipStream_t>(stream);
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return TSPM_ERR_LAUNCH;
-  const unsigned flags = cs == hipStreamCaptureStatusActive ? hipEventRecordExternal : 0u;
-  return hipEventRecordWithFlags(static_cast<hipEvent_t>(event), st, flags) == hipSuccess ? TSPM_OK : TSPM_ERR_LAUNCH;
+extern "C" int tspm_flag_bump(tspm_flag* f, tspm_stream_t stream) {
+  if (!f) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_flag_bump, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), f->dev, f->host);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
 }
-extern "C" int tspm_stream_wait_event(tspm_stream_t stream, void* event) {
-  if (!event) return TSPM_ERR_INVALID;
-  return hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0) == hipSuccess
-             ? TSPM_OK : TSPM_ERR_LAUNCH;
+extern "C" int tspm_flag_host_wait(tspm_flag* f, uint64_t value, int32_t timeout_ms) {
+  if (!f) return TSPM_ERR_INVALID;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    if (__atomic_load_n(f->host, __ATOMIC_ACQUIRE) >= value) return TSPM_OK;
+    if ((spin & 1023) == 1023) {
+      const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
+      if (ms.count() > timeout_ms) return TSPM_ERR_LAUNCH;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 extern "C" int tspm_abi_version(void) { return TSPM_ABI_VERSION; }

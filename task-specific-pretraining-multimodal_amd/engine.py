@@ -162,9 +162,11 @@ class EncoderEngine:
         self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "0") == "1"
         # bn1 + ReLU of every BasicBlock applied by conv2's operand loader (tspm_conv_fwd_bnin, ABI 15), which
         # also writes the activation a1 the backward reads: one tspm_bn_apply launch (and its pass over the
-        # activation) fewer per block in the training forward; bitwise the same y2 and a1.
-        # TSPM_BN_FOLD=0 keeps the separate apply launch (A/B switch)
-        self.bn_fold = os.environ.get("TSPM_BN_FOLD", "1") != "0"
+        # activation) fewer per block in the training forward; bitwise the same y2 and a1 (tested).  Opt-in
+        # (TSPM_BN_FOLD=1): measured at batch 128 the BN family drops 1.03 -> 0.94 ms of device time and
+        # 21 launches, but each folded conv2 grows by 2-5 us (image) and 4-15 us (audio) — the transform
+        # sits in the loader waves' per-stage path — so the step is slower (2.73 vs 2.70 ms)
+        self.bn_fold = os.environ.get("TSPM_BN_FOLD", "0") == "1"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)

@@ -202,9 +202,9 @@ class FusedTrainStep:
         """Enqueue forward + loss + backward on the current stream (+ the side stream).  phase 0:
         everything; 1: forward, loss, head backward and the encoders' backward phase 1 (fc,
         layer4, layer3); 2: the encoders' backward phase 2 (layer2, layer1, stem) — see
-        EncoderEngine.backward and ddp.PhasedGradAllReduce.  ``marks`` (phase 0 only): two external
-        events recorded after the audio / image encoder's backward phase 1 (the same launches, split
-        at the phase boundary), which the DP exchange waits on outside the graph (_run_phased)."""
+        EncoderEngine.backward and ddp.PhasedGradAllReduce.  ``marks`` (phase 0 only): two
+        ``_lib.DeviceFlag``s bumped after the audio / image encoder's backward phase 1 (the same launches,
+        split at the phase boundary), which the DP exchange waits on outside the graph (_run_phased)."""
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
@@ -235,12 +235,12 @@ class FusedTrainStep:
             self._head_bwd(sh)
         side.wait_stream(main)
         if marks is not None:
-            ev_a, ev_i = marks
+            mark_a, mark_i = marks
             self.eng_a.backward(self.dfused, self.F, phase=1)
-            ev_a.record(main)
+            mark_a.bump(main)
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F, phase=1)
-                ev_i.record(side)
+                mark_i.bump(side)
             self.eng_a.backward(None, self.F, phase=2)
             with torch.cuda.stream(side):
                 self.eng_i.backward(None, self.F, phase=2)
@@ -303,8 +303,9 @@ class FusedTrainStep:
              main (graph): [fwd both + head + head bwd + audio bwd late ─●─ audio bwd early] ─┐
              side (graph):                               [image bwd late ─●─ image bwd early] ─┴─ wait ─ [Adam graph]
              RCCL:                                      all-reduce(head+audio late) · (image late) · (both early)
-        ● = an external event (``_lib.ExternalEvent``: an event-record node of the graph that streams outside
-        it can wait on); the collectives run outside the graph, on RCCL's stream, each
+        ● = a step flag (``_lib.DeviceFlag``: a one-thread kernel in the graph publishes a per-step count to
+        pinned host memory; the host waits for it before launching the collective — ROCm 7 refuses
+        graph-external event records); the collectives run outside the graph, on RCCL's stream, each
         after the event of the backward part that writes its gradients.  ``TSPM_PHASED=split`` keeps the
         round-2 schedule (one graph per phase and encoder, _run_phased_split)."""
         if os.environ.get("TSPM_PHASED", "one") == "split":
@@ -315,8 +316,11 @@ class FusedTrainStep:
         comm = self.aux_a  # free in this schedule (the auxiliary conv streams are off)
         eager = not self.use_graph or self.calls == 0
         if getattr(self, "_marks", None) is None:
-            self._marks = (L.ExternalEvent(), L.ExternalEvent())
+            self._marks = (L.DeviceFlag(), L.DeviceFlag())
         self.eng_i.fork_ds = self.eng_a.fork_ds = False
+        # diagnostics for the structure's cost with no exchange (inactive all-reduce only): "nowait" skips
+        # the flag waits / stream hops, "inline" also keeps Adam inside the step graph
+        diag = os.environ.get("TSPM_PHASED_DIAG", "") if not ar.active() else ""
         if eager:
             self._fwd_bwd(marks=self._marks)
         else:
@@ -325,16 +329,29 @@ class FusedTrainStep:
                 g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._fwd_bwd(marks=self._marks)
+                    if diag == "inline":
+                        self._opt()
                 with torch.cuda.graph(go):
                     self._opt()
                 self.graph, self.graph_opt = g, go
             self.graph.replay()
-        # the first event follows, in graph order, everything main ran before this step (batch upload,
-        # the previous step's Adam reading the gradients) — comm waits on nothing else before it
-        self._marks[0].wait(comm)
+        if diag in ("nowait", "inline"):
+            for f in self._marks:
+                f.count += 1
+            if diag == "nowait":
+                self.graph_opt.replay() if not eager else self._opt()
+            elif eager:
+                self._opt()
+            return
+        # each flag is bumped once per step, after (in graph order) everything main ran before this step
+        # (batch upload, the previous step's Adam reading the gradients): once the host has seen it, the
+        # gradients it covers are complete, so the exchange launched then needs no device-side wait
+        for f in self._marks:
+            f.count += 1
+        self._marks[0].host_wait(self._marks[0].count)
         with torch.cuda.stream(comm):
             w_a = ar.launch(0)
-        self._marks[1].wait(comm)
+        self._marks[1].host_wait(self._marks[1].count)
         with torch.cuda.stream(comm):
             w_i = ar.launch(1)
         comm.wait_stream(main)
