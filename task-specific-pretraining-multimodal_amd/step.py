@@ -354,11 +354,8 @@ class FusedTrainStep:
         self._marks[1].host_wait(self._marks[1].count)
         with torch.cuda.stream(comm):
             w_i = ar.launch(1)
-        comm.wait_stream(main)
-        with torch.cuda.stream(comm):
-            w_e = ar.launch(2)
+        w_e = ar.launch(2)  # on main, behind the graph: no stream hop before the last exchange
         ar.wait(w_a + w_i + w_e)
-        main.wait_stream(comm)
         if eager:
             self._opt()
         else:
