@@ -67,7 +67,11 @@ typedef struct tspm_conv_shape {
  *   wk waves split every 32-deep reduction stage; splits: split-K over workgroups for fwd, dgrad
  *   and wgrad (fp32 slabs in the workspace, reduced in slab order in-launch).  tm, tn in {1,2}.
  *   Needs HWNC operands, n % (wm*tm*32) == 0 (fwd/dgrad), c % 32 == 0 (fwd), k % 32 == 0 (dgrad),
- *   n % 32 == 0 and c % (wn*tn*32) == 0 (wgrad); otherwise the call returns TSPM_ERR_INVALID. */
+ *   n % 32 == 0 and c % (wn*tn*32) == 0 (wgrad); otherwise the call returns TSPM_ERR_INVALID.
+ *   The workgroup also carries 4 loader waves that stage each operand stage through registers (3 stages
+ *   of loads in flight) into two LDS slots.
+ * variant 2 — the same tiles and rules with single-role waves: the 4 waves issue the operand loads
+ *   themselves as LDS-DMA into a 2-4-slot ring (faster for the batch-256 / 1024 grids; ABI 15). */
 typedef struct tspm_conv_algo {
   int32_t tm, tn, wn, wk, splits;
   int32_t variant;

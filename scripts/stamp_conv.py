@@ -66,7 +66,7 @@ def report(lib, kind, key, s, xs, b, algo):
             assert f() == 0
         torch.cuda.synchronize()
         buf = np.zeros((1 << 18) * SLOTS, dtype=np.uint64)
-        lds_variant = len(algo) > 5 and algo[5] == 1
+        lds_variant = len(algo) > 5 and algo[5] in (1, 2)
         assert (lib.tspm_debug_stamps_lds_clear if lds_variant else lib.tspm_debug_stamps_clear)() == 0
         torch.cuda.synchronize()
         assert f() == 0

@@ -743,8 +743,12 @@ Algo wgrad_algo(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   return pick(user, s->k, cols, iters, true);
 }
 
-// variant 1 (LDS-staged, conv_lds.hip): wm = 4 / (wn * wk)
-bool is_lds(const tspm_conv_algo* user) { return user && user->variant == 1; }
+// variants 1 and 2 (LDS-staged, conv_lds.hip: register-staged loader waves / single-role LDS-DMA ring):
+// wm = 4 / (wn * wk)
+bool is_lds(const tspm_conv_algo* user) { return user && (user->variant == 1 || user->variant == 2); }
+const tspm_detail::LdsImpl& lds_of(const tspm_conv_algo* user) {
+  return user->variant == 2 ? tspm_detail::lds_impl_dma() : tspm_detail::lds_impl_reg();
+}
 tspm_detail::LdsAlgo lds_algo(const tspm_conv_algo* u) {
   tspm_detail::LdsAlgo a{u->tm, u->tn, 0, u->wn, u->wk, u->splits > 0 ? u->splits : 1};
   const int wnk = a.wn * a.wk;
@@ -757,7 +761,7 @@ tspm_detail::LdsAlgo lds_algo(const tspm_conv_algo* u) {
 // ---------------------------------------------------------------------------------------------
 extern "C" size_t tspm_conv_fwd_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user)) return 0;  // register-direct: in-workgroup split-K only
-  return tspm_detail::lds_fwd_workspace(s, lds_algo(user));
+  return lds_of(user).fwd_workspace(s, lds_algo(user));
 }
 
 extern "C" int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
@@ -774,12 +778,12 @@ extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_
 extern "C" int32_t tspm_conv_fwd_bn_counters(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
   const int single = cdiv(s->k, 32);
-  return is_lds(user) ? std::max(single, tspm_detail::lds_fwd_bn_counters(s, lds_algo(user))) : single;
+  return is_lds(user) ? std::max(single, lds_of(user).fwd_bn_counters(s, lds_algo(user))) : single;
 }
 
 extern "C" int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
-  if (is_lds(user)) return tspm_detail::lds_fwd_bn_partial_floats(s, lds_algo(user));
+  if (is_lds(user)) return lds_of(user).fwd_bn_partial_floats(s, lds_algo(user));
   return 3LL * tspm_conv_fwd_tiles(s, user) * s->k;
 }
 
@@ -795,8 +799,8 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   }
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
-    if (!tspm_detail::lds_fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
-    return tspm_detail::lds_fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream));
+    if (!lds_of(user).fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
+    return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), nullptr);
   }
   (void)ws; (void)ws_bytes;
   Algo al = fwd_algo(s, user);
@@ -827,7 +831,7 @@ extern "C" int tspm_conv_fwd_bnin(const tspm_conv_shape* s, const tspm_conv_algo
                                   const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn,
                                   const tspm_bn_input* bi, void* ws, size_t ws_bytes, tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !w || !y || !bi) return TSPM_ERR_INVALID;
-  if (!is_lds(user) || !tspm_detail::lds_fwd_bnin_supported(s)) return TSPM_ERR_INVALID;
+  if (!is_lds(user) || !lds_of(user).fwd_bnin_supported(s)) return TSPM_ERR_INVALID;
   tspm_bn_fuse bf{};
   if (bn) {
     bf = *bn;
@@ -835,13 +839,13 @@ extern "C" int tspm_conv_fwd_bnin(const tspm_conv_shape* s, const tspm_conv_algo
     if (bf.counters && (!bf.save_mean || !bf.save_invstd)) return TSPM_ERR_INVALID;
   }
   const tspm_detail::LdsAlgo la = lds_algo(user);
-  if (!tspm_detail::lds_fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
-  return tspm_detail::lds_fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), bi);
+  if (!lds_of(user).fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
+  return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), bi);
 }
 
 extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user)) return 0;
-  return tspm_detail::lds_dgrad_workspace(s, lds_algo(user));
+  return lds_of(user).dgrad_workspace(s, lds_algo(user));
 }
 
 extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* dy,
@@ -850,8 +854,8 @@ extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   if (!shape_ok(s) || !dy || !w || !dx) return TSPM_ERR_INVALID;
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
-    if (!tspm_detail::lds_dgrad_supported(s, la)) return TSPM_ERR_INVALID;
-    return tspm_detail::lds_dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream));
+    if (!lds_of(user).dgrad_supported(s, la)) return TSPM_ERR_INVALID;
+    return lds_of(user).dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), nullptr);
   }
   (void)ws; (void)ws_bytes;
   if (s->k % 8 != 0) return TSPM_ERR_INVALID;
@@ -870,7 +874,7 @@ extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
 
 extern "C" size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
-  if (is_lds(user)) return tspm_detail::lds_wgrad_workspace(s, lds_algo(user));
+  if (is_lds(user)) return lds_of(user).wgrad_workspace(s, lds_algo(user));
   Algo al = wgrad_algo(s, user);
   if (al.splits <= 1) return 0;
   return TSPM_COUNTER_BYTES + (size_t)al.splits * s->k * s->r * s->s * s->c * sizeof(float);
@@ -882,8 +886,8 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   if (!shape_ok(s) || !x || !dy || !dw) return TSPM_ERR_INVALID;
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
-    if (!tspm_detail::lds_wgrad_supported(s, xs, la)) return TSPM_ERR_INVALID;
-    return tspm_detail::lds_wgrad(s, la, x, dy, dw, ws, ws_bytes, static_cast<hipStream_t>(stream));
+    if (!lds_of(user).wgrad_supported(s, xs, la)) return TSPM_ERR_INVALID;
+    return lds_of(user).wgrad(s, la, x, dy, dw, ws, ws_bytes, static_cast<hipStream_t>(stream));
   }
   Algo al = wgrad_algo(s, user);
   if (!algo_supported(al)) return TSPM_ERR_INVALID;
@@ -917,10 +921,10 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
 
 extern "C" int32_t tspm_conv_bwd_supported(const tspm_conv_shape* s, const tspm_conv_algo* dg,
                                           const tspm_conv_algo* wg, const tspm_strides4* xs) {
-  if (!shape_ok(s) || !is_lds(dg) || !is_lds(wg)) return 0;
+  if (!shape_ok(s) || !is_lds(dg) || !is_lds(wg) || dg->variant != wg->variant) return 0;
   const tspm_detail::LdsAlgo ad = lds_algo(dg), aw = lds_algo(wg);
-  return (tspm_detail::lds_dgrad_supported(s, ad) && tspm_detail::lds_wgrad_supported(s, xs, aw) &&
-          tspm_detail::lds_bwd_built(ad, aw)) ? 1 : 0;
+  const tspm_detail::LdsImpl& v = lds_of(dg);
+  return (v.dgrad_supported(s, ad) && v.wgrad_supported(s, xs, aw) && v.bwd_built(ad, aw)) ? 1 : 0;
 }
 
 extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
@@ -929,16 +933,16 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
                              tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
-  return tspm_detail::lds_bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w,
-                              ws_w_bytes, static_cast<hipStream_t>(stream));
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w, ws_w_bytes,
+                        static_cast<hipStream_t>(stream), nullptr);
 }
 
 // ---- dgrad epilogue with BatchNorm-backward partial sums (ABI 13, variant 1 only) --------------
 extern "C" int32_t tspm_conv_dgrad_bn_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user) || s->c % 32 != 0) return 0;  // whole 32-channel fragments
   const tspm_detail::LdsAlgo la = lds_algo(user);
-  if (!tspm_detail::lds_dgrad_supported(s, la)) return 0;
-  return tspm_detail::lds_dgrad_tiles(s, la);
+  if (!lds_of(user).dgrad_supported(s, la)) return 0;
+  return lds_of(user).dgrad_tiles(s, la);
 }
 
 static bool bnb_of(const tspm_conv_shape* s, const tspm_conv_algo* user, const tspm_bn_bwd_fuse* f, BnbFuse& out) {
@@ -957,7 +961,7 @@ extern "C" int tspm_conv_dgrad_bnfuse(const tspm_conv_shape* s, const tspm_conv_
   BnbFuse b;
   if (!bnb_of(s, user, bn, b)) return TSPM_ERR_INVALID;
   const tspm_detail::LdsAlgo la = lds_algo(user);
-  return tspm_detail::lds_dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), &b);
+  return lds_of(user).dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), &b);
 }
 
 extern "C" int tspm_conv_bwd_bnfuse(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
@@ -968,8 +972,8 @@ extern "C" int tspm_conv_bwd_bnfuse(const tspm_conv_shape* s, const tspm_conv_al
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   BnbFuse b;
   if (!bnb_of(s, dg, bn, b)) return TSPM_ERR_INVALID;
-  return tspm_detail::lds_bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w,
-                              ws_w_bytes, static_cast<hipStream_t>(stream), &b);
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w, ws_w_bytes,
+                        static_cast<hipStream_t>(stream), &b);
 }
 
 extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x_t, int64_t ldx,

@@ -294,24 +294,31 @@ namespace tspm_detail {
 struct LdsAlgo {
   int tm, tn, wm, wn, wk, splits;
 };
-bool lds_fwd_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
-bool lds_dgrad_supported(const tspm_conv_shape* s, const LdsAlgo& a);
-bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
-size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
-int lds_fwd_bn_counters(const tspm_conv_shape* s, const LdsAlgo& a);
-long long lds_fwd_bn_partial_floats(const tspm_conv_shape* s, const LdsAlgo& a);
-size_t lds_dgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
-size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a);
-int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi = nullptr);
-bool lds_fwd_bnin_supported(const tspm_conv_shape* s);
-int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
-              void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb = nullptr);
-int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
-              size_t ws_bytes, hipStream_t st);
-bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw);
-int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
-            const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-            hipStream_t st, const BnbFuse* bnb = nullptr);
-int lds_dgrad_tiles(const tspm_conv_shape* s, const LdsAlgo& a);
+// The LDS-staged kernels (conv_lds.hip) are built twice, with different operand loaders, and reached through
+// these tables: variant 1 = register-staged loader waves (lds_impl_reg), variant 2 = single-role waves with
+// an LDS-DMA ring (lds_impl_dma, built with TSPM_LOADER_WAVES=0).
+struct LdsImpl {
+  bool (*fwd_supported)(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
+  bool (*dgrad_supported)(const tspm_conv_shape* s, const LdsAlgo& a);
+  bool (*wgrad_supported)(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a);
+  size_t (*fwd_workspace)(const tspm_conv_shape* s, const LdsAlgo& a);
+  int (*fwd_bn_counters)(const tspm_conv_shape* s, const LdsAlgo& a);
+  long long (*fwd_bn_partial_floats)(const tspm_conv_shape* s, const LdsAlgo& a);
+  size_t (*dgrad_workspace)(const tspm_conv_shape* s, const LdsAlgo& a);
+  size_t (*wgrad_workspace)(const tspm_conv_shape* s, const LdsAlgo& a);
+  int (*fwd)(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
+             const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi);
+  bool (*fwd_bnin_supported)(const tspm_conv_shape* s);
+  int (*dgrad)(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
+               void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb);
+  int (*wgrad)(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
+               size_t ws_bytes, hipStream_t st);
+  bool (*bwd_built)(const LdsAlgo& ad, const LdsAlgo& aw);
+  int (*bwd)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+             const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
+             hipStream_t st, const BnbFuse* bnb);
+  int (*dgrad_tiles)(const tspm_conv_shape* s, const LdsAlgo& a);
+};
+const LdsImpl& lds_impl_reg();
+const LdsImpl& lds_impl_dma();
 }  // namespace tspm_detail

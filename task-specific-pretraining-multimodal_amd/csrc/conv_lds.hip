@@ -25,7 +25,16 @@
 // of non-padding taps is uniform per workgroup and padding taps are skipped, not multiplied.
 #include "conv_common.h"
 
-#ifdef TSPM_STAMPS
+// This file is compiled twice (Makefile): as is (variant 1, register-staged loader waves) and with
+// TSPM_LOADER_WAVES=0 TSPM_LDS_NS=tspm_lds_dma TSPM_LDS_IMPL=lds_impl_dma TSPM_LDS_SECONDARY (variant 2).
+#ifndef TSPM_LDS_NS
+#define TSPM_LDS_NS tspm_lds_reg
+#endif
+#ifndef TSPM_LDS_IMPL
+#define TSPM_LDS_IMPL lds_impl_reg
+#endif
+
+#if defined(TSPM_STAMPS) && !defined(TSPM_LDS_SECONDARY)
 __device__ unsigned long long tspm_g_stamps_lds[TSPM_STAMP_WAVES * TSPM_STAMP_SLOTS];
 extern "C" int tspm_debug_stamps_lds(void* host_dst, size_t bytes) {
   if (bytes > sizeof(tspm_g_stamps_lds)) bytes = sizeof(tspm_g_stamps_lds);
@@ -978,7 +987,8 @@ BnLevels bn_levels(const tspm_conv_shape* s, const LdsAlgo& a) {
 
 }  // namespace
 
-namespace tspm_detail {
+namespace TSPM_LDS_NS {
+using tspm_detail::LdsAlgo;
 
 bool lds_fwd_supported(const tspm_conv_shape* s, const tspm_strides4* xs, const LdsAlgo& a) {
   if (!algo_ok(a) || !hwnc(s, xs)) return false;
@@ -1208,4 +1218,15 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
   return TSPM_OK;
 }
 
+}  // namespace TSPM_LDS_NS
+
+namespace tspm_detail {
+const LdsImpl& TSPM_LDS_IMPL() {
+  namespace v = TSPM_LDS_NS;
+  static const LdsImpl t{&v::lds_fwd_supported, &v::lds_dgrad_supported, &v::lds_wgrad_supported,
+                         &v::lds_fwd_workspace, &v::lds_fwd_bn_counters, &v::lds_fwd_bn_partial_floats,
+                         &v::lds_dgrad_workspace, &v::lds_wgrad_workspace, &v::lds_fwd, &v::lds_fwd_bnin_supported,
+                         &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd, &v::lds_dgrad_tiles};
+  return t;
+}
 }  // namespace tspm_detail

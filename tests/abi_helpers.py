@@ -152,7 +152,7 @@ def lds_supported(kind: str, case, algo) -> bool:
     """Mirror of the variant-1 (LDS-staged) support rules in include/tspm.h."""
     n, c, h, w, k, r, s, st, pad = case
     tm, tn, wn, wk, sp = algo[:5]
-    if len(algo) < 6 or algo[5] != 1:
+    if len(algo) < 6 or algo[5] not in (1, 2):
         return True
     if wn * wk == 0 or 4 % (wn * wk):
         return False

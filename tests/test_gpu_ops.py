@@ -40,7 +40,9 @@ ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1,
 # variant 1 (LDS-staged): (tm, tn, wn, wk, splits, 1) with wm = 4 / (wn*wk); every (wm, wn, wk) wave
 # arrangement, both tile sizes and split-K over workgroups
 LDS_ALGOS = [(1, 1, 1, 1, 1, 1), (1, 1, 2, 1, 1, 1), (1, 1, 4, 1, 1, 1), (2, 2, 2, 1, 1, 1), (1, 1, 1, 4, 1, 1),
-             (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 2, 1, 1, 2, 1)]
+             (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 2, 1, 1, 2, 1),
+             # variant 2: the same kernels with single-role waves and an LDS-DMA ring (the batch-256 / 1024 tables)
+             (1, 1, 2, 1, 1, 2), (2, 1, 1, 4, 2, 2), (1, 1, 2, 2, 5, 2), (2, 2, 1, 1, 2, 2)]
 
 
 def _check(out, ref, bound, what):
