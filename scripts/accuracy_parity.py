@@ -376,8 +376,12 @@ def compare(out_path: str, ref_side: str = "reference", our_side: str = "ours", 
         d = 100 * (np.asarray(a) - np.asarray(b))
         m, se = float(d.mean()), float(d.std(ddof=1) / np.sqrt(len(d)))
         t = float(stats.t.ppf(0.95, len(d) - 1))
+        sd = float(d.std(ddof=1))
+        # paired runs the TOST would need to resolve at this spread and mean difference (z approximation)
+        need = int(np.ceil((1.645 * sd / (0.2 - abs(m))) ** 2)) if abs(m) < 0.2 else None
         return {"ci90_pp": [round(m - t * se, 3), round(m + t * se, 3)],
-                "equivalent_at_0.2pp": bool(m - t * se > -0.2 and m + t * se < 0.2)}
+                "equivalent_at_0.2pp": bool(m - t * se > -0.2 and m + t * se < 0.2),
+                "paired_sd_pp": round(sd, 3), "runs_needed_at_observed_sd_and_delta": need}
     last = rows[-1]
     fin_o, fin_r = last["ours_test_accuracy"], last["reference_test_accuracy"]
     t3 = lambda c, s: float(np.mean([c[s][k]["test_accuracy"] for k in range(n - 3, n)]))  # noqa: E731
