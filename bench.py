@@ -21,6 +21,7 @@ import argparse
 import json
 import os
 import re
+import subprocess
 import sys
 import time
 
@@ -315,7 +316,7 @@ def mmimdb_bench(args) -> None:
                         "traffic_unit": "HBM bytes per step, all kernels (PMC: 2 x FETCH_SIZE + WRITE_SIZE; batch 256)",
                         "traffic_source": traffic_src,
                         "flop_per_sample": fps, "adam_bytes_per_step": 28 * nparam},
-           "final_loss": round(st.eng.loss.item(), 5)}
+           "final_loss": round(st.eng.loss.item(), 5), "process_group": process_group_info()}
     if not args.no_cpu_baseline and rank == 0:
         from oracle.avmnist_ref import OracleAdam
         threads, hcpu = cpu_threads()
@@ -783,7 +784,7 @@ def mosi_bench(args) -> None:
                                   f"clip {cfg.clip}, Adam)",
                       "per_rank_batch": B, "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
                       "params": sum(p.numel() for p in model.parameters())},
-           "roofline": roof, "final_loss": round(st.eng.loss.item(), 5)}
+           "roofline": roof, "final_loss": round(st.eng.loss.item(), 5), "process_group": process_group_info()}
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         from oracle import mosi_ref as mref
         from oracle.avmnist_ref import OracleAdam
@@ -810,6 +811,13 @@ def mosi_bench(args) -> None:
         dist.destroy_process_group()
 
 
+def process_group_info():
+    """Backend and world size as the initialised process group reports them (None at N=1 without one)."""
+    if not dist.is_initialized():
+        return None
+    return {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(), "rank": dist.get_rank()}
+
+
 _JSON_FD = None
 
 
@@ -831,6 +839,99 @@ def emit(obj) -> None:
         sys.stdout.flush()
     else:
         os.write(_JSON_FD, line)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` (N > 1) started as a plain process: this parent makes NO GPU call (it only counts
+    nothing, binds a port and waits) and starts N child processes of this same script, one per GPU, with
+    the torchrun-style env (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free
+    MASTER_PORT) — children, not an exec of this process.  It forwards rank 0's ONE JSON line (with
+    ``launch`` added) and exits non-zero, after stopping the others, as soon as any child fails."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # rank 0's stdout carries the JSON line; the other ranks' stdout joins this process's stderr
+        out = subprocess.PIPE if r == 0 else sys.stderr.fileno()
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out))
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.poll() not in (None, 0):
+                failed = (r, p.returncode)
+                break
+        time.sleep(0.2)
+    if failed is None:
+        bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
+        failed = bad[0] if bad else None
+    if failed is not None:
+        for p in procs:  # the exact PIDs this process started
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        print(f"bench.py: rank {failed[0]} exited with status {failed[1]}", file=sys.stderr)
+        return failed[1] or 1
+    lines = [ln for ln in procs[0].stdout.read().decode().splitlines() if ln.strip().startswith("{")]
+    if len(lines) != 1:
+        print(f"bench.py: rank 0 printed {len(lines)} JSON lines, expected 1", file=sys.stderr)
+        return 1
+    res = json.loads(lines[0])
+    res["launch"] = {"mode": "spawned by bench.py --gpus (one child process per GPU)", "ranks": n}
+    emit(res)
+    return 0
+
+
+def check_world(gpus: int) -> None:
+    """Refuse a launch whose torchrun world disagrees with --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (launch one rank per GPU)")
+
+
+def dry_run(args) -> None:
+    """--dry-run: the multi-rank plumbing without a GPU — the same launch (torchrun env or spawn_ranks),
+    process group (gloo), barrier-bracketed timed region, max over ranks and rank-0 JSON line as the
+    real bench, with an empty step.  Every rank reports (rank, pid, world size of the process group)."""
+    from tspm_amd import ddp
+    rank, world, _ = ddp.init_from_env("gloo")
+    B = args.batch_per_rank
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    el = max(time.perf_counter() - t0, 1e-9)
+    me = torch.tensor([rank, os.getpid(), dist.get_world_size() if dist.is_initialized() else 1, el],
+                      dtype=torch.float64)
+    allr = [torch.zeros_like(me) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(allr, me)
+    else:
+        allr = [me]
+    el = max(float(t[3]) for t in allr)
+    if rank == 0:
+        emit({"metric": METRIC, "value": round(world * B * args.steps / el, 2), "unit": "samples/sec",
+              "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+              "process_group_world_size": int(allr[0][2]),
+              "ranks": [{"rank": int(t[0]), "pid": int(t[1]), "pg_world_size": int(t[2])} for t in allr],
+              "config": {"per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"}})
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def main() -> None:
@@ -868,7 +969,17 @@ def main() -> None:
     ap.add_argument("--pcie-steps", type=int, default=20,
                     help="steps of the secondary PCIe-inclusive measurement (0: skip)")
     ap.add_argument("--kernel-table", default=None, help="write the per-launch conv durations (JSON) here")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="multi-rank plumbing only (gloo, no GPU, empty step): launch, barriers, max over ranks")
     args = ap.parse_args()
+    check_world(args.gpus)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.input_stage or args.eval or args.mono:
+            raise SystemExit("bench.py: --input-stage / --eval / --mono are single-GPU benches")
+        sys.exit(spawn_ranks(args.gpus))
+    if args.dry_run:
+        dry_run(args)
+        return
     if args.input_stage:
         input_stage_bench(args)
         return
@@ -1057,6 +1168,7 @@ def main() -> None:
             "roofline": rl,
             "pcie_inclusive": pcie,
             "final_loss": round(loss, 5),
+            "process_group": process_group_info(),
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(B, args.cpu_budget)

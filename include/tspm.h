@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 15
+#define TSPM_ABI_VERSION 16
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -372,6 +372,38 @@ int tspm_dropout_mask(int64_t count, float p, uint64_t seed, const uint64_t* cou
  * if stats != NULL: stats[0] += loss*n, stats[1] += #correct (argmax == label), stats[2] += n. */
 int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const int64_t* labels, float* loss,
                        float* dlogits, float grad_scale, float* stats, tspm_stream_t stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Fusion head train step (ABI 16) — AVMNIST's classifier `net` = Linear(in, hidden) → ReLU →
+ * Dropout(p) → Linear(hidden, hidden2) → ReLU → Linear(hidden2, classes) (models/avmnist.py:219-230,
+ * forward :267), the LossFunctionGroup's weighted cross-entropy (experiment_utils/loss.py:98-148) and
+ * the head's whole backward, in TWO launches instead of ten:
+ *   (1) row blocks of 8 samples per workgroup: dropout keep mask (same counter-hash bits as
+ *       tspm_dropout_mask, or read from `keep` when gen_keep == 0), h1, hh, logits, per-row CE,
+ *       dlogits, dz3 = (dlogits @ w5) * (hh > 0), dz0 = (dz3 @ w3) * (h1 > 0 ? 1/(1-p) : 0) and
+ *       dx = dz0 @ w0 (the gradient flowing into the two encoders' embeddings);
+ *   (2) the three weight / bias gradients (dw = dz^T @ input, db = column sums; overwritten) on the
+ *       small-GEMM tiles, plus one workgroup that reduces the per-row losses in a fixed order:
+ *       loss[0] = weight * mean CE, stats[0] += sum CE, stats[1] += #(argmax == label), stats[2] += n.
+ * Every buffer below is caller-owned device memory; row_ws holds 2*n floats.  Same semantics as
+ * tspm_linear_fwd/_bwd + tspm_act_bwd + tspm_dropout_mask + tspm_cross_entropy (out-of-range label →
+ * NaN loss and gradients), up to summation order.  Limits: in <= 256, hidden <= 256, hidden2 <= 128,
+ * classes <= 16; in, hidden, hidden2 multiples of 4; w0 / w3 / x rows 16-byte aligned. */
+typedef struct tspm_head_desc {
+  int32_t n, in, hidden, hidden2, classes, ldx, lddx, gen_keep;
+  const float* x;                  /* [n, ldx] the fused embeddings (concat of the two encoders) */
+  const float *w0, *b0, *w3, *b3, *w5, *b5;
+  float p;                         /* dropout probability (0: no mask) */
+  float loss_weight;               /* the cross-entropy term's weight */
+  uint64_t seed;
+  const uint64_t* counter;         /* device step counter (fresh masks per graph replay) */
+  uint8_t* keep;                   /* [n, hidden] */
+  const int64_t* labels;           /* [n] */
+  float *h1, *hh, *logits, *dlogits, *dz3, *dz0, *dx, *row_ws;
+  float *gw0, *gb0, *gw3, *gb3, *gw5, *gb5;
+  float *loss, *stats;             /* stats nullable */
+} tspm_head_desc;
+int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Adam — torch.optim.Adam (L2 weight decay folded into the gradient) as instantiated by

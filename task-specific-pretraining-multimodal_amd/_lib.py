@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 15
+ABI_VERSION = 16
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -74,6 +74,15 @@ class LinearBwdDesc(Structure):
     """tspm_linear_bwd_desc: one Linear's backward for tspm_linear_bwd_multi."""
     _fields_ = [(n, c_int32) for n in ("n", "in_", "out", "ldx", "ldy", "lddx")] + \
                [(n, c_void_p) for n in ("x", "dy", "w", "dw", "db", "dx")]
+
+
+class HeadDesc(Structure):
+    """tspm_head_desc (ABI 16): the AVMNIST fusion head's train step in two launches."""
+    _fields_ = [(n, c_int32) for n in ("n", "in_", "hidden", "hidden2", "classes", "ldx", "lddx", "gen_keep")] + \
+        [(n, c_void_p) for n in ("x", "w0", "b0", "w3", "b3", "w5", "b5")] + \
+        [("p", c_float), ("loss_weight", c_float), ("seed", c_uint64)] + \
+        [(n, c_void_p) for n in ("counter", "keep", "labels", "h1", "hh", "logits", "dlogits", "dz3", "dz0", "dx",
+                                 "row_ws", "gw0", "gb0", "gw3", "gb3", "gw5", "gb5", "loss", "stats")]
 
 
 # name -> (restype, argtypes)
@@ -149,6 +158,8 @@ _SIGS = {
     "tspm_dropout_mask": (c_int32, [c_int64, c_float, c_uint64, _P, _P, _P]),
     "tspm_cross_entropy": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_counters_add": (c_int32, [_P, c_int64, c_int64, _P]),
+    # ABI 16: the fusion head's train step (fwd + CE + bwd) in two launches
+    "tspm_head_train_step": (c_int32, [POINTER(HeadDesc), _P]),
     # ABI 15: step flags (the DP step's exchange ordering across the graph boundary)
     "tspm_flag_create": (c_int32, [POINTER(c_void_p)]),
     "tspm_flag_destroy": (c_int32, [_P]),

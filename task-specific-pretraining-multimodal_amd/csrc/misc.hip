@@ -741,3 +741,275 @@ extern "C" const char* tspm_status_string(int status) {
     default: return "unknown status";
   }
 }
+
+namespace {
+
+// ---- fusion head train step (tspm_head_train_step) ---------------------------------------------------
+// Launch 1: one workgroup per HEAD_RB samples runs the head's whole row-local chain on data in LDS:
+//   h1 = relu(x w0^T + b0) * keep/(1-p),  hh = relu(h1 w3^T + b3),  logits = hh w5^T + b5,  CE per row,
+//   dlogits,  dz3 = (dlogits w5) * (hh > 0),  dz0 = (dz3 w3) * (h1 > 0 ? 1/(1-p) : 0),  dx = dz0 w0.
+// Every product is row-block x weight with <= 256 outputs per row, so a thread owns one output column
+// for RPT rows: the weight column is read once per thread (16-byte loads along a weight row for the
+// forward products; consecutive columns across lanes for the transposed backward products) and the row
+// values are LDS broadcasts.  Launch 2 (k_head_wgrad): the weight gradients on the small-GEMM tiles +
+// one workgroup reducing the per-row losses in row order.
+constexpr int HEAD_RB = 8;
+constexpr int HEAD_MAXIN = 256, HEAD_MAXH = 256, HEAD_MAXH2 = 128, HEAD_MAXC = 16;
+
+struct HeadArgs {
+  tspm_head_desc d;
+  float scale;  // 1/(1-p), or 1
+};
+
+// Y[r][o] = sum_k X[r][k] W[o][k] (W global [O][K], K % 4 == 0, rows 16-byte aligned; X in LDS, ld ldx)
+// for rows [0, RB) in groups of RPT rows; epi(r, o, acc) consumes each result.
+template <int RPT, class Epi>
+TSPM_DEV void head_xwT(const float* X, int ldx, const float* __restrict__ W, int K, int O, Epi epi) {
+  constexpr int G = HEAD_RB / RPT;
+  for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
+    const int o = item % O, rg = item / O;
+    const float* wp = W + (long long)o * K;
+    const float* xp = X + rg * RPT * ldx;
+    float acc[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+    for (int k = 0; k < K; k += 4) {
+      const f32x4 w = ld4(wp + k);
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const f32x4 x = ld4(xp + r * ldx + k);
+        acc[r] = fmaf(x[0], w[0], acc[r]);
+        acc[r] = fmaf(x[1], w[1], acc[r]);
+        acc[r] = fmaf(x[2], w[2], acc[r]);
+        acc[r] = fmaf(x[3], w[3], acc[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) epi(rg * RPT + r, o, acc[r]);
+  }
+}
+
+// Y[r][o] = sum_k X[r][k] W[k][o] (W global [K][O]: consecutive o across lanes), rows in groups of RPT.
+template <int RPT, class Epi>
+TSPM_DEV void head_xW(const float* X, int ldx, const float* __restrict__ W, int K, int O, Epi epi) {
+  constexpr int G = HEAD_RB / RPT;
+  for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
+    const int o = item % O, rg = item / O;
+    const float* xp = X + rg * RPT * ldx;
+    float acc[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+    int k = 0;
+    for (; k + 4 <= K; k += 4) {
+      float w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = W[(long long)(k + j) * O + o];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const f32x4 x = ld4(xp + r * ldx + k);
+        acc[r] = fmaf(x[0], w[0], acc[r]);
+        acc[r] = fmaf(x[1], w[1], acc[r]);
+        acc[r] = fmaf(x[2], w[2], acc[r]);
+        acc[r] = fmaf(x[3], w[3], acc[r]);
+      }
+    }
+    for (; k < K; ++k) {
+      const float w = W[(long long)k * O + o];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) acc[r] = fmaf(xp[r * ldx + k], w, acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) epi(rg * RPT + r, o, acc[r]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
+  const tspm_head_desc& d = a.d;
+  // LDS row blocks; leading dimensions padded by 4 floats (16-byte aligned rows, staggered banks)
+  __shared__ __attribute__((aligned(16))) float sx[HEAD_RB * (HEAD_MAXIN + 4)];
+  __shared__ __attribute__((aligned(16))) float sh1[HEAD_RB * (HEAD_MAXH + 4)];
+  __shared__ __attribute__((aligned(16))) float shh[HEAD_RB * (HEAD_MAXH2 + 4)];
+  __shared__ __attribute__((aligned(16))) float sz[HEAD_RB * (HEAD_MAXC + 4)];
+  const int F = d.in, H = d.hidden, H2 = d.hidden2, C = d.classes;
+  const int ldx = F + 4, ldh = H + 4, ldh2 = H2 + 4, ldc = C + 4;
+  const int n0 = blockIdx.x * HEAD_RB;
+  const int rows = min(HEAD_RB, d.n - n0);
+  const int t = threadIdx.x;
+  // stage the row block's inputs (rows past n: zeros, never stored)
+  for (int i = t; i < HEAD_RB * (F / 4); i += blockDim.x) {
+    const int r = i / (F / 4), k4 = i % (F / 4);
+    const f32x4 v = r < rows ? ld4(d.x + (long long)(n0 + r) * d.ldx + 4 * k4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    st4(sx + r * ldx + 4 * k4, v);
+  }
+  uint64_t base = 0;
+  if (d.p > 0.f && d.gen_keep) base = tspm_dropout_base(d.seed, d.counter ? *d.counter : 0ULL);
+  __syncthreads();
+  // fc0 + ReLU + dropout (tspm_linear_fwd's epilogue order: + bias, relu, * keep*scale)
+  head_xwT<4>(sx, ldx, d.w0, F, H, [&](int r, int o, float acc) {
+    float v = relu_f(acc + d.b0[o]);
+    if (d.p > 0.f) {
+      const long long i = (long long)(n0 + r) * H + o;
+      bool kp;
+      if (d.gen_keep) {
+        kp = tspm_dropout_keep(base, i, d.p);
+        if (r < rows) d.keep[i] = kp ? 1 : 0;
+      } else {
+        kp = r < rows ? d.keep[i] != 0 : false;
+      }
+      v *= kp ? a.scale : 0.f;
+    }
+    sh1[r * ldh + o] = v;
+    if (r < rows) d.h1[(long long)(n0 + r) * H + o] = v;
+  });
+  __syncthreads();
+  head_xwT<2>(sh1, ldh, d.w3, H, H2, [&](int r, int o, float acc) {
+    const float v = relu_f(acc + d.b3[o]);
+    shh[r * ldh2 + o] = v;
+    if (r < rows) d.hh[(long long)(n0 + r) * H2 + o] = v;
+  });
+  __syncthreads();
+  head_xwT<1>(shh, ldh2, d.w5, H2, C, [&](int r, int o, float acc) {
+    const float v = acc + d.b5[o];
+    sz[r * ldc + o] = v;
+    if (r < rows) d.logits[(long long)(n0 + r) * C + o] = v;
+  });
+  __syncthreads();
+  // cross-entropy per row (tspm_cross_entropy's arithmetic); sz becomes dlogits
+  if (t < HEAD_RB) {
+    float* z = sz + t * ldc;
+    if (t < rows) {
+      float mx = z[0];
+      int am = 0;
+      for (int k = 1; k < C; ++k)
+        if (z[k] > mx) { mx = z[k]; am = k; }
+      float se = 0.f;
+      for (int k = 0; k < C; ++k) se += expf(z[k] - mx);
+      const float lse = logf(se);
+      const long long lab64 = d.labels[n0 + t];
+      const bool lok = lab64 >= 0 && lab64 < C;
+      const int lab = lok ? (int)lab64 : 0;
+      d.row_ws[n0 + t] = lok ? lse - (z[lab] - mx) : __builtin_nanf("");
+      d.row_ws[d.n + n0 + t] = (am == lab) ? 1.f : 0.f;
+      const float invn = 1.0f / (float)d.n;
+      for (int k = 0; k < C; ++k) {  // in place: class k's logit is read once, after mx and se
+        const float pk = expf(z[k] - mx) / se;
+        const float g = lok ? (pk - (k == lab ? 1.f : 0.f)) * invn * d.loss_weight : __builtin_nanf("");
+        z[k] = g;
+        d.dlogits[(long long)(n0 + t) * C + k] = g;
+      }
+    } else {
+      for (int k = 0; k < C; ++k) z[k] = 0.f;
+    }
+  }
+  __syncthreads();
+  // dz3 = (dlogits w5) * (hh > 0)   (w5 is [C][H2]: the transposed product) -> shh
+  head_xW<2>(sz, ldc, d.w5, C, H2, [&](int r, int o, float acc) {
+    const float v = shh[r * ldh2 + o] > 0.f ? acc : 0.f;
+    if (r < rows) d.dz3[(long long)(n0 + r) * H2 + o] = v;
+    // every thread has read its hh value before any thread overwrites: item (r, o) is read and written
+    // by the same thread only
+    shh[r * ldh2 + o] = v;
+  });
+  __syncthreads();
+  // dz0 = (dz3 w3) * (h1 > 0 ? scale : 0)   (w3 is [H2][H]) -> sh1
+  head_xW<4>(shh, ldh2, d.w3, H2, H, [&](int r, int o, float acc) {
+    const float v = sh1[r * ldh + o] > 0.f ? acc * a.scale : 0.f;
+    if (r < rows) d.dz0[(long long)(n0 + r) * H + o] = v;
+    sh1[r * ldh + o] = v;
+  });
+  __syncthreads();
+  // dx = dz0 w0   (w0 is [H][F])
+  head_xW<8>(sh1, ldh, d.w0, H, F, [&](int r, int o, float acc) {
+    if (r < rows) d.dx[(long long)(n0 + r) * d.lddx + o] = acc;
+  });
+}
+
+template <int WK>
+__global__ __launch_bounds__(64 * WK) void k_head_wgrad(GemmMulti mp, int total, HeadArgs a) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  if (b < total) {
+    int i = 0;
+    while (i + 1 < mp.count && b >= mp.start[i + 1]) ++i;  // workgroup-uniform
+    gemm_body<WK>(mp.p[i], b - mp.start[i], lds);
+    return;
+  }
+  // the loss: fixed-order sums of the per-row losses / correct flags, in double
+  const tspm_head_desc& d = a.d;
+  double* red = reinterpret_cast<double*>(lds);
+  const int T = 64 * WK;
+  double ls = 0.0, cs = 0.0;
+  for (int n = threadIdx.x; n < d.n; n += T) {
+    ls += (double)d.row_ws[n];
+    cs += (double)d.row_ws[d.n + n];
+  }
+  red[threadIdx.x] = ls;
+  red[T + threadIdx.x] = cs;
+  __syncthreads();
+  for (int s = T / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      red[threadIdx.x] += red[threadIdx.x + s];
+      red[T + threadIdx.x] += red[T + threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float l = (float)(red[0] / (double)d.n);
+    d.loss[0] = l * d.loss_weight;
+    if (d.stats) {
+      d.stats[0] += (float)red[0];
+      d.stats[1] += (float)red[T];
+      d.stats[2] += (float)d.n;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t stream) {
+  if (!desc) return TSPM_ERR_INVALID;
+  const tspm_head_desc& d = *desc;
+  if (d.n <= 0 || d.in <= 0 || d.hidden <= 0 || d.hidden2 <= 0 || d.classes <= 0) return TSPM_ERR_INVALID;
+  if (d.in > HEAD_MAXIN || d.hidden > HEAD_MAXH || d.hidden2 > HEAD_MAXH2 || d.classes > HEAD_MAXC)
+    return TSPM_ERR_INVALID;
+  if (d.in % 4 || d.hidden % 4 || d.hidden2 % 4 || d.ldx < d.in || d.ldx % 4 || d.lddx < d.in) return TSPM_ERR_INVALID;
+  if (!d.x || !d.w0 || !d.b0 || !d.w3 || !d.b3 || !d.w5 || !d.b5 || !d.labels || !d.h1 || !d.hh || !d.logits ||
+      !d.dlogits || !d.dz3 || !d.dz0 || !d.dx || !d.row_ws || !d.gw0 || !d.gb0 || !d.gw3 || !d.gb3 || !d.gw5 ||
+      !d.gb5 || !d.loss)
+    return TSPM_ERR_INVALID;
+  if (!aligned16(d.x) || !aligned16(d.w0) || !aligned16(d.w3) || !aligned16(d.w5)) return TSPM_ERR_INVALID;
+  if (d.p < 0.f || d.p >= 1.f || (d.p > 0.f && !d.keep)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HeadArgs a{d, d.p > 0.f ? 1.0f / (1.0f - d.p) : 1.0f};
+  hipLaunchKernelGGL(k_head_rows, dim3(cdiv(d.n, HEAD_RB)), dim3(256), 0, st, a);
+  TSPM_LAUNCH_CHECK();
+  // weight gradients: dw[o,i] = sum_n dz[n,o] in[n,i], db[o] = sum_n dz[n,o] (tspm_linear_bwd_weight's
+  // operands), plus the loss workgroup
+  GemmMulti mp{};
+  mp.p[0] = GemmArgs{d.classes, d.hidden2, d.n, d.dlogits, 1, d.classes, d.hh, d.hidden2, 1, d.gw5, d.hidden2,
+                     nullptr, 0, nullptr, 1.f, d.gb5};
+  mp.p[1] = GemmArgs{d.hidden2, d.hidden, d.n, d.dz3, 1, d.hidden2, d.h1, d.hidden, 1, d.gw3, d.hidden, nullptr, 0,
+                     nullptr, 1.f, d.gb3};
+  mp.p[2] = GemmArgs{d.hidden, d.in, d.n, d.dz0, 1, d.hidden, d.x, d.ldx, 1, d.gw0, d.in, nullptr, 0, nullptr, 1.f,
+                     d.gb0};
+  mp.count = 3;
+  int total = 0, wk = 1;
+  for (int i = 0; i < 3; ++i) {
+    const int w = gemm_wk(mp.p[i]);
+    wk = w > wk ? w : wk;
+    mp.start[i] = total;
+    total += cdiv(mp.p[i].M, 32) * cdiv(mp.p[i].N, 32);
+  }
+  mp.start[3] = total;
+  // LDS: the small-GEMM combine, or 2 x threads doubles for the loss workgroup
+  const size_t lds_gemm = (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
+  const size_t lds_loss = (size_t)2 * 64 * wk * sizeof(double);
+  const size_t lds = lds_gemm > lds_loss ? lds_gemm : lds_loss;
+  switch (wk) {
+    case 1: hipLaunchKernelGGL(k_head_wgrad<1>, dim3(total + 1), dim3(64), lds, st, mp, total, a); break;
+    case 2: hipLaunchKernelGGL(k_head_wgrad<2>, dim3(total + 1), dim3(128), lds, st, mp, total, a); break;
+    default: hipLaunchKernelGGL(k_head_wgrad<4>, dim3(total + 1), dim3(256), lds, st, mp, total, a); break;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}

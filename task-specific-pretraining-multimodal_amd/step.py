@@ -25,7 +25,6 @@ from . import _lib as L
 from .engine import EncoderEngine, prepare_encoder_layout
 from .ddp import PhasedGradAllReduce
 from .optim import FusedAdam
-from .linear import linear_bwd
 
 NUM_CLASSES = 10
 
@@ -120,34 +119,22 @@ class FusedTrainStep:
         self.hh = torch.empty(batch, self.h2, **f32)
         self.logits = torch.empty(batch, NUM_CLASSES, **f32)
         self.dlogits = torch.empty(batch, NUM_CLASSES, **f32)
-        self.dh = torch.empty(batch, self.h2, **f32)
-        self.dh1 = torch.empty(batch, hd, **f32)
+        self.dh = torch.empty(batch, self.h2, **f32)     # fc3 pre-activation gradient
+        self.dh1 = torch.empty(batch, hd, **f32)         # fc0 pre-activation gradient
         self.dfused = torch.empty(batch, self.F, **f32)
+        self.row_ws = torch.empty(2 * batch, **f32)       # per-row CE / correct flags (tspm_head_train_step)
         self.keep = torch.ones(batch, hd, dtype=torch.uint8, device=dev)
         self.loss = torch.zeros(1, **f32)
         self.stats = torch.zeros(4, **f32)  # loss*n, correct, n (accumulated on device)
         self.keep_override: Optional[torch.Tensor] = None
         self.nbt = shared_batches_tracked(model, dev)
-        # side stream + per-encoder auxiliary streams (weight-grad convs, downsample branch): 4 streams in
-        # all with the main one, matching the 4 hardware queues HIP gives a process by default; one set
-        # per process, shared by every step build (L.shared_streams)
-        self.side, self.aux_a, self.aux_i = L.shared_streams(dev, 3)
+        # the image encoder's branch runs on a side stream; the DP exchange on a third (one set per process,
+        # shared by every step build: L.shared_streams)
+        self.side, self.comm = L.shared_streams(dev, 2)
         self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
-        # Off by default: measured on MI355X (ROCm 7), an eager step gains ~3 % from the auxiliary
-        # streams but a replayed HIP graph with their ~50 cross-stream edges runs ~30 % SLOWER than
-        # the two-branch graph (25.5k vs 36.4k samples/s at batch 128).  TSPM_AUX=1 turns them on.
-        self.use_aux = os.environ.get("TSPM_AUX", "0") == "1"
-        # single-GPU step: Adam over the late layers' parameters (fc, layer4, layer3 of both encoders
-        # + the head: 94 % of the parameters) overlapping the early layers' backward (element-wise
-        # update: bitwise the same result).  TSPM_OVERLAP_OPT: "0" off (default), "stream" on a third
-        # stream, "main" on the audio encoder's stream between its two backward phases (the image
-        # encoder's chain is the longer one).  Measured at batch 128: "stream" 2.96 ms vs 2.82 ms off.
-        self.overlap_opt = os.environ.get("TSPM_OVERLAP_OPT", "0")
-        if self.overlap_opt not in ("0", "stream", "main"):
-            raise L.TspmError("TSPM_OVERLAP_OPT must be 0, stream or main")
-        self._opt_ranges = None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
+        self._graph_gen_keep = True
         self.calls = 0
         self._sig = (id(optimizer), id(loss_functions), batch)
         # dropout RNG counter = FusedAdam's device step counter (distinct per step, graph-safe)
@@ -159,80 +146,44 @@ class FusedTrainStep:
             tuple(self.A.shape[1:]),) and tuple(I.shape[-2:]) == tuple(self.I.shape[-2:])
 
     # ------------------------------------------------------------------------------------------
-    def _head_fwd(self, sh: int) -> None:
-        lib = L.lib()
-        n, F, hd, h2 = self.N, self.F, self.hd, self.h2
+    def _head(self, sh: int) -> None:
+        """The fusion head's forward, the loss group's cross-entropy and the head's backward in two launches
+        (tspm_head_train_step, ABI 16; MML_Suite/models/avmnist.py:219-230,267, experiment_utils/loss.py:98-148):
+        h1 / hh / logits / loss, the dropout keep mask (drawn on the device from the step counter unless
+        keep_override was copied in), the net.{0,3,5} weight and bias gradients into FusedAdam's flat
+        buffer, and dfused = the gradient into both encoders' embeddings."""
         net = self.model.net
-        p = self.model.dropout_p
-        keep = None
-        scale = 1.0
-        if p > 0:
-            scale = 1.0 / (1.0 - p)
-            if self.keep_override is None:
-                L.check(lib.tspm_dropout_mask(n * hd, p, self.model._rng_seed, self._rng_ctr_ptr, self.keep.data_ptr(),
-                                              sh), "dropout_mask")
-            keep = self.keep
-        L.check(lib.tspm_linear_fwd(n, F, hd, self.fused.data_ptr(), F, net[0].weight.data_ptr(), net[0].bias.data_ptr(),
-                                    1, L.ptr(keep), scale, self.h1.data_ptr(), hd, sh), "head fc0")
-        L.check(lib.tspm_linear_fwd(n, hd, h2, self.h1.data_ptr(), hd, net[3].weight.data_ptr(), net[3].bias.data_ptr(),
-                                    1, None, 1.0, self.hh.data_ptr(), h2, sh), "head fc3")
-        L.check(lib.tspm_linear_fwd(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, net[5].weight.data_ptr(),
-                                    net[5].bias.data_ptr(), 0, None, 1.0, self.logits.data_ptr(), NUM_CLASSES, sh),
-                "head fc5")
-        self._scale = scale
+        p = float(self.model.dropout_p)
+        g = lambda t: t.data_ptr()  # noqa: E731
+        d = L.HeadDesc(n=self.N, in_=self.F, hidden=self.hd, hidden2=self.h2, classes=NUM_CLASSES, ldx=self.F,
+                       lddx=self.F, gen_keep=1 if (p > 0 and self.keep_override is None) else 0,
+                       x=g(self.fused), w0=g(net[0].weight), b0=g(net[0].bias), w3=g(net[3].weight), b3=g(net[3].bias),
+                       w5=g(net[5].weight), b5=g(net[5].bias), p=p, loss_weight=self.ce_weight,
+                       seed=int(self.model._rng_seed) if p > 0 else 0, counter=self._rng_ctr_ptr if p > 0 else None,
+                       keep=g(self.keep), labels=g(self.labels), h1=g(self.h1), hh=g(self.hh), logits=g(self.logits),
+                       dlogits=g(self.dlogits), dz3=g(self.dh), dz0=g(self.dh1), dx=g(self.dfused), row_ws=g(self.row_ws),
+                       gw0=g(net[0].weight.grad), gb0=g(net[0].bias.grad), gw3=g(net[3].weight.grad),
+                       gb3=g(net[3].bias.grad), gw5=g(net[5].weight.grad), gb5=g(net[5].bias.grad),
+                       loss=g(self.loss), stats=g(self.stats))
+        L.check(L.lib().tspm_head_train_step(d, sh), "head_train_step")
 
-    def _head_bwd(self, sh: int) -> None:
-        lib = L.lib()
-        n, F, hd, h2 = self.N, self.F, self.hd, self.h2
-        net = self.model.net
-        g = lambda p: p.grad  # noqa: E731  (flat views)
-        # each layer's weight-grad and data-grad in one launch (tspm_linear_bwd, bitwise the two launches)
-        linear_bwd(n, h2, NUM_CLASSES, self.hh.data_ptr(), h2, self.dlogits.data_ptr(), NUM_CLASSES,
-                   net[5].weight.data_ptr(), g(net[5].weight).data_ptr(), g(net[5].bias).data_ptr(),
-                   self.dh.data_ptr(), h2, sh)
-        L.check(lib.tspm_act_bwd(n, h2, self.dh.data_ptr(), h2, self.hh.data_ptr(), h2, 1.0, sh), "head relu")
-        linear_bwd(n, hd, h2, self.h1.data_ptr(), hd, self.dh.data_ptr(), h2, net[3].weight.data_ptr(),
-                   g(net[3].weight).data_ptr(), g(net[3].bias).data_ptr(), self.dh1.data_ptr(), hd, sh)
-        L.check(lib.tspm_act_bwd(n, hd, self.dh1.data_ptr(), hd, self.h1.data_ptr(), hd, self._scale, sh),
-                "head relu+dropout")
-        linear_bwd(n, F, hd, self.fused.data_ptr(), F, self.dh1.data_ptr(), hd, net[0].weight.data_ptr(),
-                   g(net[0].weight).data_ptr(), g(net[0].bias).data_ptr(), self.dfused.data_ptr(), F, sh)
-
-    def _fwd_bwd(self, phase: int = 0, marks=None) -> None:
-        """Enqueue forward + loss + backward on the current stream (+ the side stream).  phase 0:
-        everything; 1: forward, loss, head backward and the encoders' backward phase 1 (fc,
-        layer4, layer3); 2: the encoders' backward phase 2 (layer2, layer1, stem) — see
-        EncoderEngine.backward and ddp.PhasedGradAllReduce.  ``marks`` (phase 0 only): two
-        ``_lib.DeviceFlag``s bumped after the audio / image encoder's backward phase 1 (the same launches,
-        split at the phase boundary), which the DP exchange waits on outside the graph (_run_phased)."""
+    def _fwd_bwd(self, marks=None) -> None:
+        """Enqueue forward + loss + backward on the current stream (+ the side stream for the image encoder).
+        ``marks``: two ``_lib.DeviceFlag``s bumped after the audio / image encoder's backward phase 1 (fc,
+        layer4, layer3: the same launches, split at the phase boundary), which the DP exchange waits on outside
+        the graph (_run_phased)."""
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
-        self.eng_a.aux = None if self.serial or not self.use_aux else self.aux_a
-        self.eng_i.aux = None if self.serial or not self.use_aux else self.aux_i
-        # see EncoderEngine.fork_ds: the image encoder runs on a forked stream, so its helper
-        # stream may only join the origin (main) stream
-        self.eng_i.fork_ds = False
-        self.eng_i.join_aux = False
-        # TSPM_ENC_ORDER=ai: capture the audio encoder's launches before the image encoder's (A/B of the
-        # graph's node order for the two independent branches; default "ia")
-        audio_first = os.environ.get("TSPM_ENC_ORDER", "ia") == "ai"
-        if phase in (0, 1):
-            side.wait_stream(main)
-            if audio_first:
-                self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-            with torch.cuda.stream(side):
-                self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-            if not audio_first:
-                self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-            main.wait_stream(side)
-            sh = main.cuda_stream
-            self._head_fwd(sh)
-            L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
-                                               self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
-                                               self.stats.data_ptr(), sh), "cross_entropy")
-            self._classify(sh)
-            self._head_bwd(sh)
+        self.eng_a.aux = self.eng_i.aux = None
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
+        self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
+        main.wait_stream(side)
+        sh = main.cuda_stream
+        self._head(sh)
+        self._classify(sh)
         side.wait_stream(main)
         if marks is not None:
             mark_a, mark_i = marks
@@ -245,18 +196,11 @@ class FusedTrainStep:
             with torch.cuda.stream(side):
                 self.eng_i.backward(None, self.F, phase=2)
         else:
-            if audio_first:
-                self.eng_a.backward(self.dfused, self.F, phase=phase)
             with torch.cuda.stream(side):
-                self.eng_i.backward(self.dfused[:, ea:], self.F, phase=phase)
-            if not audio_first:
-                self.eng_a.backward(self.dfused, self.F, phase=phase)
+                self.eng_i.backward(self.dfused[:, ea:], self.F)
+            self.eng_a.backward(self.dfused, self.F)
         main.wait_stream(side)
-        if not self.serial:  # every forked stream joins the origin stream (graph capture rule)
-            main.wait_stream(self.aux_a)
-            main.wait_stream(self.aux_i)
-        if phase in (0, 2):
-            L.counters_add(self.nbt)
+        L.counters_add(self.nbt)
 
     def phased_allreduce(self, force: bool = False, bucket_mb: float = 64.0, group=None):
         """The overlapped DP exchange for this step: gradient ranges of FusedAdam's flat buffers in
@@ -278,49 +222,21 @@ class FusedTrainStep:
                                                                   [id(p) in st for p in fg.params])]
         return PhasedGradAllReduce(views, bucket_mb=bucket_mb, group=group, force=force)
 
-    def _fwd_head(self) -> None:
-        """Forward of both encoders (two streams), fusion head, cross-entropy, head backward."""
-        main = torch.cuda.current_stream()
-        ea = self.model.embd_size_A
-        self.eng_a.aux = self.eng_i.aux = None
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-        self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-        main.wait_stream(self.side)
-        sh = main.cuda_stream
-        self._head_fwd(sh)
-        L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
-                                           self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
-                                           self.stats.data_ptr(), sh), "cross_entropy")
-        self._classify(sh)
-        self._head_bwd(sh)
-        L.counters_add(self.nbt)
-
     def _run_phased(self) -> None:
         """DP step with the RCCL exchange overlapped with backward, the whole forward + backward as ONE
-        HIP graph (the plain step's two-stream schedule; VERDICT r2 item 6):
-             main (graph): [fwd both + head + head bwd + audio bwd late ─●─ audio bwd early] ─┐
-             side (graph):                               [image bwd late ─●─ image bwd early] ─┴─ wait ─ [Adam graph]
-             RCCL:                                      all-reduce(head+audio late) · (image late) · (both early)
+        HIP graph (the plain step's two-stream schedule):
+             main (graph): [fwd both + head + audio bwd late ─●─ audio bwd early] ─┐
+             side (graph):                   [image bwd late ─●─ image bwd early] ─┴─ wait ─ [Adam graph]
+             RCCL:                          all-reduce(head+audio late) · (image late) · (both early)
         ● = a step flag (``_lib.DeviceFlag``: a one-thread kernel in the graph publishes a per-step count to
         pinned host memory; the host waits for it before launching the collective — ROCm 7 refuses
         graph-external event records); the collectives run outside the graph, on RCCL's stream, each
-        after the event of the backward part that writes its gradients.  ``TSPM_PHASED=split`` keeps the
-        round-2 schedule (one graph per phase and encoder, _run_phased_split)."""
-        if os.environ.get("TSPM_PHASED", "one") == "split":
-            self._run_phased_split()
-            return
+        after the flag of the backward part that writes its gradients."""
         ar = self.allreduce
-        main = torch.cuda.current_stream()
-        comm = self.aux_a  # free in this schedule (the auxiliary conv streams are off)
         eager = not self.use_graph or self.calls == 0
         if getattr(self, "_marks", None) is None:
             self._marks = (L.DeviceFlag(), L.DeviceFlag())
         self.eng_i.fork_ds = self.eng_a.fork_ds = False
-        # diagnostics for the structure's cost with no exchange (inactive all-reduce only): "nowait" skips
-        # the flag waits / stream hops, "inline" also keeps Adam inside the step graph
-        diag = os.environ.get("TSPM_PHASED_DIAG", "") if not ar.active() else ""
         if eager:
             self._fwd_bwd(marks=self._marks)
         else:
@@ -329,30 +245,21 @@ class FusedTrainStep:
                 g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._fwd_bwd(marks=self._marks)
-                    if diag == "inline":
-                        self._opt()
                 with torch.cuda.graph(go):
                     self._opt()
                 self.graph, self.graph_opt = g, go
+                self._graph_gen_keep = self.keep_override is None
             self.graph.replay()
-        if diag in ("nowait", "inline"):
-            for f in self._marks:
-                f.count += 1
-            if diag == "nowait":
-                self.graph_opt.replay() if not eager else self._opt()
-            elif eager:
-                self._opt()
-            return
         # each flag is bumped once per step, after (in graph order) everything main ran before this step
         # (batch upload, the previous step's Adam reading the gradients): once the host has seen it, the
         # gradients it covers are complete, so the exchange launched then needs no device-side wait
         for f in self._marks:
             f.count += 1
         self._marks[0].host_wait(self._marks[0].count)
-        with torch.cuda.stream(comm):
+        with torch.cuda.stream(self.comm):
             w_a = ar.launch(0)
         self._marks[1].host_wait(self._marks[1].count)
-        with torch.cuda.stream(comm):
+        with torch.cuda.stream(self.comm):
             w_i = ar.launch(1)
         w_e = ar.launch(2)  # on main, behind the graph: no stream hop before the last exchange
         ar.wait(w_a + w_i + w_e)
@@ -360,65 +267,6 @@ class FusedTrainStep:
             self._opt()
         else:
             self.graph_opt.replay()
-
-    def _run_phased_split(self) -> None:
-        """DP step with the RCCL exchange overlapped with backward:
-             main:   [fwd both + head + head bwd] ──────────────────────────── wait ─ [Adam]
-             s_a:        └ [audio bwd late] ─ [audio bwd early] ─┤
-             s_i:        └ [image bwd late] ─ [image bwd early] ─┤
-             RCCL:          all-reduce(head+audio late) · (image late) · (both early)
-        Each bracket is a HIP graph (captured on the second call); the collectives stay outside the
-        graphs on RCCL's stream, ordered against the compute streams by events."""
-        ar = self.allreduce
-        main = torch.cuda.current_stream()
-        sa, si = self.aux_a, self.aux_i
-        ea, F = self.model.embd_size_A, self.F
-        parts = [
-            (main, lambda: self._fwd_head()),
-            (sa, lambda: self.eng_a.backward(self.dfused, F, phase=1)),
-            (si, lambda: self.eng_i.backward(self.dfused[:, ea:], F, phase=1)),
-            (sa, lambda: self.eng_a.backward(None, F, phase=2)),
-            (si, lambda: self.eng_i.backward(None, F, phase=2)),
-            (main, self._opt),
-        ]
-        eager = not self.use_graph or self.calls == 0
-        if not eager and self.graph is None:
-            torch.cuda.synchronize(self.device)
-            gs = []
-            for stream, fn in parts:
-                g = torch.cuda.CUDAGraph()
-                # main-stream parts are captured on torch's own capture stream (the current stream
-                # may be the legacy default stream, which cannot capture) and replayed on main
-                with torch.cuda.graph(g, stream=None if stream is main else stream):
-                    fn()
-                gs.append(g)
-            self.graph = gs
-
-        def run(k):
-            stream, fn = parts[k]
-            with torch.cuda.stream(stream):
-                if eager:
-                    fn()
-                else:
-                    self.graph[k].replay()
-
-        self.eng_i.fork_ds = self.eng_a.fork_ds = False
-        run(0)
-        sa.wait_stream(main)
-        si.wait_stream(main)
-        run(1)
-        with torch.cuda.stream(sa):
-            w_a = ar.launch(0)
-        run(2)
-        with torch.cuda.stream(si):
-            w_i = ar.launch(1)
-        run(3)
-        run(4)
-        main.wait_stream(sa)
-        main.wait_stream(si)
-        w_e = ar.launch(2)
-        ar.wait(w_a + w_i + w_e)
-        run(5)
 
     def _classify(self, sh: int) -> None:
         log = self.log
@@ -432,79 +280,7 @@ class FusedTrainStep:
     def _opt(self) -> None:
         self.opt.launch(torch.cuda.current_stream().cuda_stream)
 
-    def _late_early_ranges(self):
-        """FusedAdam flat-buffer ranges of (late: head + both encoders' backward phase 1, early: phase 2)."""
-        if self._opt_ranges is None:
-            from .ddp import flat_ranges
-            late = {id(p) for p in self.eng_a.phase_params(1) + self.eng_i.phase_params(1)}
-            late |= {id(p) for p in self.model.net.parameters()}
-            out = ([], [])
-            for fg in self.opt.flat_groups():
-                numels = [p.numel() for p in fg.params]
-                sel = [id(p) in late for p in fg.params]
-                out[0].append(flat_ranges(fg.offsets, numels, fg.numel, sel))
-                out[1].append(flat_ranges(fg.offsets, numels, fg.numel, [not x for x in sel]))
-            self._opt_ranges = out
-        return self._opt_ranges
-
-    def _fwd_bwd_overlap_opt(self) -> None:
-        """Single-GPU step with Adam split in two: forward, head, both encoders' backward phase 1 (fc,
-        layer4, layer3) → the late parameters' Adam on a third stream ‖ backward phase 2 (layer2,
-        layer1, stem) → the early parameters' Adam."""
-        main = torch.cuda.current_stream()
-        late, early = self._late_early_ranges()
-        if self.overlap_opt == "main":
-            ea, F = self.model.embd_size_A, self.F
-            self._fwd_head_only()
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
-                self.eng_i.backward(self.dfused[:, ea:], F, phase=1)
-                done_i = torch.cuda.Event()
-                done_i.record()
-                self.eng_i.backward(None, F, phase=2)
-            self.eng_a.backward(self.dfused, F, phase=1)
-            main.wait_event(done_i)
-            self.opt.launch_begin(main.cuda_stream)
-            self.opt.launch_ranges(main.cuda_stream, late)
-            self.eng_a.backward(None, F, phase=2)
-            main.wait_stream(self.side)
-            self.opt.launch_ranges(main.cuda_stream, early)
-            L.counters_add(self.nbt)
-            return
-        s3 = self.aux_a
-        self._fwd_bwd(phase=1)
-        self.opt.launch_begin(main.cuda_stream)  # one step-count increment, seen by both halves
-        s3.wait_stream(main)
-        with torch.cuda.stream(s3):
-            self.opt.launch_ranges(s3.cuda_stream, late)
-        self._fwd_bwd(phase=2)
-        self.opt.launch_ranges(main.cuda_stream, early)
-        main.wait_stream(s3)
-
-    def _fwd_head_only(self) -> None:
-        """Both encoders' forward (two streams), head, cross-entropy, head backward — on main."""
-        main = torch.cuda.current_stream()
-        ea = self.model.embd_size_A
-        self.eng_a.aux = self.eng_i.aux = None
-        self.eng_i.fork_ds = False
-        self.eng_i.join_aux = False
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-        self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
-        main.wait_stream(self.side)
-        sh = main.cuda_stream
-        self._head_fwd(sh)
-        L.check(L.lib().tspm_cross_entropy(self.N, NUM_CLASSES, self.logits.data_ptr(), self.labels.data_ptr(),
-                                           self.loss.data_ptr(), self.dlogits.data_ptr(), self.ce_weight,
-                                           self.stats.data_ptr(), sh), "cross_entropy")
-        self._classify(sh)
-        self._head_bwd(sh)
-
     def _enqueue_all(self) -> None:
-        if self.allreduce is None and self.overlap_opt != "0" and not self.serial and not self.use_aux:
-            self._fwd_bwd_overlap_opt()
-            return
         self._fwd_bwd()
         if self.allreduce is None:
             self._opt()
@@ -536,6 +312,9 @@ class FusedTrainStep:
             self._graph_log = self.log
         if self.keep_override is not None:
             self.keep.copy_(self.keep_override.reshape(self.keep.shape).to(torch.uint8), non_blocking=True)
+        # the captured head either draws its keep mask or reads the copied-in one: re-capture on a change
+        if self.graph is not None and self._graph_gen_keep != (self.keep_override is None):
+            self.graph, self.graph_opt = None, None
         if isinstance(self.allreduce, PhasedGradAllReduce):
             self._run_phased()
             self.opt.note_steps(1)
@@ -565,6 +344,7 @@ class FusedTrainStep:
             else:
                 self._fwd_bwd()
         self.graph = g
+        self._graph_gen_keep = self.keep_override is None
         if self.allreduce is not None:
             go = torch.cuda.CUDAGraph()
             with torch.cuda.graph(go):

@@ -80,6 +80,9 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.tspm_conv_fwd(ctypes.byref(s32), ctypes.byref(vs), 16, None, 16, 16, None, None, 0, None) == 3
     assert lib.tspm_adam_step(10, 17, 16, 16, 16, 16, None) == 1   # misaligned
     assert lib.tspm_dropout_mask(10, 1.0, 0, None, 16, None) == 1   # p must be < 1
+    hd = L.HeadDesc(n=8, in_=192, hidden=128, hidden2=64, classes=10, ldx=192, lddx=192)
+    assert lib.tspm_head_train_step(ctypes.byref(hd), None) == 1       # null buffers
+    assert lib.tspm_head_train_step(None, None) == 1
 
 
 def test_workspace_queries():

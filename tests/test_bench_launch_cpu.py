@@ -1,0 +1,76 @@
+"""bench.py's multi-rank launch on CPU (verdict r3 item 1): ``python bench.py --gpus N`` started as ONE
+plain process must start N ranks itself (the driver runs exactly that command on an 8-GPU node), the
+torchrun launch must keep working, and a world size that disagrees with --gpus must be refused.
+``--dry-run`` runs the launch + gloo process group + barrier-bracketed, max-over-ranks timed region
+with an empty step, so no GPU is needed."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env=None, timeout=120):
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=env if env is not None else _env(), cwd=REPO)
+
+
+def _one_json(out):
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus2_spawns_two_ranks():
+    p = _run(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _one_json(p.stdout)
+    assert res["n_gpus"] == 2
+    assert res["config"]["global_batch"] == 256 and res["config"]["per_rank_batch"] == 128
+    assert res["process_group_world_size"] == 2
+    ranks = res["ranks"]
+    assert sorted(r["rank"] for r in ranks) == [0, 1]
+    assert len({r["pid"] for r in ranks}) == 2 and os.getpid() not in {r["pid"] for r in ranks}
+    assert all(r["pg_world_size"] == 2 for r in ranks)
+    assert res["launch"]["ranks"] == 2
+
+
+def test_gpus1_runs_in_process():
+    p = _run(["--gpus", "1", "--dry-run", "--steps", "2"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _one_json(p.stdout)
+    assert res["n_gpus"] == 1 and "launch" not in res and res["config"]["global_batch"] == 128
+
+
+def test_torchrun_env_is_honoured():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2", "--dry-run",
+                        "--steps", "2"], capture_output=True, text=True, timeout=120, env=_env(), cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _one_json(p.stdout)
+    assert res["n_gpus"] == 2 and "launch" not in res
+
+
+def test_world_size_mismatch_refused():
+    p = _run(["--gpus", "4", "--dry-run"], env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_failing_rank_fails_the_launch():
+    # rank 1 cannot start (the mismatch check fires in the child only for a bad env): simulate with an
+    # unknown flag passed through to both children -> argparse exits 2 in each, the parent must fail
+    p = _run(["--gpus", "2", "--dry-run", "--no-such-flag"])
+    assert p.returncode != 0
