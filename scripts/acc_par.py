@@ -34,6 +34,7 @@ def main() -> int:
     ap.add_argument("--jobs", type=int, default=4)
     ap.add_argument("--limit", type=int, default=900, help="seconds per child")
     ap.add_argument("--deadline", type=int, default=0, help="stop launching new seeds after this many seconds")
+    ap.add_argument("--script", default="accuracy_parity.py", help="the per-seed script under scripts/")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest and a.rest[0] == "--" else a.rest
@@ -47,8 +48,8 @@ def main() -> int:
     while pending or running:
         while pending and len(running) < a.jobs and not failed and not (a.deadline and time.time() - t0 > a.deadline):
             s = pending.pop(0)
-            log = open(os.path.join(OUT, f"accpar_{base[0]}_s{s}.log"), "w")
-            cmd = ["timeout", "-k", "10", str(a.limit), sys.executable, "-u", os.path.join(HERE, "accuracy_parity.py")]
+            log = open(os.path.join(OUT, f"accpar_{a.script[:-3]}_{base[0]}_s{s}.log"), "w")
+            cmd = ["timeout", "-k", "10", str(a.limit), sys.executable, "-u", os.path.join(HERE, a.script)]
             running[s] = (subprocess.Popen(cmd + base + ["--seeds", str(s)], stdout=log, stderr=subprocess.STDOUT,
                                            env=env), log)
         if a.deadline and time.time() - t0 > a.deadline:

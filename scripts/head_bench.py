@@ -1,0 +1,57 @@
+"""Graph-timed tspm_head_train_step (both launches) at batch 128 / 1024, and its two kernels' device
+durations from torch.profiler: the fusion head's cost in isolation."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import tspm_amd  # noqa: E402,F401
+from tspm_amd import _lib as L  # noqa: E402
+from test_gpu_head import _buffers  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    for n in (128, 1024):
+        ws, out = _buffers(n, 192, 128, 64, 10, dev, seed=1)
+        keep = torch.ones(n, 128, dtype=torch.uint8, device=dev)
+        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        d = L.HeadDesc(n=n, in_=192, hidden=128, hidden2=64, classes=10, ldx=192, lddx=192, gen_keep=1, p=0.5,
+                       loss_weight=1.0, seed=7, counter=ctr.data_ptr(), keep=keep.data_ptr(),
+                       labels=ws["labels"].data_ptr(),
+                       **{k: ws[k].data_ptr() for k in ("x", "w0", "b0", "w3", "b3", "w5", "b5")},
+                       **{k: v.data_ptr() for k, v in out.items()})
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            for _ in range(5):
+                L.check(L.lib().tspm_head_train_step(ctypes.byref(d), s.cuda_stream), "head")
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            R = 50
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(R):
+                    L.check(L.lib().tspm_head_train_step(ctypes.byref(d), torch.cuda.current_stream().cuda_stream),
+                            "head")
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (5 * R)
+        from tspm_amd.roofline import device_kernels
+        ks = device_kernels(lambda: g.replay(), 2)
+        per = {}
+        for k in ks:
+            nm = "rows" if "k_head_rows" in k["name"] else "wgrad" if "k_head_wgrad" in k["name"] else k["name"][:30]
+            per[nm] = per.get(nm, 0.0) + k["dur"] / (2 * R)
+        print(f"n={n}: graph-timed {us:.2f} us per head step; device us per launch {per}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -54,7 +54,7 @@ def distinct_ops(batch, dev):
                 kinds = ("fwd", "wgrad")
             else:
                 xs = L.hwnc_strides(s.n, s.h, s.w, s.c)
-                kinds = ("fwd", "dgrad", "wgrad_t" if eng.use_t else "wgrad")
+                kinds = ("fwd", "dgrad", "wgrad")
             for kind in kinds:
                 out.setdefault((kind,) + key, (s, xs, op is eng.stem))
     return out

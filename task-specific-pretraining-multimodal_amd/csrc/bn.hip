@@ -106,20 +106,13 @@ __global__ __launch_bounds__(256) void k_bn_finalize(long long M, int C, int G, 
                  sinv, red, smu);
 }
 
-// "Wide" BN launches for the few-channel layers (TSPM_BN_WIDE, default on; 0 = the previous shapes, read
-// per call): the statistics merge with fewer channels per workgroup (64 workgroups at C = 64 instead of
-// 16, each merging its tiles with all 256 threads) and the backward partial sums with more rows' loads
-// in flight per thread (the C = 64 layers' partial pass has only 64 workgroups: 1/4 of the CUs, so each
-// must keep more bytes in flight).  Both change only the (fixed) order of the double-precision sums.
-bool bn_wide() {
-  const char* e = getenv("TSPM_BN_WIDE");
-  return !(e && e[0] == '0');
-}
-// A/B switch read per call: unset = `dflt`, "0" = off, anything else = on
-bool getenv_flag(const char* name, bool dflt) {
-  const char* e = getenv(name);
-  return e ? e[0] != '0' : dflt;
-}
+// "Wide" BN launches for the few-channel layers (measured: BN 1.04 -> 1.02 ms): the statistics
+// merge with fewer channels per workgroup (64 workgroups at C = 64 instead of 16, each merging its tiles
+// with all 256 threads) and the backward partial sums with more rows' loads in flight per thread (the
+// C = 64 layers' partial pass has only 64 workgroups: 1/4 of the CUs, so each must keep more bytes in
+// flight).  Both change only the (fixed) order of the double-precision sums.
+constexpr bool bn_wide() { return true; }
+
 
 // ------------------------------------------------------------------------------------------------
 // apply: out = act(y*scale + shift [+ res | + res*scale2 + shift2])
@@ -733,13 +726,10 @@ int bwd_fused_u(long long m, int c) {
   return 0;
 }
 
-// Off by default (TSPM_BN_BWD_FUSED=1 enables it; read per call): measured on MI355X
-// (scripts/bn_bench.py, graph-timed) the barrier round trips cost more than the launch they save —
-// 8.0 vs 7.0 us at 128 x 512, 11.5 vs 7.3 us at 512 x 256, 22.6 vs 18.5 us at 24576 x 64.
-bool bwd_fused_enabled() {
-  const char* e = getenv("TSPM_BN_BWD_FUSED");
-  return e && e[0] == '1';
-}
+// Off: measured on MI355X (scripts/bn_bench.py, graph-timed) the barrier round trips cost more than the
+// launch they save — 8.0 vs 7.0 us at 128 x 512, 11.5 vs 7.3 us at 512 x 256, 22.6 vs 18.5 us at 24576 x 64.
+// Not reachable (kept as the measured alternative: DESIGN §7).
+constexpr bool bwd_fused_enabled() { return false; }
 
 // Tiled backward apply: [64 rows x 64 channels] per workgroup; also writes dy_t (and dy2_t) in
 // the transposed wgrad operand layout through LDS.
@@ -1013,7 +1003,9 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   // 1,024-thread workgroups for the 64-channel layers' tiles (TSPM_BN_PART_RG64=1; off by default: measured
   // BN device time 1.020 -> 0.972 ms per step but the step 2.778 -> 2.786 ms — the wider workgroups
   // crowd the other encoder's stream)
-  const bool wide_rg = bn_wide() && c <= 64 && rpb >= 64 && getenv_flag("TSPM_BN_PART_RG64", false);
+  // (1,024-thread workgroups for the C = 64 partial pass: BN 1.020 -> 0.972 ms of device time but the step
+  // 2.778 -> 2.786 ms — the wide workgroups crowd the other encoder's stream; off)
+  constexpr bool wide_rg = false;
 #define BNB_P(HO, TW, U)                                                                                     \
   if (wide_rg)                                                                                               \
     hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, (U > 4 ? U / 2 : 4), 64>), pgrid, dim3(1024), 0, st,        \

@@ -594,8 +594,7 @@ __global__ __launch_bounds__(256) void k_reduce_slabs_wide(long long count, int 
 void launch_reduce_slabs(long long count, int nslab, long long slab_stride, const float* slabs, float* out, int beta,
                          hipStream_t st) {
   constexpr int kQ = 8;
-  const char* e = getenv("TSPM_SLAB_WIDE");  // A/B switch (read per call): 0 = the element-parallel loop only
-  if (!(e && e[0] == '0') && nslab >= 2 * kQ && count <= (1LL << 18)) {
+  if (nslab >= 2 * kQ && count <= (1LL << 18)) {  // slab-parallel: many slabs of a small output
     hipLaunchKernelGGL((k_reduce_slabs_wide<kQ>), dim3((unsigned)cdiv64(count, 256 / kQ)), dim3(256), 0, st, count,
                        nslab, slab_stride, slabs, out, beta);
     return;
@@ -708,15 +707,8 @@ ConvArgs make_args(const tspm_conv_shape* s) {
 constexpr int kMaxFusedSplits = 16;   // wgrad: in-launch slab reduction up to this many slabs
 constexpr int kMaxFusedMergeIters = 16;  // fwd: in-launch BN merge when each thread reads <= this many tiles
 
-// TSPM_INLAUNCH=0 turns the in-launch hand-offs off (separate merge / reduction launches) — an A/B
-// switch for measurements; read once.
-bool inlaunch_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("TSPM_INLAUNCH");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// In-launch hand-offs (BN merge / slab reduction by the last arriving workgroup) are always on.
+constexpr bool inlaunch_enabled() { return true; }
 
 bool is_hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
   if (!st) return true;

@@ -918,15 +918,15 @@ bool hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
   return st->sc == 1 && st->sn == s->c && st->sw == (long long)s->n * s->c && st->sh == (long long)s->w * s->n * s->c;
 }
 
-// TSPM_XCD_SWIZZLE=1 / 2: XCD-aware workgroup -> tile mapping over the whole grid / within each
-// split-K plane; default 0 = identity (results are bitwise the same either way)
-int xcd_enabled() {
-  const char* e = getenv("TSPM_XCD_SWIZZLE");
-  return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-}
+// XCD-aware workgroup -> tile mapping (1: over the whole grid, 2: within each split-K plane): measured
+// slower in the step (2.82 -> 3.01 ms) or neutral — identity mapping.  Results are bitwise the
+// same either way).  Not reachable.
+constexpr int xcd_enabled() { return 0; }
 
-// TSPM_HANDOFF_ACQUIRE=1: the last arriver of a split-K tile / BN merge group takes an agent-scope
-// acquire before its (sc1) payload loads; default 0 = sc1 stores + sc1 loads only (bitwise the same)
+// The last arriver of a split-K tile / BN merge group reads the sc1 payload with sc1 loads and takes no
+// agent-scope acquire (conv 2.612 -> 2.595 ms without it; bitwise the same).  TSPM_HANDOFF_ACQUIRE=1
+// restores the acquire: the reference side of the hand-off validation (tests/test_gpu_handoff.py), not a
+// performance option.
 int acquire_enabled() {
   const char* e = getenv("TSPM_HANDOFF_ACQUIRE");
   return (e && e[0] == '1') ? 1 : 0;

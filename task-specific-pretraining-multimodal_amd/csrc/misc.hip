@@ -208,16 +208,10 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_pair(GemmArgs a, GemmArgs b, i
     gemm_body<WK>(b, blockIdx.x - tiles_a, lds);
 }
 
-// Quad tiles are opt-in (TSPM_GEMM_QUAD=1; read once): measured on the MMIMDb image-encoder products
-// at batch 256 they did not pay — weight-grad 25.4 us (25.0 with 32x32 tiles), data-grad 36.8 us
-// (25-31) — the L1 sharing between a workgroup's waves does not materialise for these strides.
-bool getenv_flag_quad() {
-  static const bool v = [] {
-    const char* e = getenv("TSPM_GEMM_QUAD");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
+// Quad tiles (64x64, one quadrant per wave) measured on the MMIMDb image-encoder products at batch 256 did
+// not pay — weight-grad 25.4 us (25.0 with 32x32 tiles), data-grad 36.8 us (25-31): the L1 sharing between
+// a workgroup's waves does not materialise for these strides.  Off (not reachable).
+constexpr bool getenv_flag_quad() { return false; }
 
 // Split-K combine: C = epi(sum over slices in order of slab[s]) with gemm_small's epilogue.
 __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs g, int splits) {
@@ -745,15 +739,17 @@ extern "C" const char* tspm_status_string(int status) {
 namespace {
 
 // ---- fusion head train step (tspm_head_train_step) ---------------------------------------------------
-// Launch 1: one workgroup per HEAD_RB samples runs the head's whole row-local chain on data in LDS:
+// Launch 1: one workgroup per HEAD_RB samples runs the head's whole row-local chain with the three weight
+// matrices staged in LDS (w0 + w3 + w5 = 134 KB at 192 -> 128 -> 64 -> 10; read once per workgroup with
+// 16-byte loads, so the six dependent products below see LDS latency, not L2 latency):
 //   h1 = relu(x w0^T + b0) * keep/(1-p),  hh = relu(h1 w3^T + b3),  logits = hh w5^T + b5,  CE per row,
 //   dlogits,  dz3 = (dlogits w5) * (hh > 0),  dz0 = (dz3 w3) * (h1 > 0 ? 1/(1-p) : 0),  dx = dz0 w0.
-// Every product is row-block x weight with <= 256 outputs per row, so a thread owns one output column
-// for RPT rows: the weight column is read once per thread (16-byte loads along a weight row for the
-// forward products; consecutive columns across lanes for the transposed backward products) and the row
-// values are LDS broadcasts.  Launch 2 (k_head_wgrad): the weight gradients on the small-GEMM tiles +
-// one workgroup reducing the per-row losses in row order.
-constexpr int HEAD_RB = 8;
+// A thread owns one output column for RPT rows: forward products read a weight row as 16-byte LDS loads
+// (row pitch = 4 mod 64 words: the 16 lanes of a ds_read_b128 group hit distinct banks), transposed
+// backward products read consecutive columns across lanes; the row values are LDS broadcasts.
+// Launch 2 (k_head_wgrad): the weight gradients on the small-GEMM tiles + one workgroup reducing the
+// per-row losses in row order.
+constexpr int HEAD_RB = 4;
 constexpr int HEAD_MAXIN = 256, HEAD_MAXH = 256, HEAD_MAXH2 = 128, HEAD_MAXC = 16;
 
 struct HeadArgs {
@@ -761,37 +757,61 @@ struct HeadArgs {
   float scale;  // 1/(1-p), or 1
 };
 
-// Y[r][o] = sum_k X[r][k] W[o][k] (W global [O][K], K % 4 == 0, rows 16-byte aligned; X in LDS, ld ldx)
-// for rows [0, RB) in groups of RPT rows; epi(r, o, acc) consumes each result.
+// LDS floats of k_head_rows for a shape (weights + row blocks, every row padded by 4 floats)
+size_t head_lds_floats(int F, int H, int H2, int C) {
+  return (size_t)H * (F + 4) + (size_t)H2 * (H + 4) + (size_t)C * (H2 + 4) +
+         (size_t)HEAD_RB * ((F + 4) + (H + 4) + (H2 + 4) + (C + 4)) + (size_t)(H + H2 + C + HEAD_RB);
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
+// stores (__syncthreads' workgroup fence waits vmcnt(0) — a full write round trip per phase of the head's
+// chain; no thread of k_head_rows reads another thread's global stores)
+TSPM_DEV void head_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Y[r][o] = sum_k X[r][k] W[o][k] (W in LDS [O][ldw], K % 4 == 0; X in LDS, ld ldx) for rows [0, RB) in
+// groups of RPT rows; epi(r, o, acc) consumes each result.
 template <int RPT, class Epi>
-TSPM_DEV void head_xwT(const float* X, int ldx, const float* __restrict__ W, int K, int O, Epi epi) {
+TSPM_DEV void head_xwT(const float* X, int ldx, const float* W, int ldw, int K, int O, Epi epi) {
   constexpr int G = HEAD_RB / RPT;
   for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
     const int o = item % O, rg = item / O;
-    const float* wp = W + (long long)o * K;
+    const float* wp = W + o * ldw;
     const float* xp = X + rg * RPT * ldx;
-    float acc[RPT];
+    // two partial sums per row (even / odd 4-element chunks of k): twice the independent FMA chains
+    float acc[RPT][2];
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
-    for (int k = 0; k < K; k += 4) {
-      const f32x4 w = ld4(wp + k);
+    for (int r = 0; r < RPT; ++r) acc[r][0] = acc[r][1] = 0.f;
+    int k = 0;
+#pragma unroll 2
+    for (; k + 8 <= K; k += 8) {
+      const f32x4 w0 = ld4(wp + k), w1 = ld4(wp + k + 4);
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
-        const f32x4 x = ld4(xp + r * ldx + k);
-        acc[r] = fmaf(x[0], w[0], acc[r]);
-        acc[r] = fmaf(x[1], w[1], acc[r]);
-        acc[r] = fmaf(x[2], w[2], acc[r]);
-        acc[r] = fmaf(x[3], w[3], acc[r]);
+        const f32x4 x0 = ld4(xp + r * ldx + k), x1 = ld4(xp + r * ldx + k + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[r][0] = fmaf(x0[j], w0[j], acc[r][0]);
+          acc[r][1] = fmaf(x1[j], w1[j], acc[r][1]);
+        }
+      }
+    }
+    if (k < K) {  // K % 8 == 4
+      const f32x4 w0 = ld4(wp + k);
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const f32x4 x0 = ld4(xp + r * ldx + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][0] = fmaf(x0[j], w0[j], acc[r][0]);
       }
     }
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) epi(rg * RPT + r, o, acc[r]);
+    for (int r = 0; r < RPT; ++r) epi(rg * RPT + r, o, acc[r][0] + acc[r][1]);
   }
 }
 
-// Y[r][o] = sum_k X[r][k] W[k][o] (W global [K][O]: consecutive o across lanes), rows in groups of RPT.
+// Y[r][o] = sum_k X[r][k] W[k][o] (W in LDS [K][ldw]: consecutive o across lanes), rows in groups of RPT.
 template <int RPT, class Epi>
-TSPM_DEV void head_xW(const float* X, int ldx, const float* __restrict__ W, int K, int O, Epi epi) {
+TSPM_DEV void head_xW(const float* X, int ldx, const float* W, int ldw, int K, int O, Epi epi) {
   constexpr int G = HEAD_RB / RPT;
   for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
     const int o = item % O, rg = item / O;
@@ -800,10 +820,11 @@ TSPM_DEV void head_xW(const float* X, int ldx, const float* __restrict__ W, int 
 #pragma unroll
     for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
     int k = 0;
+#pragma unroll 2
     for (; k + 4 <= K; k += 4) {
       float w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = W[(long long)(k + j) * O + o];
+      for (int j = 0; j < 4; ++j) w[j] = W[(k + j) * ldw + o];
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
         const f32x4 x = ld4(xp + r * ldx + k);
@@ -814,7 +835,7 @@ TSPM_DEV void head_xW(const float* X, int ldx, const float* __restrict__ W, int 
       }
     }
     for (; k < K; ++k) {
-      const float w = W[(long long)k * O + o];
+      const float w = W[k * ldw + o];
 #pragma unroll
       for (int r = 0; r < RPT; ++r) acc[r] = fmaf(xp[r * ldx + k], w, acc[r]);
     }
@@ -823,30 +844,93 @@ TSPM_DEV void head_xW(const float* X, int ldx, const float* __restrict__ W, int 
   }
 }
 
+// Staging of k_head_rows: the row block's inputs and the three weight matrices, global -> LDS (LDS rows
+// padded by 4 floats).  The first U float4 of every thread of each segment are loaded for ALL segments
+// before any LDS store, so the 134 KB of the 192 -> 128 -> 64 -> 10 head arrive in one memory round trip
+// (one load at a time left every iteration waiting a full L2 round trip: 32 us for the head; 8 at a
+// time: 20 us); larger shapes finish in further rounds.
+struct HeadSeg {
+  const float* src;
+  float* dst;
+  int rows, c4, srows;  // rows to write, float4 per row, rows present in src (the rest are zeros)
+  long long ld;          // src row pitch (floats)
+  TSPM_DEV int total() const { return rows * c4; }
+  TSPM_DEV f32x4 load(int i) const {
+    const int r = i / c4, k = i % c4;
+    return r < srows ? ld4(src + (long long)r * ld + 4 * k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  TSPM_DEV void store(int i, f32x4 v) const {
+    const int r = i / c4, k = i % c4;
+    st4(dst + r * (4 * c4 + 4) + 4 * k, v);
+  }
+};
+template <int U>
+TSPM_DEV void head_load(const HeadSeg& g, f32x4 (&v)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = u * (int)blockDim.x + (int)threadIdx.x;
+    v[u] = i < g.total() ? g.load(i) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+template <int U>
+TSPM_DEV void head_store(const HeadSeg& g, const f32x4 (&v)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = u * (int)blockDim.x + (int)threadIdx.x;
+    if (i < g.total()) g.store(i, v[u]);
+  }
+  for (int i = U * (int)blockDim.x + (int)threadIdx.x; i < g.total(); i += blockDim.x) g.store(i, g.load(i));
+}
+
 __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   const tspm_head_desc& d = a.d;
-  // LDS row blocks; leading dimensions padded by 4 floats (16-byte aligned rows, staggered banks)
-  __shared__ __attribute__((aligned(16))) float sx[HEAD_RB * (HEAD_MAXIN + 4)];
-  __shared__ __attribute__((aligned(16))) float sh1[HEAD_RB * (HEAD_MAXH + 4)];
-  __shared__ __attribute__((aligned(16))) float shh[HEAD_RB * (HEAD_MAXH2 + 4)];
-  __shared__ __attribute__((aligned(16))) float sz[HEAD_RB * (HEAD_MAXC + 4)];
+  extern __shared__ float lds[];
   const int F = d.in, H = d.hidden, H2 = d.hidden2, C = d.classes;
   const int ldx = F + 4, ldh = H + 4, ldh2 = H2 + 4, ldc = C + 4;
+  float* sw0 = lds;                      // [H][F + 4]
+  float* sw3 = sw0 + H * ldx;            // [H2][H + 4]
+  float* sw5 = sw3 + H2 * ldh;           // [C][H2 + 4]
+  float* sx = sw5 + C * ldh2;            // [RB][F + 4]
+  float* sh1 = sx + HEAD_RB * ldx;       // [RB][H + 4]
+  float* shh = sh1 + HEAD_RB * ldh;      // [RB][H2 + 4]
+  float* sz = shh + HEAD_RB * ldh2;      // [RB][C + 4]
+  float* sb0 = sz + HEAD_RB * ldc;       // biases [H], [H2], [C]; labels of the row block [RB] (as int)
+  float* sb3 = sb0 + H;
+  float* sb5 = sb3 + H2;
+  int* slab = reinterpret_cast<int*>(sb5 + C);
   const int n0 = blockIdx.x * HEAD_RB;
   const int rows = min(HEAD_RB, d.n - n0);
   const int t = threadIdx.x;
-  // stage the row block's inputs (rows past n: zeros, never stored)
-  for (int i = t; i < HEAD_RB * (F / 4); i += blockDim.x) {
-    const int r = i / (F / 4), k4 = i % (F / 4);
-    const f32x4 v = r < rows ? ld4(d.x + (long long)(n0 + r) * d.ldx + 4 * k4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    st4(sx + r * ldx + 4 * k4, v);
+  // stage the row block's inputs (rows past n: zeros, never stored) and the weights
+  {
+    const HeadSeg gx{d.x + (long long)n0 * d.ldx, sx, HEAD_RB, F / 4, rows, d.ldx};
+    const HeadSeg g0{d.w0, sw0, H, F / 4, H, F}, g3{d.w3, sw3, H2, H / 4, H2, H}, g5{d.w5, sw5, C, H2 / 4, C, H2};
+    f32x4 vx[1], v0[24], v3[8], v5[1];  // the default head: 192 x 128 (24 per thread), 128 x 64 (8), 64 x 10
+    head_load(gx, vx);
+    head_load(g0, v0);
+    head_load(g3, v3);
+    head_load(g5, v5);
+    head_store(gx, vx);
+    head_store(g0, v0);
+    head_store(g3, v3);
+    head_store(g5, v5);
+    for (int i = t; i < H + H2 + C + HEAD_RB; i += blockDim.x) {
+      if (i < H) sb0[i] = d.b0[i];
+      else if (i < H + H2) sb3[i - H] = d.b3[i - H];
+      else if (i < H + H2 + C) sb5[i - H - H2] = d.b5[i - H - H2];
+      else {  // label of row r; out-of-range labels (int64) clamp to -1 (the CE below turns them into NaN)
+        const int r = i - H - H2 - C;
+        const long long l = r < rows ? d.labels[n0 + r] : 0;
+        slab[r] = (l >= 0 && l < C) ? (int)l : -1;
+      }
+    }
   }
   uint64_t base = 0;
   if (d.p > 0.f && d.gen_keep) base = tspm_dropout_base(d.seed, d.counter ? *d.counter : 0ULL);
-  __syncthreads();
+  head_sync();
   // fc0 + ReLU + dropout (tspm_linear_fwd's epilogue order: + bias, relu, * keep*scale)
-  head_xwT<4>(sx, ldx, d.w0, F, H, [&](int r, int o, float acc) {
-    float v = relu_f(acc + d.b0[o]);
+  head_xwT<2>(sx, ldx, sw0, ldx, F, H, [&](int r, int o, float acc) {
+    float v = relu_f(acc + sb0[o]);
     if (d.p > 0.f) {
       const long long i = (long long)(n0 + r) * H + o;
       bool kp;
@@ -861,19 +945,19 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
     sh1[r * ldh + o] = v;
     if (r < rows) d.h1[(long long)(n0 + r) * H + o] = v;
   });
-  __syncthreads();
-  head_xwT<2>(sh1, ldh, d.w3, H, H2, [&](int r, int o, float acc) {
-    const float v = relu_f(acc + d.b3[o]);
+  head_sync();
+  head_xwT<1>(sh1, ldh, sw3, ldh, H, H2, [&](int r, int o, float acc) {
+    const float v = relu_f(acc + sb3[o]);
     shh[r * ldh2 + o] = v;
     if (r < rows) d.hh[(long long)(n0 + r) * H2 + o] = v;
   });
-  __syncthreads();
-  head_xwT<1>(shh, ldh2, d.w5, H2, C, [&](int r, int o, float acc) {
-    const float v = acc + d.b5[o];
+  head_sync();
+  head_xwT<1>(shh, ldh2, sw5, ldh2, H2, C, [&](int r, int o, float acc) {
+    const float v = acc + sb5[o];
     sz[r * ldc + o] = v;
     if (r < rows) d.logits[(long long)(n0 + r) * C + o] = v;
   });
-  __syncthreads();
+  head_sync();
   // cross-entropy per row (tspm_cross_entropy's arithmetic); sz becomes dlogits
   if (t < HEAD_RB) {
     float* z = sz + t * ldc;
@@ -885,9 +969,8 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
       float se = 0.f;
       for (int k = 0; k < C; ++k) se += expf(z[k] - mx);
       const float lse = logf(se);
-      const long long lab64 = d.labels[n0 + t];
-      const bool lok = lab64 >= 0 && lab64 < C;
-      const int lab = lok ? (int)lab64 : 0;
+      const bool lok = slab[t] >= 0;
+      const int lab = lok ? slab[t] : 0;
       d.row_ws[n0 + t] = lok ? lse - (z[lab] - mx) : __builtin_nanf("");
       d.row_ws[d.n + n0 + t] = (am == lab) ? 1.f : 0.f;
       const float invn = 1.0f / (float)d.n;
@@ -901,25 +984,24 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
       for (int k = 0; k < C; ++k) z[k] = 0.f;
     }
   }
-  __syncthreads();
-  // dz3 = (dlogits w5) * (hh > 0)   (w5 is [C][H2]: the transposed product) -> shh
-  head_xW<2>(sz, ldc, d.w5, C, H2, [&](int r, int o, float acc) {
+  head_sync();
+  // dz3 = (dlogits w5) * (hh > 0)   (w5 is [C][H2]: the transposed product) -> shh; item (r, o)'s hh value
+  // is read and overwritten by its own thread only
+  head_xW<1>(sz, ldc, sw5, ldh2, C, H2, [&](int r, int o, float acc) {
     const float v = shh[r * ldh2 + o] > 0.f ? acc : 0.f;
     if (r < rows) d.dz3[(long long)(n0 + r) * H2 + o] = v;
-    // every thread has read its hh value before any thread overwrites: item (r, o) is read and written
-    // by the same thread only
     shh[r * ldh2 + o] = v;
   });
-  __syncthreads();
+  head_sync();
   // dz0 = (dz3 w3) * (h1 > 0 ? scale : 0)   (w3 is [H2][H]) -> sh1
-  head_xW<4>(shh, ldh2, d.w3, H2, H, [&](int r, int o, float acc) {
+  head_xW<2>(shh, ldh2, sw3, ldh, H2, H, [&](int r, int o, float acc) {
     const float v = sh1[r * ldh + o] > 0.f ? acc * a.scale : 0.f;
     if (r < rows) d.dz0[(long long)(n0 + r) * H + o] = v;
     sh1[r * ldh + o] = v;
   });
-  __syncthreads();
+  head_sync();
   // dx = dz0 w0   (w0 is [H][F])
-  head_xW<8>(sh1, ldh, d.w0, H, F, [&](int r, int o, float acc) {
+  head_xW<4>(sh1, ldh, sw0, ldx, H, F, [&](int r, int o, float acc) {
     if (r < rows) d.dx[(long long)(n0 + r) * d.lddx + o] = acc;
   });
 }
@@ -981,7 +1063,9 @@ extern "C" int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t st
   if (d.p < 0.f || d.p >= 1.f || (d.p > 0.f && !d.keep)) return TSPM_ERR_INVALID;
   hipStream_t st = static_cast<hipStream_t>(stream);
   HeadArgs a{d, d.p > 0.f ? 1.0f / (1.0f - d.p) : 1.0f};
-  hipLaunchKernelGGL(k_head_rows, dim3(cdiv(d.n, HEAD_RB)), dim3(256), 0, st, a);
+  const size_t lds_rows = head_lds_floats(d.in, d.hidden, d.hidden2, d.classes) * sizeof(float);
+  if (lds_rows > 160 * 1024) return TSPM_ERR_INVALID;
+  hipLaunchKernelGGL(k_head_rows, dim3(cdiv(d.n, HEAD_RB)), dim3(256), lds_rows, st, a);
   TSPM_LAUNCH_CHECK();
   // weight gradients: dw[o,i] = sum_n dz[n,o] in[n,i], db[o] = sum_n dz[n,o] (tspm_linear_bwd_weight's
   // operands), plus the loss workgroup

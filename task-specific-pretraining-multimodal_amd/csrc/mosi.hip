@@ -549,7 +549,7 @@ extern "C" int tspm_textcnn_bwd(int32_t batch, int32_t steps, int32_t feat, int3
                      keep_scale, pooled, g_work);
   TSPM_LAUNCH_CHECK();
   const bool slab = channels == kWgC && feat % kWgFB == 0 && steps <= 256 &&
-                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && getenv("TSPM_TEXTCNN_WGRAD_ROWS") == nullptr;
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   if (slab) {
     for (int i = 0; i < nconv; ++i)
       if (reinterpret_cast<uintptr_t>(dw[i]) & 15) return TSPM_ERR_INVALID;

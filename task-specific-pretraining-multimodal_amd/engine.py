@@ -112,18 +112,10 @@ class BlockPlan:
     y2: torch.Tensor = None
     yd: Optional[torch.Tensor] = None
     out: torch.Tensor = None
-    # backward: per-block gradients of the conv outputs (read by the weight-grad convs, which may
-    # run on the auxiliary stream while the data-grad chain moves on to the next block)
+    # backward: per-block gradients of the conv outputs
     g_y1: torch.Tensor = None
     g_y2: torch.Tensor = None
     g_yd: Optional[torch.Tensor] = None
-    # transposed copies ([C][rows], tspm_conv_wgrad_t operands): a1, out (if a later block reads
-    # it), and the three conv-output gradients
-    a1_t: Optional[torch.Tensor] = None
-    out_t: Optional[torch.Tensor] = None
-    g_y1_t: Optional[torch.Tensor] = None
-    g_y2_t: Optional[torch.Tensor] = None
-    g_yd_t: Optional[torch.Tensor] = None
 
 
 class EncoderEngine:
@@ -135,38 +127,13 @@ class EncoderEngine:
         self.N, self.H, self.W = batch, height, width
         self.device = device
         self.grad_of = grad_of or _default_grad_of
-        # optional second stream: weight-grad convs and the downsample branch run there, off the
-        # critical path (set by FusedTrainStep; None = everything on the caller's stream)
-        self.aux: Optional[torch.cuda.Stream] = None
-        # HIP graph capture (ROCm 7) crashes in hipStreamEndCapture when a forked stream is joined
-        # into another forked stream (scripts/capture_repro.py: "nested", "nested_double_join");
-        # joins into the capture origin work.  So: fork_ds (the downsample branch, which must join
-        # back into this encoder's stream) only when this encoder runs on the origin stream, and
-        # join_aux=False lets the caller join the weight-grad stream into the origin itself.
-        self.fork_ds = True
-        self.join_aux = True
+        # Every launch goes to the caller's current stream.  (Measured and removed, DESIGN §7: weight-grad
+        # convs / the downsample branch on auxiliary streams — a replayed graph with their ~50 cross-stream
+        # edges ran ~30 % slower; BN statistics merged in two levels inside the conv (2.88 vs 2.83 ms); BN
+        # backward partials in the dgrad epilogue (conv +5 us per launch, step unchanged); bn1 + ReLU in conv2's
+        # loader (tspm_conv_fwd_bnin: step 2.73 vs 2.70 ms); transposed wgrad operands (34.7k vs 36.1k
+        # samples/s).  The ABI entry points stay, tested at the kernel level.)
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
-        # dgrad + wgrad of a conv as ONE launch (tspm_conv_bwd) when the tile pair is built in;
-        # TSPM_FUSE_BWD=0 keeps the two separate launches (A/B switch)
-        self.fuse_bwd = os.environ.get("TSPM_FUSE_BWD", "1") != "0"
-        # BN statistics of layers with many row tiles merged in two levels inside the conv launch
-        # instead of by a tspm_bn_finalize launch (TSPM_BN_TWO_LEVEL=1).  Off by default: measured at
-        # batch 128 the merge tail on the conv's critical path costs more than the finalize launch
-        # (2.88 vs 2.83 ms per step)
-        self.bn_two_level = os.environ.get("TSPM_BN_TWO_LEVEL", "0") == "1"
-        # BN-backward partial sums emitted by the producing dgrad's epilogue (small-row BatchNorms: one
-        # launch instead of partial + apply).  Opt-in (TSPM_BN_DGRAD_FUSE=1): measured at batch 128 the
-        # BN family drops 1.04 -> 0.87-0.91 ms of device time but the fused conv backward launches grow
-        # by ~5 us each (the epilogue's operand round trips sit in the split-K tail): conv 2.59 -> 2.77
-        # ms, ResNet34 3x3 at 0.133 instead of 0.149 of peak, step time unchanged (2.82 ms)
-        self.fuse_bnb = os.environ.get("TSPM_BN_DGRAD_FUSE", "0") == "1"
-        # bn1 + ReLU of every BasicBlock applied by conv2's operand loader (tspm_conv_fwd_bnin, ABI 15), which
-        # also writes the activation a1 the backward reads: one tspm_bn_apply launch (and its pass over the
-        # activation) fewer per block in the training forward; bitwise the same y2 and a1 (tested).  Opt-in
-        # (TSPM_BN_FOLD=1): measured at batch 128 the BN family drops 1.03 -> 0.94 ms of device time and
-        # 21 launches, but each folded conv2 grows by 2-5 us (image) and 4-15 us (audio) — the transform
-        # sits in the loader waves' per-stage path — so the step is slower (2.73 vs 2.70 ms)
-        self.bn_fold = os.environ.get("TSPM_BN_FOLD", "0") == "1"
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -216,25 +183,6 @@ class EncoderEngine:
         # backward phase split: the first block of layer3 (ResNet18 [2,2,2,2] -> 4, ResNet34 [3,4,6,3] -> 7)
         self.split_block = len(encoder.layer1) + len(encoder.layer2)
         self._bw_state = None
-        # weight gradients from transposed operands (16-byte loads on both GEMM operands) whenever
-        # an 8-row chunk shares one output position
-        # Off by default: measured on MI355X at batch 128 (same box, interleaved runs) the transposed
-        # copies cost the BN/maxpool kernels more than tspm_conv_wgrad_t saves once the two encoder
-        # streams overlap (34.7k vs 36.1k samples/s), although each wgrad_t launch alone is faster.
-        # TSPM_WGRAD_T=1 turns it on.
-        self.use_t = N % 8 == 0 and os.environ.get("TSPM_WGRAD_T", "0") == "1"
-        self.mp_t = None
-        if self.use_t:
-            self.mp_t = torch.empty(C0, self.mp.shape[0], **f32)
-            for i, bp in enumerate(self.blocks):
-                rows, planes = bp.out.shape
-                bp.a1_t = torch.empty(planes, rows, **f32)
-                if i + 1 < len(self.blocks):
-                    bp.out_t = torch.empty(planes, rows, **f32)
-                bp.g_y1_t = torch.empty(planes, rows, **f32)
-                bp.g_y2_t = torch.empty(planes, rows, **f32)
-                if bp.ds_conv is not None:
-                    bp.g_yd_t = torch.empty(planes, rows, **f32)
         self.pooled = torch.empty(N, c, **f32)
         self.hidden = encoder.fc.out_features
 
@@ -277,35 +225,24 @@ class EncoderEngine:
                         lib.tspm_bn_bwd_workspace(bn.rows, bn.channels))
         self.ws_conv_bytes = max(conv_ws, 256)
         self.ws_bn_bytes = max(bn_ws, 256)
-        # zero-filled once: both workspaces start with arrival counters that every call leaves zero;
-        # launches on the auxiliary stream (downsample branch, weight grads) get their own
+        # zero-filled once: the workspaces start with arrival counters that every call leaves zero; the fused
+        # backward (tspm_conv_bwd) takes a second one for its weight-gradient half
         self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
-        self.ws_conv_aux = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        self.ws_conv2 = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
-        # BN-backward partial sums written by the producing dgrad's epilogue (tspm_conv_*_bnfuse) for the
-        # small-row BatchNorms: 3 planes of [<= max_tiles][C]
-        self.bnb_max_tiles = int(lib.tspm_bn_bwd_apply_max_tiles())
-        cmax = max(bn.channels for bn in self.all_bns())
-        self.bnb_part = torch.zeros(3 * self.bnb_max_tiles * cmax, device=self.device, dtype=torch.float32)
-        # BN statistics merged in-launch (one or two levels, tspm_conv_fwd_bn_counters / _partial_floats)
-        ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
+        # BN statistics merged in-launch (tspm_conv_fwd_bn_counters / _partial_floats)
         ncnt = max(op.bn_counters() for op in self.all_convs())
-        ncnt_ds = max([op.bn_counters() for op in ds] + [1])
         self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
-        self.bn_cnt_aux = torch.zeros(ncnt_ds, device=self.device, dtype=torch.int32)
         part = max(op.bn_partial_floats() for op in self.all_convs())
         self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
-        part_ds = max([op.bn_partial_floats() for op in ds] + [1])
-        self.bn_part_aux = torch.empty(part_ds, device=self.device, dtype=torch.float32)
 
     def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
         """Override tile configs: key (kind, n,h,w,c,k,r,s,stride) -> (tm, tn, wm, wn, splits)."""
         for op in self.all_convs():
             s = op.shape
             base = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride)
-            wkind = "wgrad_t" if (self.use_t and op is not self.stem) else "wgrad"
             tuned_bwd = False
-            for kind, key in (("fwd", "fwd"), ("dgrad", "dgrad"), ("wgrad", wkind)):
+            for kind, key in (("fwd", "fwd"), ("dgrad", "dgrad"), ("wgrad", "wgrad")):
                 v = table.get((key,) + base)
                 if v is not None:
                     setattr(op, f"algo_{kind}", L.ConvAlgo(*v))
@@ -327,10 +264,10 @@ class EncoderEngine:
         return w
 
     def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                  bnf: Optional[L.BnFuse] = None, aux: bool = False) -> None:
+                  bnf: Optional[L.BnFuse] = None) -> None:
         lib = L.lib()
         s, a = op.shape, op.algo_fwd
-        ws = self.ws_conv_aux if aux else self.ws_conv
+        ws = self.ws_conv
         if self.conv_timer:
             self.conv_timer.begin(op, "fwd")
         L.check(lib.tspm_conv_fwd(ctypes.byref(s), ctypes.byref(a), x_ptr, ctypes.byref(strides), self._w(op).data_ptr(),
@@ -339,44 +276,18 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
-    def _bnf(self, bn: BNOp, aux: bool = False) -> L.BnFuse:
+    def _bnf(self, bn: BNOp) -> L.BnFuse:
         m = bn.module
-        part, cnt = (self.bn_part_aux, self.bn_cnt_aux) if aux else (self.bn_part, self.bn_cnt)
-        return L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
+        return L.BnFuse(self.bn_part.data_ptr(), self.bn_cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
                         BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                        bn.invstd.data_ptr(), cnt.numel() if self.bn_two_level else 0, 0,
-                        part.numel() if self.bn_two_level else 0)
+                        bn.invstd.data_ptr(), 0, 0, 0)
 
-    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                 aux: bool = False) -> None:
+    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
         """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
         per channel block, merges them (save_mean/invstd + running statistics): one launch."""
-        self._conv_fwd(op, x_ptr, strides, y, sh, self._bnf(bn, aux), aux)
+        self._conv_fwd(op, x_ptr, strides, y, sh, self._bnf(bn))
 
-    def _can_fold(self, op: ConvOp) -> bool:
-        """conv2 of a block may take bn1 + ReLU in its operand loader (tspm_conv_fwd_bnin)."""
-        s = op.shape
-        return (self.bn_fold and not self.use_t and op.algo_fwd.variant == 1 and s.stride == 1
-                and s.r == s.s == 3 and s.pad == 1)
-
-    def _conv_bn_in(self, op: ConvOp, bn: BNOp, bn_in: BNOp, y_in: torch.Tensor, a_out: torch.Tensor,
-                    strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
-        """_conv_bn whose input operand is relu(bn_in(y_in)), formed by the loader; a_out receives it."""
-        m = bn_in.module
-        bi = L.BnInput(bn_in.mean.data_ptr(), bn_in.invstd.data_ptr(), m.weight.data_ptr(), m.bias.data_ptr(),
-                       a_out.data_ptr())
-        bnf = self._bnf(bn)
-        s, a = op.shape, op.algo_fwd
-        if self.conv_timer:
-            self.conv_timer.begin(op, "fwd")
-        L.check(L.lib().tspm_conv_fwd_bnin(ctypes.byref(s), ctypes.byref(a), y_in.data_ptr(), ctypes.byref(strides),
-                                           self._w(op).data_ptr(), y.data_ptr(), ctypes.byref(bnf), ctypes.byref(bi),
-                                           self.ws_conv.data_ptr(), self.ws_conv_bytes, sh), "conv_fwd_bnin")
-        if self.conv_timer:
-            self.conv_timer.end()
-
-    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
-               out_t: Optional[torch.Tensor] = None):
+    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True):
         lib = L.lib()
         m = bn.module
         if train:
@@ -384,8 +295,7 @@ class EncoderEngine:
                                       m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res),
                                       L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
                                       L.ptr(bn2.module.weight) if bn2 else None, L.ptr(bn2.module.bias) if bn2 else None,
-                                      1 if relu else 0, out.data_ptr(), L.ptr(out_t),
-                                      bn.rows if out_t is not None else 0, sh), "bn_apply")
+                                      1 if relu else 0, out.data_ptr(), None, 0, sh), "bn_apply")
         else:
             m2 = bn2.module if bn2 else None
             L.check(lib.tspm_bn_apply_eval(bn.rows, bn.channels, y.data_ptr(), m.running_mean.data_ptr(),
@@ -435,52 +345,33 @@ class EncoderEngine:
         if train:
             self._conv_bn(self.stem, self.stem_bn, x.data_ptr(), xs, self.y0, sh)
         else:
-            self._conv_fwd_eval(self.stem, x.data_ptr(), xs, self.y0, sh)
+            self._conv_fwd(self.stem, x.data_ptr(), xs, self.y0, sh)
         self._apply(self.stem_bn, self.y0, self.a0, relu=True, sh=sh, train=train)
-        mp_t = self.mp_t if train else None
         L.check(lib.tspm_maxpool_fwd(N, p1, q1, C0, 3, 2, 1, p2, q2, self.a0.data_ptr(), self.mp.data_ptr(),
-                                     self.mp_idx.data_ptr(), L.ptr(mp_t), self.mp.shape[0] if mp_t is not None else 0,
-                                     sh), "maxpool_fwd")
+                                     self.mp_idx.data_ptr(), None, 0, sh), "maxpool_fwd")
         xin = self.mp
         for bp in self.blocks:
             s1 = bp.conv1.shape
             xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
-            fork = bp.ds_conv is not None and self.aux is not None and self.fork_ds
-            if fork:  # downsample conv + BN statistics concurrently with conv1 -> bn1 -> conv2
-                main = torch.cuda.current_stream()
-                self.aux.wait_stream(main)
-                with torch.cuda.stream(self.aux):
-                    ash = self.aux.cuda_stream
-                    if train:
-                        self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, ash, aux=True)
-                    else:
-                        self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, ash, aux=True)
             if train:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
-                self._conv_fwd_eval(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
+                self._conv_fwd(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
-            if train and self._can_fold(bp.conv2):
-                self._conv_bn_in(bp.conv2, bp.bn2, bp.bn1, bp.y1, bp.a1, xs_a1, bp.y2, sh)
-            elif train:
-                self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train, out_t=bp.a1_t)
+            self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
+            if train:
                 self._conv_bn(bp.conv2, bp.bn2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             else:
-                self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
-                self._conv_fwd_eval(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
+                self._conv_fwd(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             if bp.ds_conv is not None:
-                if fork:
-                    main.wait_stream(self.aux)
-                elif train:
+                if train:
                     self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
                 else:
-                    self._conv_fwd_eval(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train,
-                            out_t=bp.out_t if train else None)
+                    self._conv_fwd(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train)
             else:
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train,
-                            out_t=bp.out_t if train else None)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train)
             xin = bp.out
         h, w = self.final_hw
         L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh), "avgpool_fwd")
@@ -489,16 +380,11 @@ class EncoderEngine:
                                     fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb, sh),
                 "linear_fwd(fc)")
 
-    def _conv_fwd_eval(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
-                       aux: bool = False) -> None:
-        self._conv_fwd(op, x_ptr, strides, y, sh, None, aux)
-
     # ---------------------------------------------------------------------------------------
     def _grad(self, p: torch.Tensor) -> torch.Tensor:
         return self.grad_of(p)
 
-    def _bn_bwd(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None, sh=0,
-                dy_t=None, dy2_t=None):
+    def _bn_bwd(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None, sh=0):
         lib = L.lib()
         m = bn.module
         gw, gb = self._grad(m.weight), self._grad(m.bias)
@@ -509,73 +395,27 @@ class EncoderEngine:
                                 bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
                                 L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
                                 L.ptr(bn2.module.weight) if bn2 else None, L.ptr(gw2) if bn2 else None,
-                                L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), L.ptr(dy_t), L.ptr(dy2_t),
-                                bn.rows if dy_t is not None else 0, self.ws_bn.data_ptr(), self.ws_bn_bytes, sh),
-                "bn_bwd")
+                                L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), None, None, 0,
+                                self.ws_bn.data_ptr(), self.ws_bn_bytes, sh), "bn_bwd")
 
-    def _bn_bwd_apply(self, bn: BNOp, tiles: int, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None,
-                      dres=None, sh=0):
-        """tspm_bn_bwd with the partial sums already written by the producing dgrad (one launch)."""
-        m = bn.module
-        gw, gb = self._grad(m.weight), self._grad(m.bias)
-        m2 = bn2.module if bn2 is not None else None
-        gw2, gb2 = (self._grad(m2.weight), self._grad(m2.bias)) if m2 is not None else (None, None)
-        L.check(L.lib().tspm_bn_bwd_apply(
-            bn.rows, bn.channels, tiles, self.bnb_part.data_ptr(), g.data_ptr(), L.ptr(out_mask), y.data_ptr(),
-            bn.mean.data_ptr(), bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
-            L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
-            L.ptr(m2.weight) if m2 is not None else None, L.ptr(gw2), L.ptr(gb2), L.ptr(dy2), L.ptr(dres), sh),
-            "bn_bwd_apply")
-
-    def _bnb_for(self, op: ConvOp, out_mask, y, bn: BNOp, y2=None, bn2: Optional[BNOp] = None):
-        """(tspm_bn_bwd_fuse, tiles) when op's dgrad can emit bn's backward partial sums in its epilogue
-        (LDS-staged dgrad with <= max_tiles row tiles), else None."""
-        if not self.fuse_bnb or self.use_t:
-            return None
-        tiles = int(L.lib().tspm_conv_dgrad_bn_tiles(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad)))
-        if not (0 < tiles <= self.bnb_max_tiles):
-            return None
-        f = L.BnBwdFuse(self.bnb_part.data_ptr(), L.ptr(out_mask), y.data_ptr(), bn.mean.data_ptr(), L.ptr(y2),
-                        L.ptr(bn2.mean) if bn2 is not None else None)
-        return f, tiles
-
-    def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int,
-               x_t: Optional[torch.Tensor] = None, dy_t: Optional[torch.Tensor] = None) -> None:
-        lib = L.lib()
+    def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int) -> None:
         gw = self._grad(op.module.weight)
         if not gw.is_contiguous(memory_format=torch.channels_last):
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
-        if self.aux is not None:  # off the critical path: only Adam consumes weight gradients
-            self.aux.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.aux):
-                self._wgrad_launch(op, x_ptr, strides, dy, gw, self.aux.cuda_stream, x_t, dy_t, self.ws_conv_aux)
-        else:
-            self._wgrad_launch(op, x_ptr, strides, dy, gw, sh, x_t, dy_t, self.ws_conv)
-
-    def _wgrad_launch(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, gw: torch.Tensor,
-                      sh: int, x_t: Optional[torch.Tensor], dy_t: Optional[torch.Tensor], ws: torch.Tensor) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "wgrad")
-        lib = L.lib()
-        if x_t is not None and dy_t is not None:
-            L.check(lib.tspm_conv_wgrad_t(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_t.data_ptr(),
-                                          x_t.shape[1], dy_t.data_ptr(), dy_t.shape[1], gw.data_ptr(),
-                                          ws.data_ptr(), self.ws_conv_bytes, sh), "conv_wgrad_t")
-        else:
-            L.check(lib.tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr,
-                                        ctypes.byref(strides), dy.data_ptr(), gw.data_ptr(), ws.data_ptr(),
-                                        self.ws_conv_bytes, sh), "conv_wgrad")
+        L.check(L.lib().tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides),
+                                        dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh),
+                "conv_wgrad")
         if self.conv_timer:
             self.conv_timer.end()
 
     def _bwd_pair(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, dx: torch.Tensor, beta: int,
-                  sh: int, bnb=None) -> bool:
+                  sh: int) -> bool:
         """Input and weight gradient of ``op`` in one launch (tspm_conv_bwd: the two GEMMs read the same
-        dy and are independent, so their workgroups share the grid).  False (nothing launched) when
-        the pair is not built in, an auxiliary stream carries the weight gradients, or the transposed
-        wgrad operands are in use; the caller then launches the two separately."""
-        if not self.fuse_bwd or self.aux is not None or self.use_t:
-            return False
+        dy and are independent, so their workgroups share the grid).  False (nothing launched) when the
+        pair is not built in or the tuner found the two separate launches faster; the caller then launches
+        the two separately."""
         lib = L.lib()
         if op.bwd_fused is None:
             op.bwd_fused = bool(lib.tspm_conv_bwd_supported(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
@@ -587,32 +427,20 @@ class EncoderEngine:
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
         if self.conv_timer:
             self.conv_timer.begin(op, "bwd")
-        if bnb is not None:
-            L.check(lib.tspm_conv_bwd_bnfuse(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
-                                             ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides), dy.data_ptr(),
-                                             self._w(op).data_ptr(), dx.data_ptr(), beta, gw.data_ptr(),
-                                             self.ws_conv.data_ptr(), self.ws_conv_bytes, self.ws_conv_aux.data_ptr(),
-                                             self.ws_conv_bytes, ctypes.byref(bnb), sh), "conv_bwd_bnfuse")
-        else:
-            L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
-                                      x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
-                                      beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
-                                      self.ws_conv_aux.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
+        L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
+                                  x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
+                                  beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
+                                  self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
         if self.conv_timer:
             self.conv_timer.end()
         return True
 
-    def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int, bnb=None) -> None:
+    def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "dgrad")
-        if bnb is not None:
-            L.check(L.lib().tspm_conv_dgrad_bnfuse(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
-                                                   self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
-                                                   self.ws_conv_bytes, ctypes.byref(bnb), sh), "conv_dgrad_bnfuse")
-        else:
-            L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
-                                            self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
-                                            self.ws_conv_bytes, sh), "conv_dgrad")
+        L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
+                                        self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
+                                        self.ws_conv_bytes, sh), "conv_dgrad")
         if self.conv_timer:
             self.conv_timer.end()
 
@@ -657,9 +485,8 @@ class EncoderEngine:
             L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(),
                                          sh), "avgpool_bwd")
             lo, hi = (self.split_block if phase == 1 else 0), len(self.blocks)
-            pend = None  # row tiles of the block-output BN's partial sums, written by the previous dgrad
         else:
-            G, Gn, pend = self._bw_state
+            G, Gn = self._bw_state
             lo, hi = 0, self.split_block
         for i in range(hi - 1, lo - 1, -1):
             bp = self.blocks[i]
@@ -673,59 +500,34 @@ class EncoderEngine:
             d2 = bp.g_y2
             if bp.ds_conv is not None:
                 dd = bp.g_yd
-                if pend is not None:
-                    self._bn_bwd_apply(bp.bn2, pend, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
-                else:
-                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh,
-                                 dy_t=bp.g_y2_t, dy2_t=bp.g_yd_t)
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
-                if pend is not None:
-                    self._bn_bwd_apply(bp.bn2, pend, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
-                else:
-                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh, dy_t=bp.g_y2_t)
-            pend = None
+                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
-            # conv2's input gradient is bn1's whole gradient: its epilogue emits bn1's backward partials
-            fb1 = self._bnb_for(bp.conv2, bp.a1, bp.y1, bp.bn1)
-            bnb1 = fb1[0] if fb1 else None
-            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, bnb1):
-                self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh, bp.a1_t, bp.g_y2_t)
-                self._dgrad(bp.conv2, d2, da1, 0, sh, bnb1)
+            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh):
+                self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh)
+                self._dgrad(bp.conv2, d2, da1, 0, sh)
             d1 = bp.g_y1
-            if fb1:
-                self._bn_bwd_apply(bp.bn1, fb1[1], da1, bp.a1, bp.y1, d1, sh=sh)
-            else:
-                self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh, dy_t=bp.g_y1_t)
+            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
             if self.debug_hook is not None:
                 self.debug_hook(f"block{i}.g_out", Gv)
                 self.debug_hook(f"block{i}.d_y2", d2)
                 self.debug_hook(f"block{i}.d_a1", da1)
                 self.debug_hook(f"block{i}.d_y1", d1)
-            xin_t = (self.blocks[i - 1].out_t if i > 0 else self.mp_t) if self.use_t else None
             # the downsample's input gradient overwrites Gnv before conv1's accumulates onto it
             if bp.ds_conv is not None and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
-                self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh, xin_t, bp.g_yd_t)
+                self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
-            # conv1's input gradient accumulates last onto the previous block's output gradient: its epilogue
-            # emits that block's bn2 (+ downsample BN) backward partials
-            fb2 = None
-            if i > 0:
-                pb = self.blocks[i - 1]
-                fb2 = self._bnb_for(bp.conv1, pb.out, pb.y2, pb.bn2, pb.yd if pb.ds_conv is not None else None,
-                                    pb.ds_bn if pb.ds_conv is not None else None)
-            bnb2 = fb2[0] if fb2 else None
-            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, bnb2):
-                self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh, xin_t, bp.g_y1_t)
-                self._dgrad(bp.conv1, d1, Gnv, 1, sh, bnb2)
-            pend = fb2[1] if fb2 else None
+            # conv1's input gradient accumulates last onto the previous block's output gradient
+            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh):
+                self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
+                self._dgrad(bp.conv1, d1, Gnv, 1, sh)
             G, Gn = Gn, G
         if phase == 1:
-            self._bw_state = (G, Gn, pend)
-            if self.aux is not None and self.join_aux:
-                torch.cuda.current_stream().wait_stream(self.aux)
+            self._bw_state = (G, Gn)
             return
         # stem: maxpool -> relu/bn -> conv1 (weight grad only)
         p1, q1, p2, q2 = self.mp_shape
@@ -734,8 +536,6 @@ class EncoderEngine:
                                      self.g_stem.data_ptr(), sh), "maxpool_bwd")
         self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
         self._wgrad(self.stem, self.x_in.data_ptr(), self.input_strides(self.x_in), self.dy_stem, sh)
-        if self.aux is not None and self.join_aux:
-            torch.cuda.current_stream().wait_stream(self.aux)
 
 
 def _default_grad_of(p: torch.Tensor) -> torch.Tensor:

@@ -34,16 +34,15 @@ from .optim import FusedAdam
 from .step import shared_batches_tracked
 
 _BN_MOMENTUM_DEFAULT = 0.1
-# TSPM_MMIMDB_FUSE=1: BatchNorm1d backward + MaxOut backward in one launch (tspm_bn1d_bwd_maxout, bitwise
-# equal).  Off by default: measured 618k vs 653k samples/s at batch 256 — the BN kernel's 8 workgroups
-# (64 channels each) take on the routing that the wide element-wise kernel spreads over the chip.
-_FUSE_BN_MAXOUT = os.environ.get("TSPM_MMIMDB_FUSE", "0") == "1"
-# TSPM_MMIMDB_PAIRS=0: the independent image / text launches (input BatchNorm1d forward and backward, the
-# GMU projections) as separate launches instead of merged pairs (A/B; bitwise equal)
-_PAIRS = os.environ.get("TSPM_MMIMDB_PAIRS", "1") != "0"
-# TSPM_MMIMDB_RNG=0: draw the dropout masks with a separate tspm_dropout_mask launch instead of inside the
-# MaxOut forwards (tspm_maxout_fwd_rng; same bits — A/B switch for that fusion alone)
-_RNG_INLAUNCH = os.environ.get("TSPM_MMIMDB_RNG", "1") != "0"
+# BatchNorm1d backward + MaxOut backward in one launch (tspm_bn1d_bwd_maxout, bitwise equal) measured slower:
+# 618k vs 653k samples/s at batch 256 — the BN kernel's 8 workgroups (64 channels each) take on the routing
+# that the wide element-wise kernel spreads over the chip.  Off.
+_FUSE_BN_MAXOUT = False
+# the independent image / text launches (input BatchNorm1d forward and backward, the GMU projections) as
+# merged pairs (bitwise the separate launches; 665-670k -> 756k samples/s)
+_PAIRS = True
+# dropout masks drawn inside the MaxOut forwards (tspm_maxout_fwd_rng; the bits of tspm_dropout_mask)
+_RNG_INLAUNCH = True
 
 
 # ------------------------------------------------------------------------------------------------
@@ -222,17 +221,15 @@ class MMIMDbEngine:
             self.keep_pool = torch.ones(n, 2 * d, dtype=torch.uint8, device=device)
             self.pool_keep_override: Optional[torch.Tensor] = None
         self.dXn, self.dXnT = z(n, self.di), z(n, self.dt)
-        # TSPM_MMIMDB_STREAMS=2: text branch on a side stream (forward: text encoder + fc_two; backward:
-        # their gradients), joined by events before the gate / at the end of the backward.  Measured
-        # (graph replay): 0.4385 vs 0.4278 ms at batch 256, 0.373 vs 0.365 at 128, 0.859 vs 0.876 at
-        # 1024 — the two stream edges cost about what the overlap saves, so one stream is the default.
-        self.side = torch.cuda.Stream(device) if os.environ.get("TSPM_MMIMDB_STREAMS", "1") == "2" else None
+        # one stream: the text branch on a side stream measured 0.4385 vs 0.4278 ms at batch 256, 0.373 vs
+        # 0.365 at 128, 0.859 vs 0.876 at 1024 — the two stream edges cost about what the overlap saves
+        self.side = None
         self.keep = torch.ones(2, n, h, dtype=torch.uint8, device=device)
         widths = (self.di, self.dt, d, h)
         self.stat = {k: (z(w), z(w)) for k, w in zip(("i", "t", "b0", "b1", "b2"), widths + (h,))}
         self.stats = z(3 + 3 * c)
         # split-K for the long encoder Linear when its output tiles cannot fill the chip
-        self.enc_splits = int(os.environ.get("TSPM_MMIMDB_SPLITK", "4"))
+        self.enc_splits = 4
         tiles = -(-n // 32) * -(-e // 32)
         if self.di < 2048 or tiles >= 256:
             self.enc_splits = 1

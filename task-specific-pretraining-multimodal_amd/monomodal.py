@@ -234,7 +234,6 @@ class FusedMonoStep(_MonoBuffers):
         sh = torch.cuda.current_stream().cuda_stream
         n, hid, K = self.N, self.hid, self.K
         cls = self.model.classifier
-        self.eng.aux = None
         self.eng.forward(self.X, self.emb, hid, train=True, bump_batches_tracked=False)
         L.check(lib.tspm_linear_fwd(n, hid, K, self.emb.data_ptr(), hid, cls.weight.data_ptr(), cls.bias.data_ptr(), 0,
                                     None, 1.0, self.logits.data_ptr(), K, sh), "classifier fwd")
@@ -279,7 +278,6 @@ class FusedMonoEvalStep(_MonoBuffers):
         sh = torch.cuda.current_stream().cuda_stream
         n, hid, K = self.N, self.hid, self.K
         cls = self.model.classifier
-        self.eng.aux = None
         self.eng.forward(self.X, self.emb, hid, train=False)
         L.check(lib.tspm_linear_fwd(n, hid, K, self.emb.data_ptr(), hid, cls.weight.data_ptr(), cls.bias.data_ptr(), 0,
                                     None, 1.0, self.logits.data_ptr(), K, sh), "eval classifier")

@@ -175,7 +175,6 @@ class FusedTrainStep:
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
         side = main if self.serial else self.side
-        self.eng_a.aux = self.eng_i.aux = None
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
@@ -236,7 +235,6 @@ class FusedTrainStep:
         eager = not self.use_graph or self.calls == 0
         if getattr(self, "_marks", None) is None:
             self._marks = (L.DeviceFlag(), L.DeviceFlag())
-        self.eng_i.fork_ds = self.eng_a.fork_ds = False
         if eager:
             self._fwd_bwd(marks=self._marks)
         else:
@@ -401,8 +399,6 @@ class FusedEvalStep:
         lib = L.lib()
         main = torch.cuda.current_stream()
         ea = self.model.embd_size_A
-        for e in (self.eng_a, self.eng_i):
-            e.aux = None
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=False)

@@ -395,24 +395,6 @@ def test_linear_backward_large_vs_fp64(gpu, n, k, o):
     assert rel_l2(dx, dy.double() @ w.double()) < 1e-5
 
 
-def test_two_stream_step_equals_one_stream(gpu, monkeypatch):
-    """TSPM_MMIMDB_STREAMS=2 (text branch on a side stream) computes the same step bitwise."""
-    n = 64
-    a, _, sa, _, _ = _setup(gpu, n)
-    monkeypatch.setenv("TSPM_MMIMDB_STREAMS", "2")
-    b, _, sb, _, _ = _setup(gpu, n)
-    assert sb.eng.side is not None and sa.eng.side is None
-    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=12))
-    for s in range(3):
-        keep = _keep(n, 60 + s).to(gpu)
-        sa.keep_override, sb.keep_override = keep, keep
-        sa.step(I, T, y)
-        sb.step(I, T, y)
-    torch.cuda.synchronize()
-    for (na, pa), (_, pb) in zip(a.state_dict().items(), b.state_dict().items()):
-        assert torch.equal(pa, pb), na
-
-
 def test_rccl_allreduce_step_equals_plain_step(gpu):
     """The DP path of the MMIMDb step (captured fwd/bwd graph | RCCL all-reduce of the flat gradient |
     Adam) under a 1-rank RCCL group (all-reduce = identity) gives bitwise the plain step's parameters."""
@@ -467,61 +449,6 @@ def test_linear_bwd_pair_bitwise_equals_two_launches(gpu, n, fin, fout):
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
     assert rel_l2(out[0][2], dy.double() @ w.double()) < 1e-5
-
-
-def test_fused_bn_maxout_backward_equals_separate(gpu, monkeypatch):
-    """tspm_bn1d_bwd_maxout (BatchNorm1d backward + MaxOut/Dropout backward in one launch) gives bitwise
-    the step of the separate tspm_bn1d_bwd + tspm_maxout_bwd launches."""
-    n, res = 96, []
-    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=14))
-    for fuse in (True, False):
-        monkeypatch.setattr(M, "_FUSE_BN_MAXOUT", fuse)
-        ours, _, st, _, _ = _setup(gpu, n)
-        for s in range(3):
-            st.keep_override = _keep(n, 80 + s).to(gpu)
-            st.step(I, T, y)
-        torch.cuda.synchronize()
-        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
-    assert torch.equal(res[0], res[1])
-
-
-def test_paired_launches_equal_separate(gpu, monkeypatch):
-    """Merged image/text launch pairs (tspm_bn1d_fwd_pair / _bwd_pair, tspm_linear_fwd_pair) give bitwise
-    the step of the separate launches."""
-    n, res = 64, []
-    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=15))
-    for pairs in (True, False):
-        monkeypatch.setattr(M, "_PAIRS", pairs)
-        ours, _, st, _, _ = _setup(gpu, n)
-        for s in range(3):
-            st.keep_override = _keep(n, 90 + s).to(gpu)
-            st.step(I, T, y)
-        torch.cuda.synchronize()
-        ours.eval()
-        ev = ours(I, T)
-        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]
-                             + [ev.reshape(-1).cpu()]))
-    assert torch.equal(res[0], res[1])
-
-
-def test_inlaunch_dropout_masks_equal_mask_kernel(gpu, monkeypatch):
-    """tspm_maxout_fwd_rng draws exactly the keep bits tspm_dropout_mask writes: the step with in-launch
-    masks equals bitwise the step with the separate mask launch (TSPM_MMIMDB_RNG=0: only that fusion
-    differs between the two runs)."""
-    n, res, masks = 64, [], []
-    I, T, y = (t.to(gpu) for t in orc.synthetic_batch(n, seed=16))
-    for rng in (True, False):
-        monkeypatch.setattr(M, "_RNG_INLAUNCH", rng)
-        ours, _, st, _, _ = _setup(gpu, n)
-        ours._rng_seed = 12345
-        for s in range(3):
-            st.step(I, T, y)
-            masks.append(st.eng.keep.clone())
-        torch.cuda.synchronize()
-        res.append(torch.cat([v.detach().reshape(-1).float().cpu() for v in ours.state_dict().values()]))
-    assert torch.equal(res[0], res[1])
-    for a, b in zip(masks[:3], masks[3:]):
-        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("n,h,ctr", [(37, 53, 5), (64, 512, 0), (3, 7, 123456789)])

@@ -244,12 +244,9 @@ def _bn_ref_block(y, y2, gamma, beta, gamma2, beta2, res, mode, relu):
 @pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (384, 512), (24576, 64), (1536, 256), (100, 8),
                                  (96256, 64)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("fused", [True, False])
-def test_bn_block_fwd_bwd(gpu, m, c, mode, fused, monkeypatch):
-    """BN apply + backward against float64 autograd; the backward both as the single launch with the
-    in-launch barrier (fused) and as the two-launch partial / apply pair."""
+def test_bn_block_fwd_bwd(gpu, m, c, mode):
+    """BN apply + backward (the two-launch partial / apply pair) against float64 autograd."""
     from tspm_amd import _lib as L
-    monkeypatch.setenv("TSPM_BN_BWD_FUSED", "1" if fused else "0")
     lib = L.lib()
     g = torch.Generator().manual_seed(5)
     y = torch.randn(m, c, generator=g) * 3 + 1
