@@ -230,6 +230,31 @@ def pmc_traffic(family: str = "conv", path: str = "main"):
     return fam["total"], fam.get("launches"), os.path.relpath(files[-1], REPO)
 
 
+def mfma_counters(batch: int):
+    """The conv family's MFMA-busy / wave-state PMC counters at this batch from the newest committed summary
+    (profiles/r<round>_b<batch>_mfma_busy.json, scripts/pmc_mfma.sh + pmc_mfma.py over this bench command):
+    MFMA pipe utilisation and where the conv waves' cycles go.  None if no summary for this batch."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_b{batch}_mfma_busy.json")),
+                   key=lambda p: int(re.search(r"r(\d+)_b", os.path.basename(p)).group(1)))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    c = d.get("families", {}).get("conv")
+    if not c:
+        return None
+    waits = {"frac_wait_inst_any": c["frac_wait_inst_any"], "frac_wait_any": c["frac_wait_any"],
+             "frac_active_inst": c["frac_active_inst"]}
+    return {"source": os.path.relpath(files[-1], REPO), "batch": batch,
+            "mfma_busy_cycles_per_step": c["mfma_busy_cycles"] / max(1, d.get("steps_in_run", 1)),
+            "mfma_util": c["mfma_util_at_2p4GHz"], "mfma_util_at_measured_clock": c["mfma_util_at_measured_clock"],
+            "wave_state": waits, "capping_state": max(waits, key=waits.get),
+            "what": "SQ_VALU_MFMA_BUSY_CYCLES over the conv kernels' device time x 256 CUs x 4 SIMDs x clock "
+                    "(64 busy cycles per f32 32x32x2 MFMA); wave_state = fractions of SQ_WAVE_CYCLES"}
+
+
 def mmimdb_flops_per_sample(di=4096, dt=300, e=512, d=512, h=512, c=23):
     """Algorithmic train FLOPs per sample of the MMIMDb step: 2 x MACs of forward + data-grad + weight-grad
     of every product (the encoder Linears' data-grad feeds the input BatchNorm1d's gamma/beta gradients)."""
@@ -248,7 +273,6 @@ def mmimdb_bench(args) -> None:
     import tspm_amd
     from tspm_amd import mmimdb as M
     from tspm_amd.roofline import FP32_MFMA_PEAK_TFLOPS
-    from oracle import mmimdb_ref as orc
     from tspm_amd import ddp
     rank, world, local = ddp.init_from_env("nccl")
     dev = torch.device("cuda", local)
@@ -271,7 +295,7 @@ def mmimdb_bench(args) -> None:
             dist.broadcast(fg.param, src=0)
         allreduce = ddp.GradAllReduce([fg.grad for fg in opt.flat_groups()])
     st = M.FusedMMIMDbStep(model, opt, None, B, allreduce=allreduce)
-    batches = [tuple(t.to(dev) for t in orc.synthetic_batch(B, seed=1234 + 100 * rank + i)) for i in range(16)]
+    batches = [tuple(t.to(dev) for t in M.synthetic_features(B, seed=1234 + 100 * rank + i)) for i in range(16)]
 
     def one(i):
         I, T, y = batches[i % len(batches)]
@@ -318,6 +342,7 @@ def mmimdb_bench(args) -> None:
                         "flop_per_sample": fps, "adam_bytes_per_step": 28 * nparam},
            "final_loss": round(st.eng.loss.item(), 5), "process_group": process_group_info()}
     if not args.no_cpu_baseline and rank == 0:
+        from oracle import mmimdb_ref as orc
         from oracle.avmnist_ref import OracleAdam
         threads, hcpu = cpu_threads()
         torch.set_num_threads(threads)
@@ -1066,9 +1091,13 @@ def main() -> None:
     # ---- secondary: the PCIe-inclusive step (a pinned host batch copied H2D each step) -----------
     pcie = None
     if args.pcie_steps > 0:
-        from oracle import avmnist_ref as orc_in  # synthetic batch generator only (input data, untimed)
-        ha, hi, hl, _ = orc_in.synthetic_batch(B, seed=4321 + rank)
-        ha, hi, hl = ha.pin_memory(), hi.pin_memory(), hl.pin_memory()
+        import numpy as np
+        from tspm_amd.data import default_lut, synthetic_corpus
+        hc = synthetic_corpus(B, seed=4321 + rank)  # a host batch in the collated layout (input data, untimed)
+        lut = default_lut().astype(np.float32) * np.float32(1.0 / 255.0)
+        ha = torch.from_numpy(hc.audio).pin_memory()
+        hi = torch.from_numpy(lut[hc.image.astype(np.int64)]).reshape(B, 1, 28, 28).pin_memory()
+        hl = torch.from_numpy(hc.labels).pin_memory()
 
         def one_h2d():
             step.A.copy_(ha, non_blocking=True)
@@ -1120,6 +1149,7 @@ def main() -> None:
                 r34["what"] = ("ResNet34 (image encoder) 3x3 convs: fwd + dgrad + wgrad launches, valid-tap FLOPs / "
                                "their device time (north_star target >= 0.70)")
             rl["r34_3x3"] = r34
+            rl["mfma_counters"] = {f"b{b}": mfma_counters(b) for b in sorted({B, 128, 1024})}
             # the HBM-bound families: algorithmic bytes per step, PMC HBM bytes per step and the
             # achieved rate over their device time (same replays as above)
             bn_elems = 217728 * B  # BN(+ReLU/+add) elements per step (both encoders)

@@ -34,6 +34,18 @@
 #define TSPM_LDS_IMPL lds_impl_reg
 #endif
 
+#if defined(TSPM_STAMPS) && defined(TSPM_LDS_SECONDARY)
+// the second build of this file (variant 2) records no stamps: its kernels cannot reach the first build's
+// buffer without -fgpu-rdc (a separate buffer + readback would be needed to stamp variant 2)
+#undef TSPM_STAMP
+#define TSPM_STAMP(buf, slot) \
+  do {                        \
+  } while (0)
+#undef TSPM_STAMP_CLK
+#define TSPM_STAMP_CLK(buf, slot) \
+  do {                            \
+  } while (0)
+#endif
 #if defined(TSPM_STAMPS) && !defined(TSPM_LDS_SECONDARY)
 __device__ unsigned long long tspm_g_stamps_lds[TSPM_STAMP_WAVES * TSPM_STAMP_SLOTS];
 extern "C" int tspm_debug_stamps_lds(void* host_dst, size_t bytes) {

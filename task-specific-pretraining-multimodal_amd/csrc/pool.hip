@@ -18,16 +18,35 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(int N, int H, int W, int C,
     const int p = pos / Q, q = pos - p * Q;
     f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int bi[4] = {0, 0, 0, 0};
-    for (int kh = 0; kh < k; ++kh) {
-      const int h = p * st - pad + kh;
-      if (h < 0 || h >= H) continue;
-      for (int kw = 0; kw < k; ++kw) {
-        const int w = q * st - pad + kw;
-        if (w < 0 || w >= W) continue;
-        const f32x4 v = ld4(x + (((long long)h * W + w) * N + n) * C + 4 * c4);
+    if (k == 3) {
+      // the ResNet stem pool: all nine window loads in flight before the compares (a load per `continue`d
+      // iteration waited for each tap in turn); out-of-range taps re-read a clamped element, then skipped
+      f32x4 v[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int h = min(max(p * st - pad + t / 3, 0), H - 1), w = min(max(q * st - pad + t % 3, 0), W - 1);
+        v[t] = ld4(x + (((long long)h * W + w) * N + n) * C + 4 * c4);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int h = p * st - pad + t / 3, w = q * st - pad + t % 3;
+        if (h < 0 || h >= H || w < 0 || w >= W) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (v[j] > best[j] || isnan(v[j])) { best[j] = v[j]; bi[j] = kh * k + kw; }
+          if (v[t][j] > best[j] || isnan(v[t][j])) { best[j] = v[t][j]; bi[j] = t; }
+      }
+    } else {
+      for (int kh = 0; kh < k; ++kh) {
+        const int h = p * st - pad + kh;
+        if (h < 0 || h >= H) continue;
+        for (int kw = 0; kw < k; ++kw) {
+          const int w = q * st - pad + kw;
+          if (w < 0 || w >= W) continue;
+          const f32x4 v = ld4(x + (((long long)h * W + w) * N + n) * C + 4 * c4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (v[j] > best[j] || isnan(v[j])) { best[j] = v[j]; bi[j] = kh * k + kw; }
+        }
       }
     }
     st4(y + row * C + 4 * c4, best);
@@ -111,6 +130,32 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(int N, int H, int W, int C,
     // p such that 0 <= h - (p*st - pad) < k
     const int p_lo = max(0, (h + pad - k + st) / st), p_hi = min(P - 1, (h + pad) / st);
     const int q_lo = max(0, (w + pad - k + st) / st), q_hi = min(Q - 1, (w + pad) / st);
+    if (k == 3 && st == 2) {
+      // the ResNet stem pool: an input element sits in at most 2 x 2 windows; all their loads in flight
+      // before the sums (same window order: p, then q, ascending)
+      uchar4 u4[4];
+      f32x4 g4[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int pc = min(p_lo + (t >> 1), P - 1), qc = min(q_lo + (t & 1), Q - 1);
+        const long long o = (((long long)pc * Q + qc) * N + n) * C + 4 * c4;
+        u4[t] = *reinterpret_cast<const uchar4*>(idx + o);
+        g4[t] = ld4(dy + o);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int p = p_lo + (t >> 1), q = q_lo + (t & 1);
+        const int kh = h - (p * st - pad), kw = w - (q * st - pad);
+        if (p > p_hi || q > q_hi || kh < 0 || kh >= k || kw < 0 || kw >= k) continue;
+        const int tap = kh * k + kw;
+        if (u4[t].x == tap) acc[0] += g4[t][0];
+        if (u4[t].y == tap) acc[1] += g4[t][1];
+        if (u4[t].z == tap) acc[2] += g4[t][2];
+        if (u4[t].w == tap) acc[3] += g4[t][3];
+      }
+      st4(dx + row * C + 4 * c4, acc);
+      continue;
+    }
     for (int p = p_lo; p <= p_hi; ++p) {
       const int kh = h - (p * st - pad);
       if (kh < 0 || kh >= k) continue;
@@ -188,7 +233,7 @@ extern "C" int tspm_maxpool_fwd(int32_t n, int32_t h, int32_t w, int32_t c, int3
     TSPM_LAUNCH_CHECK();
     return TSPM_OK;
   }
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for((long long)p * q * n * c / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3((unsigned)cdiv64((long long)p * q * n * c / 4, 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, x, y, idx);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
@@ -200,7 +245,7 @@ extern "C" int tspm_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, int3
   if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || c % 4 || k <= 0 || k > 15 || stride <= 0 || pad < 0 || !dy || !idx || !dx)
     return TSPM_ERR_INVALID;
   if (p != (h + 2 * pad - k) / stride + 1 || q != (w + 2 * pad - k) / stride + 1) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for((long long)h * w * n * c / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3((unsigned)cdiv64((long long)h * w * n * c / 4, 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), n, h, w, c, k, stride, pad, p, q, dy, idx, dx);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;

@@ -202,9 +202,11 @@ class MosiEpochRunner:
         return st
 
     def eval_step_for(self, b: int, t: int):
+        """The cached FusedMosiEvalStep for (b, t) — rebuilt when the model's engine for that shape is no longer
+        the one it captured (``UttFusionModel._apply`` drops the engines on .to() / re-materialisation)."""
         from .mosi import FusedMosiEvalStep
         st = self.eval_steps.get((b, t))
-        if st is None:
+        if st is None or st.eng is not self.model._engine(b, t, self.device):
             st = FusedMosiEvalStep(self.model, self.loss_functions, b, t, self.log)
             self.eval_steps[(b, t)] = st
         return st
@@ -252,10 +254,12 @@ class MosiEpochRunner:
         self.log.reset()
         t0 = time.time()
         self.model.eval()
-        for b in self.loader_for(loader, False):
-            for g in self._groups(b):
-                self._run(self.eval_step_for(*self._shape(g)), g)
-        self.model.train()
+        try:
+            for b in self.loader_for(loader, False):
+                for g in self._groups(b):
+                    self._run(self.eval_step_for(*self._shape(g)), g)
+        finally:
+            self.model.train()
         return self._finish(t0)
 
 

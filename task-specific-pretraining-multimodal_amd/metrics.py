@@ -17,6 +17,7 @@ tests/test_metrics_cpu.py).  Functions not known to be confusion-only get the ex
 from __future__ import annotations
 
 import importlib
+import logging
 from collections import OrderedDict
 from functools import partial
 from typing import Any, Callable, Dict, List, Optional, Sequence
@@ -163,7 +164,9 @@ class DeviceMetricRecorder:
                     value = evaluate(path, kw, c)
                 except (ImportError, AttributeError):
                     raise
-                except Exception:  # metric_recorder.py:199-201: a failing metric is reported and skipped
+                except Exception as e:  # metric_recorder.py:199-203: a failing metric is reported and skipped
+                    print(f"Error calculating metric {name}: {e}")
+                    logging.getLogger(__name__).error(f"Metric calculation error - {name}: {e}")
                     continue
                 if isinstance(value, dict):
                     for k, v in value.items():

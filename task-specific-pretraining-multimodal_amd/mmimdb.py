@@ -753,6 +753,18 @@ def f1_metrics(stats: torch.Tensor, classes: int) -> Dict[str, float]:
 PATTERNS = {"it": (1.0, 1.0), "i": (1.0, 0.0), "t": (0.0, 1.0)}  # (image, text) presence
 
 
+def synthetic_features(n: int, seed: int = 1234, image_dim: int = 4096, text_dim: int = 300, genres: int = 23):
+    """MM-IMDb-shaped synthetic features for benches (no dataset in the image): VGG16 fc7-like image
+    features (ReLU output, non-negative), mean-word2vec-like text features, and multi-hot genre labels with
+    at least one genre per movie (MML_Suite/data/mmimdb.py:122-200 shapes).  CPU tensors, seeded."""
+    g = torch.Generator().manual_seed(seed)
+    image = torch.relu(torch.randn(n, image_dim, generator=g))
+    text = 0.1 * torch.randn(n, text_dim, generator=g)
+    labels = (torch.rand(n, genres, generator=g) < 0.15).float()
+    labels[torch.arange(n), torch.randint(0, genres, (n,), generator=g)] = 1.0
+    return image, text, labels
+
+
 class MMIMDbCorpus:
     """HBM-resident MM-IMDb features (replaces the per-sample HDF5 reads + collate of
     MML_Suite/data/mmimdb.py:122-200 and the step's ``.to(device)``; the HDF5 file itself needs h5py,

@@ -81,7 +81,7 @@ def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: t
 
 class FusedTrainStep:
     def __init__(self, model, optimizer: FusedAdam, loss_functions, batch: int, audio_hw=(32, 94), image_hw=(28, 28),
-                 use_graph: bool = True, allreduce=None):
+                 use_graph: bool = True, allreduce=None, adam_split=False):
         self.model = model
         self.opt = optimizer
         self.loss_functions = loss_functions
@@ -134,6 +134,12 @@ class FusedTrainStep:
         self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
+        # single-GPU step: each encoder's parameters updated by Adam on that encoder's stream right after its
+        # own backward (the image encoder's as soon as its chain ends, beside the audio chain's tail), the
+        # head's with the audio encoder's; bitwise the one-launch update (Adam is element-wise)
+        self.adam_split = adam_split
+        self._split_ranges = None
+        self._phase_ranges = None
         self._graph_gen_keep = True
         self.calls = 0
         self._sig = (id(optimizer), id(loss_functions), batch)
@@ -194,12 +200,78 @@ class FusedTrainStep:
             self.eng_a.backward(None, self.F, phase=2)
             with torch.cuda.stream(side):
                 self.eng_i.backward(None, self.F, phase=2)
+        elif self.adam_split == "phase" and self.allreduce is None:
+            # Adam of each encoder's phase-1 parameters (fc, layer4, layer3: most of the 32.6 M) on the third
+            # stream as soon as that phase's backward has written them, beside both encoders' phase-2 backward;
+            # the phase-2 parameters (and the head's) on their own stream at its end
+            (a1, i1, a2, i2) = self._adam_phase_ranges()
+            comm = main if self.serial else self.comm
+            self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before every range
+            side.wait_stream(main)
+            comm.wait_stream(main)
+            self.eng_a.backward(self.dfused, self.F, phase=1)
+            comm.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(self.dfused[:, ea:], self.F, phase=1)
+            with torch.cuda.stream(comm):
+                self.opt.launch_ranges(comm.cuda_stream, a1)
+            comm.wait_stream(side)
+            with torch.cuda.stream(comm):
+                self.opt.launch_ranges(comm.cuda_stream, i1)
+            self.eng_a.backward(None, self.F, phase=2)
+            self.opt.launch_ranges(main.cuda_stream, a2)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(None, self.F, phase=2)
+                self.opt.launch_ranges(side.cuda_stream, i2)
+            main.wait_stream(comm)
+        elif self.adam_split and self.allreduce is None:
+            img, rest = self._adam_ranges()
+            self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before both halves
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.eng_i.backward(self.dfused[:, ea:], self.F)
+                self.opt.launch_ranges(side.cuda_stream, img)
+            self.eng_a.backward(self.dfused, self.F)
+            self.opt.launch_ranges(main.cuda_stream, rest)
         else:
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F)
             self.eng_a.backward(self.dfused, self.F)
         main.wait_stream(side)
         L.counters_add(self.nbt)
+
+    def _adam_ranges(self):
+        """FusedAdam flat-buffer ranges of (image encoder, audio encoder + head) per group."""
+        if self._split_ranges is None:
+            from .ddp import flat_ranges
+            img = {id(p) for p in self.model.image_encoder.parameters()}
+            out = ([], [])
+            for fg in self.opt.flat_groups():
+                numels = [p.numel() for p in fg.params]
+                sel = [id(p) in img for p in fg.params]
+                out[0].append(flat_ranges(fg.offsets, numels, fg.numel, sel))
+                out[1].append(flat_ranges(fg.offsets, numels, fg.numel, [not x for x in sel]))
+            self._split_ranges = out
+        return self._split_ranges
+
+    def _adam_phase_ranges(self):
+        """FusedAdam flat-buffer ranges per group of (audio phase 1 + head, image phase 1, audio phase 2,
+        image phase 2) — the parameter sets EncoderEngine.phase_params names."""
+        if getattr(self, "_phase_ranges", None) is None:
+            from .ddp import flat_ranges
+            sets = [{id(p) for p in self.eng_a.phase_params(1)} | {id(p) for p in self.model.net.parameters()},
+                    {id(p) for p in self.eng_i.phase_params(1)},
+                    {id(p) for p in self.eng_a.phase_params(2)},
+                    {id(p) for p in self.eng_i.phase_params(2)}]
+            out = ([], [], [], [])
+            for fg in self.opt.flat_groups():
+                numels = [p.numel() for p in fg.params]
+                if sum(1 for p in fg.params if any(id(p) in s_ for s_ in sets)) != len(fg.params):
+                    raise L.TspmError("adam_split='phase': a parameter outside the encoders' phases and the head")
+                for i, s_ in enumerate(sets):
+                    out[i].append(flat_ranges(fg.offsets, numels, fg.numel, [id(p) in s_ for p in fg.params]))
+            self._phase_ranges = out
+        return self._phase_ranges
 
     def phased_allreduce(self, force: bool = False, bucket_mb: float = 64.0, group=None):
         """The overlapped DP exchange for this step: gradient ranges of FusedAdam's flat buffers in
@@ -280,7 +352,7 @@ class FusedTrainStep:
 
     def _enqueue_all(self) -> None:
         self._fwd_bwd()
-        if self.allreduce is None:
+        if self.allreduce is None and not self.adam_split:
             self._opt()
 
     # ------------------------------------------------------------------------------------------

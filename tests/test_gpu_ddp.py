@@ -13,6 +13,9 @@ computes — on its half of a 64-sample batch, with FusedAdam(grad_scale = 1/2).
   first step, then the captured graphs);
 * on each REPLAYED step too, the exchanged gradient equals the sum of both ranks' plain-step gradients
   for the same weights and half batches (the exchange read what this step's backward wrote).
+
+The MOSI and MMIMDb data-parallel steps (bench.py --mosi / --mmimdb at N > 1: fused fwd/bwd graph, one
+bucketed all-reduce of the flat gradient, Adam) get the same sum / Adam / identical-state checks.
 """
 import os
 import socket
@@ -215,5 +218,91 @@ def test_two_rank_mosi_dp_step_on_one_gpu():
     for rank, ok_sum, ok_step, same, captured in res:
         assert ok_sum is True, (rank, ok_sum)
         assert ok_step is True, rank
+        assert same is True, rank
+        assert captured, rank
+
+
+def _mmimdb_worker(rank, world, port, q):
+    """MMIMDb GMU late-fusion data-parallel step (bench.py --mmimdb at N > 1): fused fwd/bwd graph, one
+    all-reduce of the flat gradient buffer (ddp.GradAllReduce), Adam with grad_scale = 1/world.  BatchNorm1d
+    statistics stay per rank (torch DDP without SyncBatchNorm, as the reference trains)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    try:
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path[:0] = [os.path.dirname(here), here]
+        import torch.distributed as dist
+        import tspm_amd
+        from oracle import mmimdb_ref as orc
+        from parity import adam_fp64, adam_tolerance
+        from test_mmimdb_cpu import dropin
+        from tspm_amd import ddp
+        from tspm_amd import mmimdb as M
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        lr, wd = 1e-5, 1e-3
+        I, T, y = orc.synthetic_batch(64, seed=31)
+        half = slice(32 * rank, 32 * rank + 32)
+
+        def keep(seed):
+            g = torch.Generator().manual_seed(seed)
+            return (torch.rand(2, 64, 512, generator=g) >= 0.5).to(torch.uint8)[:, half].contiguous().to(dev)
+
+        m_loc = dropin(3).to(dev)
+        o_loc = tspm_amd.FusedAdam(m_loc.parameters(), lr=lr, weight_decay=wd)
+        s_loc = M.FusedMMIMDbStep(m_loc, o_loc, None, 32)
+        s_loc.keep_override = keep(9)
+        s_loc.step(I[half].to(dev), T[half].to(dev), y[half].to(dev))
+        torch.cuda.synchronize()
+        g_loc = o_loc.flat_groups()[0].grad.clone()
+        m = dropin(3).to(dev)
+        opt = tspm_amd.FusedAdam(m.parameters(), lr=lr, weight_decay=wd, grad_scale=1.0 / world)
+        fg = opt.flat_groups()[0]
+        st = M.FusedMMIMDbStep(m, opt, None, 32, allreduce=ddp.GradAllReduce([g.grad for g in opt.flat_groups()]))
+        p0 = fg.param.detach().cpu().double().clone()
+        st.keep_override = keep(9)
+        st.step(I[half].to(dev), T[half].to(dev), y[half].to(dev))
+        torch.cuda.synchronize()
+        gs = [torch.empty_like(g_loc) for _ in range(world)]
+        dist.all_gather(gs, g_loc)
+        ok_sum = bool(torch.equal(fg.grad, gs[0] + gs[1]))
+        g = fg.grad.double().cpu() / world
+        exp, _, v = adam_fp64(p0, g, 1, lr=lr, wd=wd)
+        got = fg.param.detach().cpu().double()
+        ok_adam = bool(((got - exp).abs() <= 1e-6 * exp.abs() + adam_tolerance(p0, g, 1, v, lr, wd)).all())
+        for s in range(3):  # graph capture + replays
+            a2, t2, y2 = orc.synthetic_batch(64, seed=400 + s)
+            st.keep_override = keep(60 + s)
+            st.step(a2[half].to(dev), t2[half].to(dev), y2[half].to(dev))
+        torch.cuda.synchronize()
+        state = torch.cat([torch.cat([f.param, f.exp_avg, f.exp_avg_sq]) for f in opt.flat_groups()]).clone()
+        other = [torch.empty_like(state) for _ in range(world)]
+        dist.all_gather(other, state)
+        q.put((rank, ok_sum, ok_adam, bool(torch.equal(other[0], other[1])), st.graph is not None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
+
+
+def test_two_rank_mmimdb_dp_step_on_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mmimdb_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_sum, ok_adam, same, captured in res:
+        assert ok_sum is True, (rank, ok_sum)
+        assert ok_adam is True, rank
         assert same is True, rank
         assert captured, rank

@@ -379,8 +379,8 @@ def test_linear_splitk_vs_fp64(gpu, n, k, o, splits):
 
 @pytest.mark.parametrize("n,k,o", [(256, 4096, 512), (100, 4100, 300), (1024, 512, 1024)])
 def test_linear_backward_large_vs_fp64(gpu, n, k, o):
-    """Large weight-grad / data-grad products (the opt-in 64x64 quad-tile mode, TSPM_GEMM_QUAD=1, is
-    exercised by running this file with that variable set)."""
+    """Large weight-grad / data-grad products (32x32 MFMA tiles; the 64x64 quad-tile mode was measured
+    slower and removed in round 4)."""
     g = torch.Generator().manual_seed(n * 7 + k)
     x, w, dy = torch.randn(n, k, generator=g), torch.randn(o, k, generator=g) * 0.02, torch.randn(n, o, generator=g)
     xd, wd, dyd = x.to(gpu), w.to(gpu), dy.to(gpu)

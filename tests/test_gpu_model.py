@@ -170,6 +170,37 @@ def test_graph_replay_equals_eager(gpu):
     assert torch.equal(results[0], results[1])
 
 
+@pytest.mark.parametrize("split", [True, "phase"])
+def test_adam_split_schedules_equal_plain_step(gpu, split):
+    """The single-GPU Adam schedules that update parameter ranges on other streams as soon as their
+    gradients are final (per encoder at its chain's end; per backward phase on a third stream) give
+    bitwise the parameters, Adam moments and BN buffers of the one-launch update, eager and replayed,
+    and every flat-buffer element belongs to exactly one range."""
+    results = []
+    for mode in (False, split):
+        torch.manual_seed(13)
+        ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
+        st = tspm_amd.FusedTrainStep(ours, opt, None, 32, adam_split=mode)
+        if mode:
+            rs = st._adam_phase_ranges() if mode == "phase" else st._adam_ranges()
+            for gi, fg in enumerate(opt.flat_groups()):
+                cover = torch.zeros(fg.numel, dtype=torch.int32)
+                for part in rs:
+                    for a, b in part[gi]:
+                        cover[a:b] += 1
+                assert bool((cover == 1).all()), mode
+        for i in range(4):
+            audio, image, labels, _ = orc.synthetic_batch(32, seed=70 + i)
+            st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+        torch.cuda.synchronize()
+        assert st.graph is not None
+        bufs = [m.running_var.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        mom = [t for fg in opt.flat_groups() for t in (fg.exp_avg, fg.exp_avg_sq)]
+        results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs + mom).cpu())
+    assert torch.equal(results[0], results[1])
+
+
 def test_phased_allreduce_step_equals_plain_step(gpu):
     """The DP step path — forward + backward as one graph whose external events release the phase-1
     gradients to the RCCL all-reduce while phase 2 runs | RCCL of the rest | Adam graph — under a 1-rank RCCL group

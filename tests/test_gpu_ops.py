@@ -309,9 +309,9 @@ def test_bn_block_fwd_bwd(gpu, m, c, mode):
 
 
 def test_bn_bwd_fused_concurrent_streams(gpu):
-    """Two single-launch BN backwards with in-launch barriers in flight at once on two streams (as the
-    two encoders' backward passes run), many times: no barrier wait times out, counters re-arm, and
-    the results equal the same launches run one after the other."""
+    """Two BN backwards (partial-sum launch + apply launch each) in flight at once on two streams (as the
+    two encoders' backward passes run), many times: no barrier wait times out, workspaces do not alias,
+    and the results equal the same launches run one after the other."""
     from tspm_amd import _lib as L
     lib = L.lib()
     g = torch.Generator().manual_seed(11)
