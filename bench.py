@@ -123,6 +123,10 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
     of the two encoders overlap there and stretch each other)."""
     from tspm_amd.roofline import CONV_KERNEL, attribute_conv_kernels, device_kernels, launch_flops
     ks_all = device_kernels(run_serial, replays)
+    if sum(1 for k in ks_all if CONV_KERNEL.search(k["name"])) < len(seq):
+        # the profiler occasionally returns garbled kernel names for a whole capture ("void " / ""; seen with
+        # "ROCTracer produced duplicate flow start"): profile once more before giving up on attribution
+        ks_all = device_kernels(run_serial, replays)
     # split the trace into steps after each k_adam (the optimizer is the last kernel of a step) and
     # keep only COMPLETE steps: the profiler drops a few records in a long capture (up to ~5 % of a
     # 10-replay trace), so a chunk is kept when its conv-kernel count equals the recorded launch

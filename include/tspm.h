@@ -71,7 +71,13 @@ typedef struct tspm_conv_shape {
  *   The workgroup also carries 4 loader waves that stage each operand stage through registers (3 stages
  *   of loads in flight) into two LDS slots.
  * variant 2 — the same tiles and rules with single-role waves: the 4 waves issue the operand loads
- *   themselves as LDS-DMA into a 2-4-slot ring (faster for the batch-256 / 1024 grids; ABI 15). */
+ *   themselves as LDS-DMA into a 2-4-slot ring (faster for the batch-256 / 1024 grids; ABI 15).
+ * variant 3 — the ResNet stems only (c == 1, 7x7, stride 2, pad 3, k == 64; forward and weight
+ *   gradient; the other fields are ignored): a workgroup owns one image and a band of output rows,
+ *   stages the band's input rows (and, for the weight gradient, its dy rows) in LDS and runs the band
+ *   on MFMA.  The forward's BN partial statistics are per band (tspm_conv_fwd_tiles /
+ *   _tile_rows report the band count and rows); the weight gradient reduces per-workgroup slabs in
+ *   the workspace after its TSPM_COUNTER_BYTES header (tspm_conv_wgrad_workspace).  Round 4. */
 typedef struct tspm_conv_algo {
   int32_t tm, tn, wn, wk, splits;
   int32_t variant;

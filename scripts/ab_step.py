@@ -5,6 +5,7 @@ parameters stay bitwise equal after the same steps (options that only reschedule
 results).
 
     python scripts/ab_step.py --variants plain:{} split:{"adam_split":true} [--batch 128] [--rounds 8] [--k 50]
+    (a variant's "_stem": [tm, tn, wn, wk, splits, variant] overrides both stems' forward algo)
 """
 import argparse
 import json
@@ -23,7 +24,18 @@ def build(batch, kw, dev):
     torch.manual_seed(0)
     model = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(dev)
     opt = tspm_amd.FusedAdam(model.parameters(), lr=5e-4, weight_decay=1e-4)
+    kw = dict(kw)
+    stem = kw.pop("_stem", None)    # stem forward algo override for both encoders, e.g. [0,0,0,0,0,3]
+    stemw = kw.pop("_stemw", None)  # stem weight-gradient algo override
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
+    if stem is not None or stemw is not None:
+        from tspm_amd import _lib as L
+        for e in (step.eng_a, step.eng_i):
+            if stem is not None:
+                e.stem.algo_fwd = L.ConvAlgo(*stem)
+            if stemw is not None:
+                e.stem.algo_wgrad = L.ConvAlgo(*stemw)
+            e._alloc_workspace()
     feed = bench.corpus_loader(step, batch, 1234, dev, 16384)
     return model, step, feed
 
@@ -49,11 +61,13 @@ def main():
     torch.cuda.synchronize()
     ref = None
     same = {}
+    tol = {}
     for name, (model, _, _) in built.items():
         p = torch.cat([q.detach().reshape(-1) for q in model.parameters()])
         if ref is None:
             ref = p
         same[name] = bool(torch.equal(p, ref))
+        tol[name] = float(((p - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
     times = {name: [] for name in built}
     for r in range(a.rounds):
         order = list(built) if r % 2 == 0 else list(built)[::-1]
@@ -70,7 +84,7 @@ def main():
             torch.cuda.synchronize()
             times[name].append((time.perf_counter() - t0) / a.k * 1e3)
     out = {"batch": a.batch, "rounds": a.rounds, "steps_per_round": a.k,
-           "bitwise_equal_to_first_after_5_steps": same,
+           "bitwise_equal_to_first_after_5_steps": same, "max_rel_param_diff_after_5_steps": tol,
            "ms_per_step": {n: {"median": round(sorted(t)[len(t) // 2], 4), "all": [round(x, 4) for x in t]}
                            for n, t in times.items()}}
     print(json.dumps(out, indent=1))

@@ -1,10 +1,20 @@
 """Graph-timed tspm_head_train_step (both launches) at batch 128 / 1024, and its two kernels' device
-durations from torch.profiler: the fusion head's cost in isolation."""
+durations from torch.profiler: the fusion head's cost in isolation.
+
+    python scripts/head_bench.py            # timing
+    python scripts/head_bench.py --stamps   # + phase stamps of k_head_rows (needs `make stamps`)
+"""
 import ctypes
 import os
 import sys
 
+import numpy as np
 import torch
+
+STAMPS = "--stamps" in sys.argv
+if STAMPS:
+    os.environ["TSPM_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                          "task-specific-pretraining-multimodal_amd", "libtspm_stamps.so")
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -51,6 +61,27 @@ def main():
             nm = "rows" if "k_head_rows" in k["name"] else "wgrad" if "k_head_wgrad" in k["name"] else k["name"][:30]
             per[nm] = per.get(nm, 0.0) + k["dur"] / (2 * R)
         print(f"n={n}: graph-timed {us:.2f} us per head step; device us per launch {per}", flush=True)
+        if STAMPS:
+            lib = L.lib()
+            lib.tspm_debug_stamps_misc.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+            assert lib.tspm_debug_stamps_misc_clear() == 0
+            torch.cuda.synchronize()
+            L.check(lib.tspm_head_train_step(ctypes.byref(d), torch.cuda.current_stream().cuda_stream), "head")
+            torch.cuda.synchronize()
+            buf = np.zeros((1 << 18) * 8, dtype=np.uint64)
+            assert lib.tspm_debug_stamps_misc(buf.ctypes.data, buf.nbytes) == 0
+            st = buf.reshape(-1, 8).astype(np.int64)
+            st = st[st[:, 0] > 0]
+            rel = (st[:, :6] - st[:, 0].min()) * 0.01
+            names = ["entry", "staged", "fc0", "fc3+fc5", "CE", "bwd (dz3, dz0, dx)"]
+            print(f"   {len(st)} waves; entry spread p50 {np.percentile(rel[:, 0], 50):.2f} max {rel[:, 0].max():.2f} us; "
+                  f"last stamp max {rel.max():.2f} us", flush=True)
+            for i in range(1, 6):
+                dd = (st[:, i] - st[:, i - 1]) * 0.01
+                print(f"   {names[i]:20s} p50 {np.percentile(dd, 50):6.2f}  p90 {np.percentile(dd, 90):6.2f}  "
+                      f"max {dd.max():6.2f} us", flush=True)
+            clk = (st[:, 7] - st[:, 6]) / ((st[:, 5] - st[:, 0]) * 0.01)
+            print(f"   in-kernel clock p50 {np.percentile(clk, 50):.0f} MHz", flush=True)
 
 
 if __name__ == "__main__":

@@ -65,12 +65,14 @@ def main():
         step.run()
     torch.cuda.synchronize()
     ks = device_kernels(lambda: (next(feed), step.run()), a.replays)
+    # steps: cut before each input gather (the first kernel of a step; the Adam launches are several per
+    # step under the split schedules)
     steps, cur = [], []
     for k in ks:
-        cur.append(k)
-        if k["name"].startswith("k_adam") and "k_adam_begin" not in k["name"]:
+        if "k_avmnist_gather" in k["name"] and cur:
             steps.append(cur)
             cur = []
+        cur.append(k)
     res = []
     for st in steps[1:]:
         conv_streams = {}

@@ -48,14 +48,14 @@ def main():
         step.run()
     torch.cuda.synchronize()
     ks = device_kernels(lambda: (next(feed), step.run()), a.replays)
-    # steps: cut at k_adam (the last kernel of a step)
+    # steps: cut before each input gather (the first kernel of a step; the Adam launches are several per
+    # step under the split schedules)
     steps, cur = [], []
     for k in ks:
+        if "k_avmnist_gather" in k["name"] and cur:
+            steps.append(cur)
+            cur = []
         cur.append(k)
-        if "k_adam(" in k["name"] or k["name"].startswith("k_adam"):
-            if "k_adam_begin" not in k["name"]:
-                steps.append(cur)
-                cur = []
     res = []
     for st in steps[1:]:
         t0 = min(k["ts"] for k in st)
@@ -81,7 +81,7 @@ def main():
                     "fwd_end_main_us": round(main_fwd_end, 1), "fwd_end_side_us": round(side_end_fwd, 1) if side else None,
                     "adam_start_us": round(adam[-1]["ts"] - t0, 1) if adam else None,
                     "bwd_end_side_us": round(max(e for _, e in by[side]) - t0, 1) if side else None})
-    med = lambda key: sorted(r[key] for r in res)[len(res) // 2]  # noqa: E731
+    med = lambda key: (lambda v: v[len(v) // 2] if v else None)(sorted(r[key] for r in res if r[key] is not None))  # noqa: E731
     out = {"batch": a.batch, "steps": len(res), "median": {k: med(k) for k in
                                                           ("span_us", "union_busy_us", "both_streams_busy_us", "idle_us",
                                                            "head_start_us", "head_end_us", "fwd_end_main_us",

@@ -365,9 +365,12 @@ __global__ __launch_bounds__(256) void k_bn_bwd_final(long long M, int C, int G,
 // its 64 channels in double, in a fixed order (thread (lane, rg) sums tiles rg, rg+16, ... then a
 // fixed 16-way LDS reduction), so every workgroup derives bitwise the same coefficients; the
 // workgroups of row block 0 also write dgamma / dbeta.  Body: dy = ca*g' - cm - cb*(y - mean).
-// G is kept <= 64 by the host (kMergeTiles), so the merge is <= 12 float4 loads per thread, all in
-// flight together.
-constexpr int kMergeTiles = 64;
+// G is kept <= kMergeTiles by the host, so the merge is <= 3 * kMergeTiles / 16 float4 loads per thread, all
+// in flight together.
+#ifndef TSPM_MERGE_TILES
+#define TSPM_MERGE_TILES 128
+#endif
+constexpr int kMergeTiles = TSPM_MERGE_TILES;
 template <bool HAS_OUT, bool TWO, bool DRES>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int G, const float* __restrict__ part,
                                                         const float* __restrict__ inv, const float* __restrict__ gamma,
@@ -389,15 +392,22 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int 
   {
     double a[3][4] = {};
     if (cok) {
-      f32x4 v[4][3];
+      f32x4 v[kMergeTiles / 16][3];
 #pragma unroll
-      for (int u = 0; u < kMergeTiles / 16; ++u) {
+      for (int u = 0; u < kMergeTiles / 16; ++u) {  // unconditional loads (tile clamped), then masked
         const int gt = rg + 16 * u;
         const bool ok = gt < G;
-        const long long off = (long long)(ok ? gt : 0) * C + 4 * c4;
-        v[u][0] = ok ? ld4(part + off) : f32x4{0.f, 0.f, 0.f, 0.f};
-        v[u][1] = ok ? ld4(part + plane + off) : f32x4{0.f, 0.f, 0.f, 0.f};
-        v[u][2] = (ok && TWO) ? ld4(part + 2 * plane + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const long long off = (long long)min(gt, G - 1) * C + 4 * c4;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 l0 = ld4(part + off), l1 = ld4(part + plane + off);
+        v[u][0] = ok ? l0 : z;
+        v[u][1] = ok ? l1 : z;
+        if constexpr (TWO) {
+          const f32x4 l2 = ld4(part + 2 * plane + off);
+          v[u][2] = ok ? l2 : z;
+        } else {
+          v[u][2] = z;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kMergeTiles / 16; ++u)

@@ -178,7 +178,8 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_gather(ConvArgs g, co
     for (int b = 0; b < TN; ++b) co[b] = min(col0 + b * 32 + li, g.k - 1);
     const int T = cdiv_dev(RSC, 8);
     const int it0 = split_lo(T, wk, WK), it1 = split_lo(T, wk + 1, WK);
-    auto load = [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
+    for (int it = it0; it < it1; ++it) {
+      f32x4 A[TM], B[TN];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int kidx = it * 8 + 4 * hh + j;
@@ -195,24 +196,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_fwd_gather(ConvArgs g, co
 #pragma unroll
         for (int b = 0; b < TN; ++b) B[b][j] = kok ? w[(long long)co[b] * RSC + kk] : 0.f;
       }
-    };
-    // Short reductions (the 1-channel 7x7 stems: RSC = 49, <= 7 steps per wave): every step's gathers
-    // issued before the first MFMA — one memory round trip instead of one per step (the loop below waits
-    // for each step's loads before its MFMAs: 32 us for the audio stem at batch 128)
-    constexpr int PF = 8;
-    if (it1 - it0 <= PF) {
-      f32x4 A[PF][TM], B[PF][TN];
-#pragma unroll
-      for (int u = 0; u < PF; ++u) load(min(it0 + u, it1 - 1), A[u], B[u]);  // past the end: re-read, unused
-#pragma unroll
-      for (int u = 0; u < PF; ++u)
-        if (it0 + u < it1) acc.mma4(A[u], B[u]);
-    } else {
-      for (int it = it0; it < it1; ++it) {
-        f32x4 A[TM], B[TN];
-        load(it, A, B);
-        acc.mma4(A, B);
-      }
+      acc.mma4(A, B);
     }
   }
   acc.template combine<WN, WK>(lds, wn, wk, lane, active);
@@ -754,6 +738,7 @@ Algo wgrad_algo(const tspm_conv_shape* s, const tspm_conv_algo* user) {
 // variants 1 and 2 (LDS-staged, conv_lds.hip: register-staged loader waves / single-role LDS-DMA ring):
 // wm = 4 / (wn * wk)
 bool is_lds(const tspm_conv_algo* user) { return user && (user->variant == 1 || user->variant == 2); }
+bool is_stem(const tspm_conv_algo* user) { return user && user->variant == 3; }
 const tspm_detail::LdsImpl& lds_of(const tspm_conv_algo* user) {
   return user->variant == 2 ? tspm_detail::lds_impl_dma() : tspm_detail::lds_impl_reg();
 }
@@ -774,12 +759,14 @@ extern "C" size_t tspm_conv_fwd_workspace(const tspm_conv_shape* s, const tspm_c
 
 extern "C" int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
+  if (is_stem(user)) return tspm_detail::stem_supported(s) ? tspm_detail::stem_tiles(s) : 0;
   const int rows = is_lds(user) ? user->tm * 32 : fwd_algo(s, user).tm * 32;
   return rows > 0 ? cdiv(s->p * s->q * s->n, rows) : 0;
 }
 
 extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
+  if (is_stem(user)) return tspm_detail::stem_supported(s) ? tspm_detail::stem_tile_rows(s) : 0;
   return is_lds(user) ? user->tm * 32 : fwd_algo(s, user).tm * 32;
 }
 
@@ -792,6 +779,7 @@ extern "C" int32_t tspm_conv_fwd_bn_counters(const tspm_conv_shape* s, const tsp
 extern "C" int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
   if (is_lds(user)) return lds_of(user).fwd_bn_partial_floats(s, lds_algo(user));
+  if (is_stem(user)) return tspm_detail::stem_supported(s) ? 3LL * tspm_detail::stem_tiles(s) * s->k : 0;
   return 3LL * tspm_conv_fwd_tiles(s, user) * s->k;
 }
 
@@ -809,6 +797,14 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
     return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), nullptr);
+  }
+  if (is_stem(user)) {  // per-band partials, merged by tspm_bn_finalize when the caller asked for the merge
+    if (!tspm_detail::stem_supported(s)) return TSPM_ERR_INVALID;
+    const int rc = tspm_detail::stem_fwd(s, x, xs, w, y, bn ? bf.partial : nullptr, static_cast<hipStream_t>(stream));
+    if (rc != TSPM_OK || !bn || !bf.counters) return rc;
+    return tspm_bn_finalize((long long)s->p * s->q * s->n, s->k, tspm_detail::stem_tiles(s),
+                            tspm_detail::stem_tile_rows(s), bf.partial, bf.running_mean, bf.running_var, bf.momentum,
+                            bf.eps, bf.save_mean, bf.save_invstd, stream);
   }
   (void)ws; (void)ws_bytes;
   Algo al = fwd_algo(s, user);
@@ -883,6 +879,7 @@ extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
 extern "C" size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
   if (is_lds(user)) return lds_of(user).wgrad_workspace(s, lds_algo(user));
+  if (is_stem(user)) return tspm_detail::stem_wgrad_supported(s) ? tspm_detail::stem_wgrad_workspace(s) : 0;
   Algo al = wgrad_algo(s, user);
   if (al.splits <= 1) return 0;
   return TSPM_COUNTER_BYTES + (size_t)al.splits * s->k * s->r * s->s * s->c * sizeof(float);
@@ -896,6 +893,10 @@ extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).wgrad_supported(s, xs, la)) return TSPM_ERR_INVALID;
     return lds_of(user).wgrad(s, la, x, dy, dw, ws, ws_bytes, static_cast<hipStream_t>(stream));
+  }
+  if (is_stem(user)) {
+    if (!tspm_detail::stem_wgrad_supported(s)) return TSPM_ERR_INVALID;
+    return tspm_detail::stem_wgrad(s, x, xs, dy, dw, ws, ws_bytes, static_cast<hipStream_t>(stream));
   }
   Algo al = wgrad_algo(s, user);
   if (!algo_supported(al)) return TSPM_ERR_INVALID;

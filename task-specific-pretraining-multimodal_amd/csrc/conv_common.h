@@ -321,4 +321,15 @@ struct LdsImpl {
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();
+// The 1-channel 7x7/2 stems, tspm_conv_algo.variant 3 (stem.hip)
+bool stem_supported(const tspm_conv_shape* s);
+int stem_pb(const tspm_conv_shape* s);
+int stem_tiles(const tspm_conv_shape* s);
+int stem_tile_rows(const tspm_conv_shape* s);
+int stem_fwd(const tspm_conv_shape* s, const float* x, const tspm_strides4* xs, const float* w, float* y, float* part,
+             hipStream_t st);
+bool stem_wgrad_supported(const tspm_conv_shape* s);
+size_t stem_wgrad_workspace(const tspm_conv_shape* s);
+int stem_wgrad(const tspm_conv_shape* s, const float* x, const tspm_strides4* xs, const float* dy, float* dw, void* ws,
+               size_t ws_bytes, hipStream_t st);
 }  // namespace tspm_detail

@@ -5,6 +5,21 @@
 // built at config/optimizer_config.py:199-226) and the image colormap LUT (data/avmnist.py:186-191).
 #include "common.h"
 
+#ifdef TSPM_STAMPS
+// Diagnostic build only: phase stamps of k_head_rows (read back by scripts/head_bench.py --stamps)
+__device__ unsigned long long tspm_g_stamps_misc[TSPM_STAMP_WAVES * TSPM_STAMP_SLOTS];
+extern "C" int tspm_debug_stamps_misc(void* host_dst, size_t bytes) {
+  if (bytes > sizeof(tspm_g_stamps_misc)) bytes = sizeof(tspm_g_stamps_misc);
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(tspm_g_stamps_misc), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : 2;
+}
+extern "C" int tspm_debug_stamps_misc_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(tspm_g_stamps_misc)) != hipSuccess) return 2;
+  return hipMemset(p, 0, sizeof(tspm_g_stamps_misc)) == hipSuccess ? 0 : 2;
+}
+#endif
+
 namespace {
 
 int grid_for(long long work) {
@@ -257,7 +272,9 @@ int gemm_small(const GemmArgs& g0, hipStream_t st, int splits) {
     g.slab = nullptr;
   }
   int wk = 1;
-  while (wk < 4 && kk / (wk * 2) >= 32) wk *= 2;  // <= 256 threads: co-resides with conv work on other streams
+  // <= 256 threads: co-resides with conv work on other streams.  (8 waves per tile for the few-tile encoder fc
+  // products, K = 512: step 2.584-2.590 vs 2.584-2.589 ms, no gain — profiles/r4/r4j_gemm_wk8_*.json)
+  while (wk < 4 && kk / (wk * 2) >= 32) wk *= 2;
   // quad tiles where 32x32 tiles are plentiful (>= 1024) and K is short enough for one wave
   g.quad = (splits <= 1 && tiles >= 1024 && g.K <= 1024 && getenv_flag_quad()) ? 1 : 0;
   if (g.quad) wk = 4;
@@ -855,22 +872,29 @@ struct HeadSeg {
   int rows, c4, srows;  // rows to write, float4 per row, rows present in src (the rest are zeros)
   long long ld;          // src row pitch (floats)
   TSPM_DEV int total() const { return rows * c4; }
+  // i / c4 without an integer division (~40 instructions each: the staging's index math, not its loads, was
+  // what made it slow — 9 us for 134 KB): a float reciprocal estimate corrected by one step either way
+  TSPM_DEV int row_of(int i) const {
+    int r = (int)((float)i * (1.0f / (float)c4));
+    r -= r * c4 > i ? 1 : 0;
+    r += (r + 1) * c4 <= i ? 1 : 0;
+    return r;
+  }
+  // unconditional (clamped) load, so a round's loads are all in flight before the first LDS store
   TSPM_DEV f32x4 load(int i) const {
-    const int r = i / c4, k = i % c4;
-    return r < srows ? ld4(src + (long long)r * ld + 4 * k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ic = min(i, total() - 1), r = row_of(ic), k = ic - r * c4;
+    const f32x4 v = ld4(src + (long long)min(r, srows - 1) * ld + 4 * k);
+    return r < srows ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   TSPM_DEV void store(int i, f32x4 v) const {
-    const int r = i / c4, k = i % c4;
+    const int r = row_of(i), k = i - r * c4;
     st4(dst + r * (4 * c4 + 4) + 4 * k, v);
   }
 };
 template <int U>
 TSPM_DEV void head_load(const HeadSeg& g, f32x4 (&v)[U]) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = u * (int)blockDim.x + (int)threadIdx.x;
-    v[u] = i < g.total() ? g.load(i) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int u = 0; u < U; ++u) v[u] = g.load(u * (int)blockDim.x + (int)threadIdx.x);
 }
 template <int U>
 TSPM_DEV void head_store(const HeadSeg& g, const f32x4 (&v)[U]) {
@@ -901,6 +925,8 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   const int n0 = blockIdx.x * HEAD_RB;
   const int rows = min(HEAD_RB, d.n - n0);
   const int t = threadIdx.x;
+  TSPM_STAMP(tspm_g_stamps_misc, 0);
+  TSPM_STAMP_CLK(tspm_g_stamps_misc, 6);
   // stage the row block's inputs (rows past n: zeros, never stored) and the weights
   {
     const HeadSeg gx{d.x + (long long)n0 * d.ldx, sx, HEAD_RB, F / 4, rows, d.ldx};
@@ -928,6 +954,7 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   uint64_t base = 0;
   if (d.p > 0.f && d.gen_keep) base = tspm_dropout_base(d.seed, d.counter ? *d.counter : 0ULL);
   head_sync();
+  TSPM_STAMP(tspm_g_stamps_misc, 1);
   // fc0 + ReLU + dropout (tspm_linear_fwd's epilogue order: + bias, relu, * keep*scale)
   head_xwT<2>(sx, ldx, sw0, ldx, F, H, [&](int r, int o, float acc) {
     float v = relu_f(acc + sb0[o]);
@@ -946,6 +973,7 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
     if (r < rows) d.h1[(long long)(n0 + r) * H + o] = v;
   });
   head_sync();
+  TSPM_STAMP(tspm_g_stamps_misc, 2);
   head_xwT<1>(sh1, ldh, sw3, ldh, H, H2, [&](int r, int o, float acc) {
     const float v = relu_f(acc + sb3[o]);
     shh[r * ldh2 + o] = v;
@@ -958,33 +986,42 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
     if (r < rows) d.logits[(long long)(n0 + r) * C + o] = v;
   });
   head_sync();
-  // cross-entropy per row (tspm_cross_entropy's arithmetic); sz becomes dlogits
-  if (t < HEAD_RB) {
-    float* z = sz + t * ldc;
-    if (t < rows) {
+  TSPM_STAMP(tspm_g_stamps_misc, 3);
+  // cross-entropy per row (tspm_cross_entropy's arithmetic); sz becomes dlogits.  Wave 0: 16 lanes per row,
+  // lane k owns class k — the exponentials in parallel, the max scan and the sum of exponentials in class
+  // order by every lane of the row (the same operations and order as one thread per row)
+  if (t < 64) {
+    const int r = t >> 4, k = t & 15;
+    float* z = sz + r * ldc;
+    const bool kv = k < C;
+    if (r < rows) {
       float mx = z[0];
       int am = 0;
-      for (int k = 1; k < C; ++k)
-        if (z[k] > mx) { mx = z[k]; am = k; }
+      for (int j = 1; j < C; ++j)
+        if (z[j] > mx) { mx = z[j]; am = j; }
+      const float e = kv ? expf(z[k] - mx) : 0.f;
       float se = 0.f;
-      for (int k = 0; k < C; ++k) se += expf(z[k] - mx);
-      const float lse = logf(se);
-      const bool lok = slab[t] >= 0;
-      const int lab = lok ? slab[t] : 0;
-      d.row_ws[n0 + t] = lok ? lse - (z[lab] - mx) : __builtin_nanf("");
-      d.row_ws[d.n + n0 + t] = (am == lab) ? 1.f : 0.f;
-      const float invn = 1.0f / (float)d.n;
-      for (int k = 0; k < C; ++k) {  // in place: class k's logit is read once, after mx and se
-        const float pk = expf(z[k] - mx) / se;
-        const float g = lok ? (pk - (k == lab ? 1.f : 0.f)) * invn * d.loss_weight : __builtin_nanf("");
-        z[k] = g;
-        d.dlogits[(long long)(n0 + t) * C + k] = g;
+      for (int j = 0; j < C; ++j) se += __shfl(e, (t & ~15) + j, 64);
+      const bool lok = slab[r] >= 0;
+      const int lab = lok ? slab[r] : 0;
+      if (k == 0) {
+        const float lse = logf(se);
+        d.row_ws[n0 + r] = lok ? lse - (z[lab] - mx) : __builtin_nanf("");
+        d.row_ws[d.n + n0 + r] = (am == lab) ? 1.f : 0.f;
       }
-    } else {
-      for (int k = 0; k < C; ++k) z[k] = 0.f;
+      const float invn = 1.0f / (float)d.n;
+      const float pk = e / se;
+      const float g = lok ? (pk - (k == lab ? 1.f : 0.f)) * invn * d.loss_weight : __builtin_nanf("");
+      if (kv) {  // after every lane of the row has read z (one wave: program order)
+        z[k] = g;
+        d.dlogits[(long long)(n0 + r) * C + k] = g;
+      }
+    } else if (kv) {
+      z[k] = 0.f;
     }
   }
   head_sync();
+  TSPM_STAMP(tspm_g_stamps_misc, 4);
   // dz3 = (dlogits w5) * (hh > 0)   (w5 is [C][H2]: the transposed product) -> shh; item (r, o)'s hh value
   // is read and overwritten by its own thread only
   head_xW<1>(sz, ldc, sw5, ldh2, C, H2, [&](int r, int o, float acc) {
@@ -1004,6 +1041,8 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   head_xW<4>(sh1, ldh, sw0, ldx, H, F, [&](int r, int o, float acc) {
     if (r < rows) d.dx[(long long)(n0 + r) * d.lddx + o] = acc;
   });
+  TSPM_STAMP(tspm_g_stamps_misc, 5);
+  TSPM_STAMP_CLK(tspm_g_stamps_misc, 7);
 }
 
 template <int WK>

@@ -105,7 +105,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
 import re as _re
 
 CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|bwd_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
-                          r"conv_wgrad|conv_wgrad_t|reduce_slabs|reduce_slabs_wide)\b")
+                          r"conv_wgrad|conv_wgrad_t|stem_fwd|stem_wgrad|reduce_slabs|reduce_slabs_wide)\b")
 CONV_SECONDARY = _re.compile(r"\bk_reduce_slabs(_wide)?\b")  # second kernel of a split-K wgrad launch (variant 0)
 
 

@@ -81,7 +81,7 @@ def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: t
 
 class FusedTrainStep:
     def __init__(self, model, optimizer: FusedAdam, loss_functions, batch: int, audio_hw=(32, 94), image_hw=(28, 28),
-                 use_graph: bool = True, allreduce=None, adam_split=False):
+                 use_graph: bool = True, allreduce=None, adam_split=True):
         self.model = model
         self.opt = optimizer
         self.loss_functions = loss_functions
@@ -134,12 +134,13 @@ class FusedTrainStep:
         self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
-        # single-GPU step: each encoder's parameters updated by Adam on that encoder's stream right after its
-        # own backward (the image encoder's as soon as its chain ends, beside the audio chain's tail), the
-        # head's with the audio encoder's; bitwise the one-launch update (Adam is element-wise)
+        # single-GPU step (adam_split): each encoder's parameters updated by Adam on that encoder's stream right
+        # after its own backward (the image encoder's beside the audio chain's tail), the head's with the audio
+        # encoder's; bitwise the one-launch update (Adam is element-wise).  A cross-stream edge in the middle of
+        # the two chains (e.g. the audio layer3/4 update moved to the image stream) serialised the replayed
+        # graph: 3.55 ms vs 2.64 (profiles/r4/r4f_ab_adam_schedules.json)
         self.adam_split = adam_split
         self._split_ranges = None
-        self._phase_ranges = None
         self._graph_gen_keep = True
         self.calls = 0
         self._sig = (id(optimizer), id(loss_functions), batch)
@@ -200,34 +201,11 @@ class FusedTrainStep:
             self.eng_a.backward(None, self.F, phase=2)
             with torch.cuda.stream(side):
                 self.eng_i.backward(None, self.F, phase=2)
-        elif self.adam_split == "phase" and self.allreduce is None:
-            # Adam of each encoder's phase-1 parameters (fc, layer4, layer3: most of the 32.6 M) on the third
-            # stream as soon as that phase's backward has written them, beside both encoders' phase-2 backward;
-            # the phase-2 parameters (and the head's) on their own stream at its end
-            (a1, i1, a2, i2) = self._adam_phase_ranges()
-            comm = main if self.serial else self.comm
+        elif self._split_opt():
+            img, rest = self._adam_ranges()
             self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before every range
             side.wait_stream(main)
-            comm.wait_stream(main)
-            self.eng_a.backward(self.dfused, self.F, phase=1)
-            comm.wait_stream(main)
-            with torch.cuda.stream(side):
-                self.eng_i.backward(self.dfused[:, ea:], self.F, phase=1)
-            with torch.cuda.stream(comm):
-                self.opt.launch_ranges(comm.cuda_stream, a1)
-            comm.wait_stream(side)
-            with torch.cuda.stream(comm):
-                self.opt.launch_ranges(comm.cuda_stream, i1)
-            self.eng_a.backward(None, self.F, phase=2)
-            self.opt.launch_ranges(main.cuda_stream, a2)
-            with torch.cuda.stream(side):
-                self.eng_i.backward(None, self.F, phase=2)
-                self.opt.launch_ranges(side.cuda_stream, i2)
-            main.wait_stream(comm)
-        elif self.adam_split and self.allreduce is None:
-            img, rest = self._adam_ranges()
-            self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before both halves
-            side.wait_stream(main)
+            # each encoder's parameters on its own stream at its chain's end, the head's with the audio encoder's
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F)
                 self.opt.launch_ranges(side.cuda_stream, img)
@@ -240,8 +218,13 @@ class FusedTrainStep:
         main.wait_stream(side)
         L.counters_add(self.nbt)
 
+    def _split_opt(self) -> bool:
+        """Adam launched per encoder inside the fwd/bwd enqueue (single GPU, no gradient clipping: the
+        range launches have no clip-coefficient form)."""
+        return bool(self.adam_split) and self.allreduce is None and getattr(self.opt, "clip_coef", None) is None
+
     def _adam_ranges(self):
-        """FusedAdam flat-buffer ranges of (image encoder, audio encoder + head) per group."""
+        """FusedAdam flat-buffer ranges per group of (image encoder, audio encoder + head)."""
         if self._split_ranges is None:
             from .ddp import flat_ranges
             img = {id(p) for p in self.model.image_encoder.parameters()}
@@ -254,25 +237,6 @@ class FusedTrainStep:
             self._split_ranges = out
         return self._split_ranges
 
-    def _adam_phase_ranges(self):
-        """FusedAdam flat-buffer ranges per group of (audio phase 1 + head, image phase 1, audio phase 2,
-        image phase 2) — the parameter sets EncoderEngine.phase_params names."""
-        if getattr(self, "_phase_ranges", None) is None:
-            from .ddp import flat_ranges
-            sets = [{id(p) for p in self.eng_a.phase_params(1)} | {id(p) for p in self.model.net.parameters()},
-                    {id(p) for p in self.eng_i.phase_params(1)},
-                    {id(p) for p in self.eng_a.phase_params(2)},
-                    {id(p) for p in self.eng_i.phase_params(2)}]
-            out = ([], [], [], [])
-            for fg in self.opt.flat_groups():
-                numels = [p.numel() for p in fg.params]
-                if sum(1 for p in fg.params if any(id(p) in s_ for s_ in sets)) != len(fg.params):
-                    raise L.TspmError("adam_split='phase': a parameter outside the encoders' phases and the head")
-                for i, s_ in enumerate(sets):
-                    out[i].append(flat_ranges(fg.offsets, numels, fg.numel, [id(p) in s_ for p in fg.params]))
-            self._phase_ranges = out
-        return self._phase_ranges
-
     def phased_allreduce(self, force: bool = False, bucket_mb: float = 64.0, group=None):
         """The overlapped DP exchange for this step: gradient ranges of FusedAdam's flat buffers in
         three phases — (0) head + audio fc/layer4/layer3, (1) image fc/layer4/layer3, (2) both
@@ -283,41 +247,47 @@ class FusedTrainStep:
                 {id(p) for p in self.eng_i.phase_params(1)},
                 {id(p) for p in self.eng_a.phase_params(2) + self.eng_i.phase_params(2)}]
         views = [[], [], []]
+        ranges = ([], [], [])  # per phase, per flat group: the element ranges (Adam after that phase's exchange)
         for fg in self.opt.flat_groups():
             for p in fg.params:
                 if sum(id(p) in st for st in sets) != 1:
                     raise L.TspmError("phased all-reduce: parameter not owned by exactly one backward phase")
             numels = [p.numel() for p in fg.params]
             for k, st in enumerate(sets):
-                views[k] += [fg.grad[a:b] for a, b in flat_ranges(fg.offsets, numels, fg.numel,
-                                                                  [id(p) in st for p in fg.params])]
+                rk = flat_ranges(fg.offsets, numels, fg.numel, [id(p) in st for p in fg.params])
+                ranges[k].append(rk)
+                views[k] += [fg.grad[a:b] for a, b in rk]
+        self._phase_ranges = ranges
         return PhasedGradAllReduce(views, bucket_mb=bucket_mb, group=group, force=force)
 
     def _run_phased(self) -> None:
         """DP step with the RCCL exchange overlapped with backward, the whole forward + backward as ONE
-        HIP graph (the plain step's two-stream schedule):
-             main (graph): [fwd both + head + audio bwd late ─●─ audio bwd early] ─┐
-             side (graph):                   [image bwd late ─●─ image bwd early] ─┴─ wait ─ [Adam graph]
-             RCCL:                          all-reduce(head+audio late) · (image late) · (both early)
+        HIP graph (the plain step's two-stream schedule), and each phase's Adam update right behind that
+        phase's exchange:
+             main (graph): [fwd both + head + audio bwd late ─●─ audio bwd early] ─ RCCL(both early) ─ Adam(early)
+             side (graph):                   [image bwd late ─●─ image bwd early] ─┘
+             comm:          RCCL(head+audio late) ─ Adam(head+audio late) · RCCL(image late) ─ Adam(image late)
         ● = a step flag (``_lib.DeviceFlag``: a one-thread kernel in the graph publishes a per-step count to
         pinned host memory; the host waits for it before launching the collective — ROCm 7 refuses
-        graph-external event records); the collectives run outside the graph, on RCCL's stream, each
-        after the flag of the backward part that writes its gradients."""
+        graph-external event records); the collectives run on RCCL's stream, each after the flag of the
+        backward part that writes its gradients, and the comm / main streams wait for them before the Adam
+        ranges of the same parameters (phase 2's backward reads none of the phase-0/1 parameters).  Adam is
+        element-wise, so the per-phase ranges give bitwise the one-launch update."""
         ar = self.allreduce
         eager = not self.use_graph or self.calls == 0
         if getattr(self, "_marks", None) is None:
             self._marks = (L.DeviceFlag(), L.DeviceFlag())
+        if getattr(self, "_phase_ranges", None) is None:
+            raise L.TspmError("phased step: build the exchange with FusedTrainStep.phased_allreduce()")
         if eager:
             self._fwd_bwd(marks=self._marks)
         else:
             if self.graph is None:
                 torch.cuda.synchronize(self.device)
-                g, go = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._fwd_bwd(marks=self._marks)
-                with torch.cuda.graph(go):
-                    self._opt()
-                self.graph, self.graph_opt = g, go
+                self.graph, self.graph_opt = g, None
                 self._graph_gen_keep = self.keep_override is None
             self.graph.replay()
         # each flag is bumped once per step, after (in graph order) everything main ran before this step
@@ -325,18 +295,19 @@ class FusedTrainStep:
         # gradients it covers are complete, so the exchange launched then needs no device-side wait
         for f in self._marks:
             f.count += 1
+        main, comm, r = torch.cuda.current_stream(), self.comm, self._phase_ranges
         self._marks[0].host_wait(self._marks[0].count)
-        with torch.cuda.stream(self.comm):
-            w_a = ar.launch(0)
+        with torch.cuda.stream(comm):
+            ar.wait(ar.launch(0))
+            self.opt.launch_begin(comm.cuda_stream)  # one step-count increment, before every range
+            self.opt.launch_ranges(comm.cuda_stream, r[0])
         self._marks[1].host_wait(self._marks[1].count)
-        with torch.cuda.stream(self.comm):
-            w_i = ar.launch(1)
-        w_e = ar.launch(2)  # on main, behind the graph: no stream hop before the last exchange
-        ar.wait(w_a + w_i + w_e)
-        if eager:
-            self._opt()
-        else:
-            self.graph_opt.replay()
+        with torch.cuda.stream(comm):
+            ar.wait(ar.launch(1))
+            self.opt.launch_ranges(comm.cuda_stream, r[1])
+        ar.wait(ar.launch(2))  # on main, behind the graph: no stream hop before the last exchange
+        main.wait_stream(comm)  # the step-count increment and the phase-0/1 updates before the step ends
+        self.opt.launch_ranges(main.cuda_stream, r[2])
 
     def _classify(self, sh: int) -> None:
         log = self.log
@@ -352,7 +323,7 @@ class FusedTrainStep:
 
     def _enqueue_all(self) -> None:
         self._fwd_bwd()
-        if self.allreduce is None and not self.adam_split:
+        if self.allreduce is None and not self._split_opt():
             self._opt()
 
     # ------------------------------------------------------------------------------------------

@@ -170,20 +170,19 @@ def test_graph_replay_equals_eager(gpu):
     assert torch.equal(results[0], results[1])
 
 
-@pytest.mark.parametrize("split", [True, "phase"])
-def test_adam_split_schedules_equal_plain_step(gpu, split):
-    """The single-GPU Adam schedules that update parameter ranges on other streams as soon as their
-    gradients are final (per encoder at its chain's end; per backward phase on a third stream) give
-    bitwise the parameters, Adam moments and BN buffers of the one-launch update, eager and replayed,
-    and every flat-buffer element belongs to exactly one range."""
+def test_adam_split_schedule_equals_plain_step(gpu):
+    """The single-GPU Adam schedule (the default) that updates each encoder's parameter ranges on that
+    encoder's stream as soon as its backward ends gives bitwise the parameters, Adam moments and BN
+    buffers of the one-launch update, eager and replayed, and every flat-buffer element belongs to
+    exactly one range."""
     results = []
-    for mode in (False, split):
+    for mode in (False, True):
         torch.manual_seed(13)
         ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
         opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
         st = tspm_amd.FusedTrainStep(ours, opt, None, 32, adam_split=mode)
         if mode:
-            rs = st._adam_phase_ranges() if mode == "phase" else st._adam_ranges()
+            rs = st._adam_ranges()
             for gi, fg in enumerate(opt.flat_groups()):
                 cover = torch.zeros(fg.numel, dtype=torch.int32)
                 for part in rs:
@@ -202,8 +201,9 @@ def test_adam_split_schedules_equal_plain_step(gpu, split):
 
 
 def test_phased_allreduce_step_equals_plain_step(gpu):
-    """The DP step path — forward + backward as one graph whose external events release the phase-1
-    gradients to the RCCL all-reduce while phase 2 runs | RCCL of the rest | Adam graph — under a 1-rank RCCL group
+    """The DP step path — forward + backward as one graph whose step flags release the phase-1
+    gradients to the RCCL all-reduce (and that phase's Adam ranges) while phase 2 runs | RCCL of the rest |
+    the rest's Adam ranges — under a 1-rank RCCL group
     (all-reduce = identity) gives bitwise the parameters of the plain fused step, eager and
     graph-replayed, and covers every parameter exactly once."""
     import os
@@ -234,8 +234,8 @@ def test_phased_allreduce_step_equals_plain_step(gpu):
                 audio, image, labels, _ = orc.synthetic_batch(32, seed=50 + i)
                 st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
             torch.cuda.synchronize()
-            if phased:  # one fwd+bwd graph + the Adam graph
-                assert isinstance(st.graph, torch.cuda.CUDAGraph) and isinstance(st.graph_opt, torch.cuda.CUDAGraph)
+            if phased:  # one fwd+bwd graph; Adam per phase behind its exchange (no Adam graph)
+                assert isinstance(st.graph, torch.cuda.CUDAGraph) and st.graph_opt is None
             bufs = [m.running_var.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)]
             results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs).cpu())
         bad = (results[0] != results[1]).nonzero().reshape(-1)

@@ -68,8 +68,9 @@ def test_conv_fwd(gpu, case, algo):
     _check(out, ref, conv_bound(x, wt, st, pad), f"conv_fwd {case} {algo}")
 
 
-@pytest.mark.parametrize("case", [(4, 1, 32, 94), (8, 1, 28, 28), (3, 1, 13, 9)])
-@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 1, 1, 1), (1, 2, 2, 4, 1)])
+@pytest.mark.parametrize("case", [(4, 1, 32, 94), (8, 1, 28, 28), (3, 1, 13, 9), (128, 1, 32, 94), (128, 1, 28, 28),
+                                  (2, 1, 40, 500)])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (2, 2, 1, 1, 1), (1, 2, 2, 4, 1), (0, 0, 0, 0, 0, 3)])
 def test_stem_fwd_nchw_input(gpu, case, algo):
     """7x7/2 stem reading the reference's NCHW input in place; spectrogram-like dynamic range."""
     n, c, h, w = case
@@ -79,6 +80,31 @@ def test_stem_fwd_nchw_input(gpu, case, algo):
     ref = F.conv2d(x.double(), wt.double(), None, 2, 3)
     out = conv_fwd(x.to(gpu), wt.to(gpu), 2, 3, algo, nchw_input=True)
     _check(out, ref, conv_bound(x, wt, 2, 3), f"stem fwd {case} {algo}")
+
+
+@pytest.mark.parametrize("case", [(128, 1, 32, 94), (128, 1, 28, 28), (5, 1, 13, 9), (1024, 1, 32, 94)])
+@pytest.mark.parametrize("offset", [0.0, 3e4])
+@pytest.mark.parametrize("fused", [True, False])
+def test_stem_band_kernel_bn_statistics(gpu, case, offset, fused):
+    """Variant 3 (stem.hip: one image x a band of output rows per workgroup): the per-band BN partials merged
+    by tspm_bn_finalize (fused: inside tspm_conv_fwd; else by the caller with the queried tile count / rows)
+    give the batch mean / invstd of its output, and the output matches the fp64 convolution."""
+    from abi_helpers import conv_fwd_with_stats
+    n, c, h, w = case
+    g = torch.Generator().manual_seed(37)
+    x = torch.randn(n, c, h, w, generator=g) + offset / 100
+    wt = torch.randn(64, c, 7, 7, generator=g) * 0.1
+    wt[:, :, 3, 3] += offset / 100
+    y, mean, inv = conv_fwd_with_stats(x.to(gpu), wt.to(gpu), 2, 3, (0, 0, 0, 0, 0, 3), fused=fused)
+    torch.cuda.synchronize()
+    yd = y.double().cpu()
+    ref = F.conv2d(x.double(), wt.double(), None, 2, 3)
+    _check(y, ref, conv_bound(x, wt, 2, 3), f"stem band fwd {case}")
+    mean_ref = yd.mean((0, 2, 3))
+    var_ref = yd.var((0, 2, 3), unbiased=False)
+    scale = yd.abs().amax((0, 2, 3)) + 1
+    assert ((mean.double().cpu() - mean_ref).abs() <= 1e-6 * scale).all()
+    assert torch.allclose(inv.double().cpu(), 1 / torch.sqrt(var_ref + 1e-5), rtol=1e-4)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -121,8 +147,10 @@ def test_conv_wgrad(gpu, case, algo):
     _check(out, ref, bound, f"conv_wgrad {case} {algo}")
 
 
-@pytest.mark.parametrize("case", [(4, 1, 32, 94), (8, 1, 28, 28), (16, 1, 28, 28)])
-def test_stem_wgrad_nchw_input(gpu, case):
+@pytest.mark.parametrize("case", [(4, 1, 32, 94), (8, 1, 28, 28), (16, 1, 28, 28), (128, 1, 32, 94), (128, 1, 28, 28),
+                                  (3, 1, 13, 9)])
+@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (0, 0, 0, 0, 0, 3)])
+def test_stem_wgrad_nchw_input(gpu, case, algo):
     n, c, h, w = case
     g = torch.Generator().manual_seed(17)
     x = 10.0 ** torch.empty(n, c, h, w).uniform_(-8, 7, generator=g)
@@ -130,8 +158,8 @@ def test_stem_wgrad_nchw_input(gpu, case):
     dy = torch.randn(n, 64, p, q, generator=g) * 1e-6
     ref = torch.nn.grad.conv2d_weight(x.double(), (64, c, 7, 7), dy.double(), 2, 3)
     bound = torch.nn.grad.conv2d_weight(x.double().abs(), (64, c, 7, 7), dy.double().abs(), 2, 3)
-    out = conv_wgrad(x.to(gpu), dy.to(gpu), (7, 7), 2, 3, nchw_input=True)
-    _check(out, ref, bound, f"stem wgrad {case}")
+    out = conv_wgrad(x.to(gpu), dy.to(gpu), (7, 7), 2, 3, algo, nchw_input=True)
+    _check(out, ref, bound, f"stem wgrad {case} {algo}")
 
 
 @pytest.mark.parametrize("case", [CONV_CASES[i] for i in (0, 1, 2, 5, 6, 8, 12)])
