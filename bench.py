@@ -127,18 +127,21 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
         # the profiler occasionally returns garbled kernel names for a whole capture ("void " / ""; seen with
         # "ROCTracer produced duplicate flow start"): profile once more before giving up on attribution
         ks_all = device_kernels(run_serial, replays)
-    # split the trace into steps after each k_adam (the optimizer is the last kernel of a step) and
+    # split the trace into steps before each input gather (``run_serial`` = gather + step: the first kernel of
+    # every step; the optimizer launches Adam once per encoder, so k_adam does not mark step ends) and
     # keep only COMPLETE steps: the profiler drops a few records in a long capture (up to ~5 % of a
     # 10-replay trace), so a chunk is kept when its conv-kernel count equals the recorded launch
-    # sequence and its kernel count equals the largest such chunk's (a chunk that lost its k_adam
-    # spans two steps and fails the first test; several k_adam per step leave no chunk passing it)
+    # sequence and its kernel count equals the largest such chunk's (a chunk that lost its gather
+    # spans two steps and fails the first test)
     from tspm_amd.roofline import CONV_SECONDARY
     steps, cur = [], []
     for k in ks_all:
-        cur.append(k)
-        if re.search(r"\bk_adam\b", k["name"]):
+        if "k_avmnist_gather" in k["name"] and cur:
             steps.append(cur)
             cur = []
+        cur.append(k)
+    if cur:
+        steps.append(cur)
     full = [st for st in steps if sum(1 for k in st if CONV_KERNEL.search(k["name"])
                                       and not CONV_SECONDARY.search(k["name"])) == len(seq)]
     most = max((len(st) for st in full), default=0)

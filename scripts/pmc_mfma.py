@@ -10,7 +10,7 @@ under the counter pass is GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.
 reads high on short dispatches), so both the 2.4 GHz figure and the measured-clock figure are given.
 SQ_WAVE_CYCLES = SQ_WAIT_ANY (parked at s_waitcnt / s_barrier) + SQ_WAIT_INST_ANY (issue-stalled: MFMA
 pipe / dependency / LDS issue) + SQ_ACTIVE_INST_ANY (issuing); the fractions are of SQ_WAVE_CYCLES over
-ALL waves of the kernel (loader waves included).  A step = the dispatches between consecutive k_adam
+ALL waves of the kernel (loader waves included).  A step = the dispatches from one input gather to the next (else between consecutive k_adam
 launches; the last complete step of the run is used (PMC serialises every dispatch)."""
 import csv
 import json
@@ -19,7 +19,7 @@ import re
 import sys
 from collections import defaultdict
 
-CONV = re.compile(r"k_(fwd|dgrad|wgrad|bwd)_lds|k_conv_|k_reduce_slabs")
+CONV = re.compile(r"k_(fwd|dgrad|wgrad|bwd)_lds|k_conv_|k_stem_|k_reduce_slabs")
 CLOCK_MAX_HZ = 2.4e9
 SIMDS = 256 * 4
 
@@ -37,8 +37,22 @@ def load(d):
 
 
 def last_step(meta):
+    """The last complete step's dispatches.  Steps start at the bench's input gather (k_avmnist_gather, one
+    per step) when the run has one — the AVMNIST step launches Adam more than once (per-encoder ranges) —
+    else they end at each k_adam launch."""
+    order = sorted(meta)
+    if any("k_avmnist_gather" in meta[i][0] for i in order):
+        steps, cur = [], None
+        for i in order:
+            if "k_avmnist_gather" in meta[i][0]:
+                if cur:
+                    steps.append(cur)
+                cur = []
+            if cur is not None:
+                cur.append(i)
+        return steps[-1], len(steps)  # the run's last segment (after the last gather) may be incomplete
     steps, cur, started = [], [], False
-    for i in sorted(meta):
+    for i in order:
         if started:
             cur.append(i)
         if "k_adam(" in meta[i][0]:

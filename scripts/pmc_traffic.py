@@ -16,9 +16,9 @@ import statistics
 import sys
 from collections import defaultdict
 
-FAMILIES = [("conv", ("k_fwd_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k_conv_", "k_reduce_slabs")),
+FAMILIES = [("conv", ("k_fwd_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k_conv_", "k_stem_", "k_reduce_slabs")),
             ("bn", ("k_bn_", "k_bn1d")), ("pool", ("k_maxpool", "k_avgpool")), ("adam", ("k_adam",)),
-            ("gather", ("k_avmnist_gather",)), ("head", ("k_gemm_small", "k_gemm_pair", "k_splitk_reduce",
+            ("gather", ("k_avmnist_gather",)), ("head", ("k_head_", "k_gemm_small", "k_gemm_pair", "k_splitk_reduce",
                                                          "k_cross_entropy", "k_act_bwd", "k_dropout")),
             ("mmimdb_ew", ("k_gmu", "k_maxout", "k_bce")),
             ("mosi", ("k_lstm_", "k_textcnn", "k_seq_gather", "k_sumsq", "k_clip_coef"))]  # "head" = every small-GEMM (Linear) launch
@@ -42,6 +42,19 @@ def load(d: str, counter: str):
 
 
 def steps(rows):
+    """Complete steps: from one input gather (k_avmnist_gather, one per bench step) to the next when the run
+    has them — the AVMNIST step launches Adam more than once (per-encoder ranges) — else the dispatches
+    between consecutive k_adam launches."""
+    if any("k_avmnist_gather" in name for _, name, _ in rows):
+        out, cur = [], None
+        for _, name, v in rows:
+            if "k_avmnist_gather" in name:
+                if cur:
+                    out.append(cur)
+                cur = []
+            if cur is not None:
+                cur.append((name, v))
+        return out
     out, cur, started = [], [], False
     for _, name, v in rows:
         if started:
@@ -74,7 +87,8 @@ def main(fetch_dir: str, write_dir: str) -> None:
     out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                      f"`bench.py {bench_args}`; read bytes = 2 x FETCH_SIZE "
                      "(gfx950 wide-read correction), write bytes = WRITE_SIZE; per step = dispatches "
-                     "between consecutive k_adam launches; median over complete steps",
+                     "from one input gather to the next (else between consecutive k_adam launches); median "
+                     "over complete steps",
            "steps_read_pass": len(rd), "steps_write_pass": len(wr), "per_step_bytes": {}}
     for f in fams:
         r = statistics.median([s.get(f, 0.0) for s, _ in rd]) if rd else None

@@ -1004,8 +1004,11 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   const int Greal = (int)cdiv64(m, rpb);
   float* coef = part + (size_t)3 * G * c;
   const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
-  // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide)
-  const int pu = !bn_wide() ? 4 : rpb >= 64LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
+  // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide).  16 from
+  // 32 rows per thread on: with 128 tiles the audio stem's 96,256 rows give 752-row tiles, which the old
+  // 64-rows-per-thread threshold ran at 8 (half the loads in flight: 39.7 vs 31.6 us with 64 tiles of 16;
+  // 20.4 us with 128 tiles of 16, profiles/r4/r4l_serial_step.txt; step 2.597 vs 2.599 ms, r4m2_pu*)
+  const int pu = !bn_wide() ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
   // 1,024-thread workgroups for the 64-channel layers' tiles (TSPM_BN_PART_RG64=1; off by default: measured
   // BN device time 1.020 -> 0.972 ms per step but the step 2.778 -> 2.786 ms — the wider workgroups
   // crowd the other encoder's stream)

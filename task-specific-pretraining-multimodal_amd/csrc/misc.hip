@@ -927,32 +927,59 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   const int t = threadIdx.x;
   TSPM_STAMP(tspm_g_stamps_misc, 0);
   TSPM_STAMP_CLK(tspm_g_stamps_misc, 6);
-  // stage the row block's inputs (rows past n: zeros, never stored) and the weights
+  // stage the row block's inputs (rows past n: zeros, never stored), the weights, biases and labels: every
+  // global load is issued first (one memory round trip); x, w0, the biases and labels are stored before fc0,
+  // w3 / w5 behind it (their loads land while fc0 runs)
+  const HeadSeg g3{d.w3, sw3, H2, H / 4, H2, H}, g5{d.w5, sw5, C, H2 / 4, C, H2};
+  f32x4 v3[8], v5[1];  // the default head: 128 x 64 (8 per thread), 64 x 10 (1)
+  uint64_t base = 0;
   {
     const HeadSeg gx{d.x + (long long)n0 * d.ldx, sx, HEAD_RB, F / 4, rows, d.ldx};
-    const HeadSeg g0{d.w0, sw0, H, F / 4, H, F}, g3{d.w3, sw3, H2, H / 4, H2, H}, g5{d.w5, sw5, C, H2 / 4, C, H2};
-    f32x4 vx[1], v0[24], v3[8], v5[1];  // the default head: 192 x 128 (24 per thread), 128 x 64 (8), 64 x 10
+    const HeadSeg g0{d.w0, sw0, H, F / 4, H, F};
+    f32x4 vx[1], v0[24];  // 192 x 128: 24 per thread
+    const uint64_t ctr = (d.p > 0.f && d.gen_keep && d.counter) ? *d.counter : 0ULL;
     head_load(gx, vx);
     head_load(g0, v0);
     head_load(g3, v3);
     head_load(g5, v5);
+    // biases [H], [H2], [C] and the row block's labels: element i = t, t + blockDim (unconditional loads)
+    const int NB = H + H2 + C + HEAD_RB;
+    float bv[2];
+    long long lv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * (int)blockDim.x;
+      const float* bp = i < H ? d.b0 + i : i < H + H2 ? d.b3 + (i - H) : i < H + H2 + C ? d.b5 + (i - H - H2) : d.b0;
+      bv[u] = *bp;
+      const int r = min(max(i - (H + H2 + C), 0), rows - 1);
+      lv[u] = d.labels[n0 + r];
+    }
     head_store(gx, vx);
     head_store(g0, v0);
-    head_store(g3, v3);
-    head_store(g5, v5);
-    for (int i = t; i < H + H2 + C + HEAD_RB; i += blockDim.x) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + u * (int)blockDim.x;
+      if (i < H) sb0[i] = bv[u];
+      else if (i < H + H2) sb3[i - H] = bv[u];
+      else if (i < H + H2 + C) sb5[i - H - H2] = bv[u];
+      else if (i < NB) {  // label of row r; out-of-range labels (int64) clamp to -1 (the CE below turns them into NaN)
+        const int r = i - H - H2 - C;
+        const long long l = r < rows ? lv[u] : 0;
+        slab[r] = (l >= 0 && l < C) ? (int)l : -1;
+      }
+    }
+    for (int i = t + 2 * (int)blockDim.x; i < NB; i += blockDim.x) {  // larger heads than the default
       if (i < H) sb0[i] = d.b0[i];
       else if (i < H + H2) sb3[i - H] = d.b3[i - H];
       else if (i < H + H2 + C) sb5[i - H - H2] = d.b5[i - H - H2];
-      else {  // label of row r; out-of-range labels (int64) clamp to -1 (the CE below turns them into NaN)
+      else {
         const int r = i - H - H2 - C;
         const long long l = r < rows ? d.labels[n0 + r] : 0;
         slab[r] = (l >= 0 && l < C) ? (int)l : -1;
       }
     }
+    if (d.p > 0.f && d.gen_keep) base = tspm_dropout_base(d.seed, ctr);
   }
-  uint64_t base = 0;
-  if (d.p > 0.f && d.gen_keep) base = tspm_dropout_base(d.seed, d.counter ? *d.counter : 0ULL);
   head_sync();
   TSPM_STAMP(tspm_g_stamps_misc, 1);
   // fc0 + ReLU + dropout (tspm_linear_fwd's epilogue order: + bias, relu, * keep*scale)
@@ -972,6 +999,8 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
     sh1[r * ldh + o] = v;
     if (r < rows) d.h1[(long long)(n0 + r) * H + o] = v;
   });
+  head_store(g3, v3);
+  head_store(g5, v5);
   head_sync();
   TSPM_STAMP(tspm_g_stamps_misc, 2);
   head_xwT<1>(sh1, ldh, sw3, ldh, H, H2, [&](int r, int o, float acc) {

@@ -75,6 +75,9 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.tspm_conv_dgrad(ctypes.byref(s64), ctypes.byref(v1), 16, 16, 16, 0, None, 0, None) == 1
     v3 = L.ConvAlgo(1, 1, 3, 1, 1, 1)
     assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(v3), 16, None, 16, 16, None, None, 0, None) == 1
+    stem_only = L.ConvAlgo(0, 0, 0, 0, 0, 3)  # variant 3: the 1-channel 7x7/2 stems only
+    assert lib.tspm_conv_fwd(ctypes.byref(good), ctypes.byref(stem_only), 16, None, 16, 16, None, None, 0, None) == 1
+    assert lib.tspm_conv_wgrad(ctypes.byref(good), ctypes.byref(stem_only), 16, None, 16, 16, None, 0, None) == 1
     vs = L.ConvAlgo(1, 1, 1, 4, 2, 1)  # BM = 32, split-K 2 without workspace
     s32 = L.ConvShape(32, 8, 8, 64, 64, 3, 3, 1, 1, 8, 8)
     assert lib.tspm_conv_fwd(ctypes.byref(s32), ctypes.byref(vs), 16, None, 16, 16, None, None, 0, None) == 3
