@@ -134,6 +134,7 @@ class EncoderEngine:
         # loader (tspm_conv_fwd_bnin: step 2.73 vs 2.70 ms); transposed wgrad operands (34.7k vs 36.1k
         # samples/s).  The ABI entry points stay, tested at the kernel level.)
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
+        self.bn_two_level = False  # BN statistics of many-tile layers merged in two levels inside the conv
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -280,7 +281,8 @@ class EncoderEngine:
         m = bn.module
         return L.BnFuse(self.bn_part.data_ptr(), self.bn_cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
                         BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                        bn.invstd.data_ptr(), 0, 0, 0)
+                        bn.invstd.data_ptr(), self.bn_cnt.numel() if self.bn_two_level else 0, 0,
+                        self.bn_part.numel() if self.bn_two_level else 0)
 
     def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
         """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
