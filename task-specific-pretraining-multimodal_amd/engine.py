@@ -129,12 +129,16 @@ class EncoderEngine:
         self.grad_of = grad_of or _default_grad_of
         # Every launch goes to the caller's current stream.  (Measured and removed, DESIGN §7: weight-grad
         # convs / the downsample branch on auxiliary streams — a replayed graph with their ~50 cross-stream
-        # edges ran ~30 % slower; BN statistics merged in two levels inside the conv (2.88 vs 2.83 ms); BN
+        # edges ran ~30 % slower; BN
         # backward partials in the dgrad epilogue (conv +5 us per launch, step unchanged); bn1 + ReLU in conv2's
         # loader (tspm_conv_fwd_bnin: step 2.73 vs 2.70 ms); transposed wgrad operands (34.7k vs 36.1k
         # samples/s).  The ABI entry points stay, tested at the kernel level.)
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
-        self.bn_two_level = False  # BN statistics of many-tile layers merged in two levels inside the conv
+        # BN statistics of the many-tile layers merged in two levels inside the conv forward (last arrivers,
+        # tspm_bn_fuse.counters_len / partial_floats) instead of a tspm_bn_finalize launch: the audio chain is
+        # the step's critical path this round (-5 us at batch 128, equal at 1024: profiles/r4/r4n_ab_bn2.json,
+        # r4o_ab_bn2_b1024.json; round 2, before the two chains were unbalanced, it was slower)
+        self.bn_two_level = True
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
