@@ -243,8 +243,10 @@ def mfma_counters(batch: int):
     MFMA pipe utilisation and where the conv waves' cycles go.  None if no summary for this batch."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_b{batch}_mfma_busy.json")),
-                   key=lambda p: int(re.search(r"r(\d+)_b", os.path.basename(p)).group(1)))
+    def ver(p):  # r<round>[_v<version>]_b<batch>_mfma_busy.json: newest = highest (round, version)
+        m = re.match(r"r(\d+)(?:_v(\d+))?_b\d+_mfma_busy\.json$", os.path.basename(p))
+        return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_b{batch}_mfma_busy.json")), key=ver)
     if not files:
         return None
     with open(files[-1]) as f:
