@@ -2,7 +2,8 @@
 
     python scripts/roofline_from_trace.py gpurun_out/<tag>_prof/run_kernel_trace.csv [valid_tap_flop_per_step]
 
-A step = the dispatches between consecutive Adam launches (k_adam closes every step).  Steps whose
+A step = the dispatches between consecutive step-count increments (k_adam_begin, once per step: the Adam
+update runs as several range launches since round 4); traces without it split at k_adam.  Steps whose
 kernel count equals the modal count are the graph-replayed training steps; for those it prints the
 summed conv-kernel duration per step, the busy time (union of the conv kernels' intervals) and the
 resulting fractions of the fp32 MFMA peak, plus the per-family kernel time — the same quantities
@@ -50,10 +51,11 @@ def main(path, flops=FLOPS):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
+    mark = "k_adam_begin(" if any("k_adam_begin(" in n for _, _, n in rows) else "k_adam("
     steps, cur = [], []
     for a, b, n in rows:
         cur.append((a, b, n))
-        if "k_adam(" in n:
+        if mark in n:
             steps.append(cur)
             cur = []
     mode = Counter(len(s) for s in steps).most_common(1)[0][0]
