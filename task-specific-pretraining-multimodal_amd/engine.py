@@ -135,10 +135,11 @@ class EncoderEngine:
         # samples/s).  The ABI entry points stay, tested at the kernel level.)
         self.conv_timer = None  # optional: begin(op, kind)/end() around every conv launch (bench roofline)
         # BN statistics of the many-tile layers merged in two levels inside the conv forward (last arrivers,
-        # tspm_bn_fuse.counters_len / partial_floats) instead of a tspm_bn_finalize launch: the audio chain is
-        # the step's critical path this round (-5 us at batch 128, equal at 1024: profiles/r4/r4n_ab_bn2.json,
-        # r4o_ab_bn2_b1024.json; round 2, before the two chains were unbalanced, it was slower)
-        self.bn_two_level = True
+        # tspm_bn_fuse.counters_len / partial_floats) instead of a tspm_bn_finalize launch.  Off: -5 us per step
+        # at batch 128 (within the box-to-box spread), equal at 1024 (profiles/r4/r4n_ab_bn2.json,
+        # r4o_ab_bn2_b1024.json), while the merge tails inflate the conv kernels' device time — the conv
+        # roofline that tracks the conv kernels reads 0.193 instead of 0.205 (profiles/r4_v1_bench.json)
+        self.bn_two_level = False
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
