@@ -37,7 +37,7 @@ enum {
 };
 
 /* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 16
+#define TSPM_ABI_VERSION 17
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -249,6 +249,15 @@ int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* runnin
                        int32_t res_mode, const float* res, const float* res_rmean, const float* res_rvar,
                        const float* res_gamma, const float* res_beta, int32_t relu, float* out,
                        tspm_stream_t stream);
+
+/* ABI 17: the encoder's last block apply with the adaptive average pool folded in.  Rows are
+ * position-major (row = p*n + sample, npos positions): out = tspm_bn_apply's result over the npos*n rows
+ * (tspm_bn_apply_eval's when eval != 0: mean / inv are then the running mean / variance and eps applies),
+ * and pooled[n][c] = (sum over p of out) / npos — tspm_avgpool_fwd of out — in the same launch. */
+int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const float* mean, const float* inv,
+                       const float* gamma, const float* beta, int32_t res_mode, const float* res,
+                       const float* res_mean, const float* res_inv, const float* res_gamma, const float* res_beta,
+                       int32_t relu, int32_t eval, float eps, float* out, float* pooled, tspm_stream_t stream);
 
 /* BN backward through  out = relu(BN(y) [+ BN2(y2)])  (y2 / second BN optional, may be NULL):
  *   g' = g * (out > 0)  (out may be NULL: no ReLU)

@@ -28,6 +28,7 @@ def build(batch, kw, dev):
     stem = kw.pop("_stem", None)    # stem forward algo override for both encoders, e.g. [0,0,0,0,0,3]
     stemw = kw.pop("_stemw", None)  # stem weight-gradient algo override
     bn2 = kw.pop("_bn2", None)      # encoders ("a", "i") whose BN statistics merge in two levels in the conv
+    pool = kw.pop("_pool", None)    # False: a separate tspm_avgpool_fwd launch after the last block's apply
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
     if stem is not None or stemw is not None:
         from tspm_amd import _lib as L
@@ -37,6 +38,8 @@ def build(batch, kw, dev):
             if stemw is not None:
                 e.stem.algo_wgrad = L.ConvAlgo(*stemw)
             e._alloc_workspace()
+    if pool is not None:
+        step.eng_a.fuse_pool = step.eng_i.fuse_pool = bool(pool)
     if bn2 is not None:
         step.eng_a.bn_two_level, step.eng_i.bn_two_level = "a" in bn2, "i" in bn2
     feed = bench.corpus_loader(step, batch, 1234, dev, 16384)

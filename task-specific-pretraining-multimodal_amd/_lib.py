@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 16
+ABI_VERSION = 17
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -128,6 +128,9 @@ _SIGS = {
                                 c_int64, _P]),
     "tspm_bn_apply_eval": (c_int32, [c_int64, c_int32, _P, _P, _P, c_float, _P, _P, c_int32, _P, _P, _P, _P, _P,
                                      c_int32, _P, _P]),
+    # ABI 17: the last block's apply with the average pool folded in
+    "tspm_bn_apply_pool": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_int32, _P, _P, _P, _P, _P,
+                                     c_int32, c_int32, c_float, _P, _P, _P]),
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),

@@ -160,6 +160,67 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
   }
 }
 
+// The encoder's last BasicBlock apply with the adaptive average pool over its npos positions folded in
+// (resnet.py:55-57 then :59-60): thread = (sample n, 4 channels), looping the positions — out as k_bn_apply
+// writes it (the backward reads it) and pooled[n] = (sum over p in order) / npos, as k_avgpool_fwd computes it.
+// One launch instead of apply + pool at the tail of each encoder's forward.
+template <int RES, bool RELU, bool EVAL>
+__global__ __launch_bounds__(256) void k_bn_apply_pool(int npos, int N, int C, const float* __restrict__ y,
+                                                       const float* __restrict__ mean, const float* __restrict__ inv,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       const float* __restrict__ res, const float* __restrict__ mean2,
+                                                       const float* __restrict__ inv2, const float* __restrict__ gamma2,
+                                                       const float* __restrict__ beta2, float eps, float* __restrict__ out,
+                                                       float* __restrict__ pooled) {
+  const int L = C >> 2;
+  const long long total = (long long)N * L, plane = (long long)N * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    f32x4 mu = ld4(mean + 4 * c4), iv = ld4(inv + 4 * c4);
+    if (EVAL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) iv[j] = 1.0f / sqrtf(iv[j] + eps);
+    }
+    const f32x4 sc = ld4(gamma + 4 * c4) * iv;
+    const f32x4 sf = ld4(beta + 4 * c4) - mu * sc;
+    f32x4 sc2 = {0.f, 0.f, 0.f, 0.f}, sf2 = sc2;
+    if (RES == 2) {
+      f32x4 mu2 = ld4(mean2 + 4 * c4), iv2 = ld4(inv2 + 4 * c4);
+      if (EVAL) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) iv2[j] = 1.0f / sqrtf(iv2[j] + eps);
+      }
+      sc2 = ld4(gamma2 + 4 * c4) * iv2;
+      sf2 = ld4(beta2 + 4 * c4) - mu2 * sc2;
+    }
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < npos; ++p) {
+      const long long off = p * plane + 4 * i;
+      const f32x4 v = ld4(y + off);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaf(v[j], sc[j], sf[j]);
+      if (RES == 1) {
+        o += ld4(res + off);
+      } else if (RES == 2) {
+        const f32x4 v2 = ld4(res + off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += fmaf(v2[j], sc2[j], sf2[j]);
+      }
+      if (RELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
+      }
+      st4(out + off, o);
+      s += o;
+    }
+    f32x4 q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = s[j] / (float)npos;
+    st4(pooled + 4 * i, q);
+  }
+}
+
 // Transposed-store helper of the tiled kernels: a [64 rows x 64 channels] tile staged in LDS
 // (tile[row][65]) is written as dst[c][ld_t] rows-contiguous (the wgrad operand layout) with 16-byte
 // stores, 4 consecutive threads per channel.  Requires (m % 4 == 0) and 16-byte aligned dst/ld_t.
@@ -948,6 +1009,36 @@ extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const fl
                                   tspm_stream_t stream) {
   return bn_apply_common(m, c, y, running_mean, running_var, gamma, beta, res_mode, res, res_rmean, res_rvar,
                          res_gamma, res_beta, relu, out, nullptr, 0, true, eps, stream);
+}
+
+#define BN_APPLY_POOL_LAUNCH(RES, RELU, EVAL)                                                               \
+  hipLaunchKernelGGL((k_bn_apply_pool<RES, RELU, EVAL>), dim3(ew_blocks(total)), dim3(256), 0, st, npos, n, c, y, \
+                     mean, inv, gamma, beta, res, mean2, inv2, gamma2, beta2, eps, out, pooled)
+
+extern "C" int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const float* mean,
+                                  const float* inv, const float* gamma, const float* beta, int32_t res_mode,
+                                  const float* res, const float* mean2, const float* inv2, const float* gamma2,
+                                  const float* beta2, int32_t relu, int32_t eval, float eps, float* out,
+                                  float* pooled, tspm_stream_t stream) {
+  if (npos <= 0 || n <= 0 || !c_ok(c) || !y || !mean || !inv || !gamma || !beta || !out || !pooled)
+    return TSPM_ERR_INVALID;
+  if (res_mode < 0 || res_mode > 2) return TSPM_ERR_INVALID;
+  if (res_mode >= 1 && !res) return TSPM_ERR_INVALID;
+  if (res_mode == 2 && (!mean2 || !inv2 || !gamma2 || !beta2)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const long long total = (long long)n * c / 4;
+  const bool r = relu != 0;
+  if (!eval) {
+    if (res_mode == 0) { if (r) BN_APPLY_POOL_LAUNCH(0, true, false); else BN_APPLY_POOL_LAUNCH(0, false, false); }
+    else if (res_mode == 1) { if (r) BN_APPLY_POOL_LAUNCH(1, true, false); else BN_APPLY_POOL_LAUNCH(1, false, false); }
+    else { if (r) BN_APPLY_POOL_LAUNCH(2, true, false); else BN_APPLY_POOL_LAUNCH(2, false, false); }
+  } else {
+    if (res_mode == 0) { if (r) BN_APPLY_POOL_LAUNCH(0, true, true); else BN_APPLY_POOL_LAUNCH(0, false, true); }
+    else if (res_mode == 1) { if (r) BN_APPLY_POOL_LAUNCH(1, true, true); else BN_APPLY_POOL_LAUNCH(1, false, true); }
+    else { if (r) BN_APPLY_POOL_LAUNCH(2, true, true); else BN_APPLY_POOL_LAUNCH(2, false, true); }
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
 }
 
 constexpr size_t kBwdBarrierBytes = 256;  // counters of the fused path (2 per channel block; zero before first use)

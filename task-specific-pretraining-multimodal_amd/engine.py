@@ -140,6 +140,9 @@ class EncoderEngine:
         # r4o_ab_bn2_b1024.json), while the merge tails inflate the conv kernels' device time — the conv
         # roofline that tracks the conv kernels reads 0.193 instead of 0.205 (profiles/r4_v1_bench.json)
         self.bn_two_level = False
+        # the last block's BN apply also writes the average-pooled features (tspm_bn_apply_pool, ABI 17): one
+        # launch less at the tail of each encoder's forward
+        self.fuse_pool = True
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
@@ -294,9 +297,23 @@ class EncoderEngine:
         per channel block, merges them (save_mean/invstd + running statistics): one launch."""
         self._conv_fwd(op, x_ptr, strides, y, sh, self._bnf(bn))
 
-    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True):
+    def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
+               pooled: Optional[torch.Tensor] = None):
         lib = L.lib()
         m = bn.module
+        if pooled is not None:  # the last block: the adaptive average pool in the same launch
+            h, w = self.final_hw
+            m2 = bn2.module if bn2 else None
+            if train:
+                st = (bn.mean, bn.invstd, bn2.mean if bn2 else None, bn2.invstd if bn2 else None)
+            else:
+                st = (m.running_mean, m.running_var, m2.running_mean if m2 else None, m2.running_var if m2 else None)
+            L.check(lib.tspm_bn_apply_pool(h * w, self.N, bn.channels, y.data_ptr(), st[0].data_ptr(), st[1].data_ptr(),
+                                           m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res), L.ptr(st[2]),
+                                           L.ptr(st[3]), L.ptr(m2.weight) if m2 else None,
+                                           L.ptr(m2.bias) if m2 else None, 1 if relu else 0, 0 if train else 1, m.eps,
+                                           out.data_ptr(), pooled.data_ptr(), sh), "bn_apply_pool")
+            return
         if train:
             L.check(lib.tspm_bn_apply(bn.rows, bn.channels, y.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
                                       m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res),
@@ -358,6 +375,7 @@ class EncoderEngine:
                                      self.mp_idx.data_ptr(), None, 0, sh), "maxpool_fwd")
         xin = self.mp
         for bp in self.blocks:
+            pool = self.pooled if (bp is self.blocks[-1] and self.fuse_pool) else None
             s1 = bp.conv1.shape
             xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
             if train:
@@ -376,12 +394,15 @@ class EncoderEngine:
                     self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
                 else:
                     self._conv_fwd(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=2, res=bp.yd, bn2=bp.ds_bn, relu=True, sh=sh, train=train,
+                            pooled=pool)
             else:
-                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train)
+                self._apply(bp.bn2, bp.y2, bp.out, res_mode=1, res=xin, relu=True, sh=sh, train=train, pooled=pool)
             xin = bp.out
-        h, w = self.final_hw
-        L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh), "avgpool_fwd")
+        if not self.fuse_pool:
+            h, w = self.final_hw
+            L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh),
+                    "avgpool_fwd")
         fc = self.enc.fc
         L.check(lib.tspm_linear_fwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
                                     fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb, sh),
