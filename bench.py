@@ -180,6 +180,75 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
     return out
 
 
+def _stats(xs):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    return {"mean": round(sum(xs) / len(xs), 4), "median": round(xs[len(xs) // 2], 4), "max": round(xs[-1], 4)}
+
+
+def exchange_block(step, one, args, world: int, ms_per_step: float) -> dict:
+    """How much of the DP gradient exchange the phased step hides (every rank takes part; after the timed
+    region).  (1) ``--exchange-steps`` more phased steps with ``FusedTrainStep.exchange_probe`` on: the host's
+    wait for each backward phase's step flag and the device time from the end of the fwd+bwd graph to the end
+    of the step — the exposed tail: the last phase's all-reduce and its Adam ranges, plus whatever of the
+    first two phases' exchange + Adam had not finished on the comm stream by then; (2) the same number of
+    LOCAL steps (the plain step re-captured: same kernels, no collective) timed like the headline, so
+    ``ms_per_step - local_step_ms`` is the exchange's total exposed cost.  Values are maxima over ranks."""
+    ar = step.allreduce
+    P = args.exchange_steps
+    probe = []
+    step.exchange_probe = probe
+    for i in range(P):
+        one(i)
+    torch.cuda.synchronize()
+    step.exchange_probe = None
+    w0 = [p["host_wait_ms"][0] for p in probe]
+    w1 = [p["host_wait_ms"][1] for p in probe]
+    tail = [p["events"][0].elapsed_time(p["events"][1]) for p in probe]
+    phase_bytes = [sum(v.numel() * 4 for v in ph) for ph in ar.phases]
+    step.allreduce, step.graph, step.graph_opt = None, None, None
+    for i in range(3):  # capture + settle the local step
+        one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(P):
+        one(i)
+    torch.cuda.synchronize()
+    local_ms = (time.perf_counter() - t0) / P * 1e3
+    vals = [local_ms, sum(tail) / len(tail), max(tail), sum(w0) / len(w0), sum(w1) / len(w1)]
+    if world > 1:
+        t = torch.tensor(vals, dtype=torch.float64, device=step.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        vals = t.tolist()
+    out = exchange_summary(vals, phase_bytes, [len(ph) for ph in ar.phases], world, ms_per_step, P)
+    out["rank0_tail_ms"] = _stats(tail)
+    out["rank0_host_wait_ms"] = {"phase0": _stats(w0), "phase1": _stats(w1)}
+    return out
+
+
+def exchange_summary(vals, phase_bytes, buckets, world: int, ms_per_step: float, steps: int) -> dict:
+    """The line's ``exchange`` block from [local_ms, tail_mean, tail_max, wait0_mean, wait1_mean] (maxima over
+    ranks; shared by the GPU bench and the gloo dry run)."""
+    return {"rccl_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": str(dist.get_backend()) if dist.is_initialized() else None,
+            "forced_1rank_exchange": world == 1,
+            "phases": len(phase_bytes), "bytes_per_phase": phase_bytes, "buckets_per_phase": buckets,
+            "steps_probed": steps,
+            "exposed_tail_ms_per_step": {"mean": round(vals[1], 4), "max": round(vals[2], 4)},
+            "host_wait_ms_per_step": {"phase0_flag_mean": round(vals[3], 4), "phase1_flag_mean": round(vals[4], 4)},
+            "local_step_ms": round(vals[0], 4),
+            "exchange_exposed_ms_per_step": round(ms_per_step - vals[0], 4),
+            "what": "phased DP step (ddp.PhasedGradAllReduce): the all-reduce of each backward phase starts when the "
+                    "host sees that phase's step flag and runs on the comm stream beside the rest of the backward; "
+                    "exposed tail = device time from the fwd+bwd graph's end to the step's end; local_step_ms = the "
+                    "same kernels without the collective, timed after the timed region; exchange_exposed = "
+                    "ms_per_step - local_step_ms (maxima over ranks)"}
+
+
 def subset_roofline(per_launch, pred, peak):
     """Valid-tap TFLOP/s of the launches (encoder, op, kind, us) satisfying ``pred(encoder, op)``."""
     if not per_launch:
@@ -258,7 +327,7 @@ def mfma_counters(batch: int):
              "frac_active_inst": c["frac_active_inst"]}
     return {"source": os.path.relpath(files[-1], REPO), "batch": batch,
             "mfma_busy_cycles_per_step": c["mfma_busy_cycles"] / max(1, d.get("steps_in_run", 1)),
-            "mfma_util": c["mfma_util_at_2p4GHz"], "mfma_util_at_measured_clock": c["mfma_util_at_measured_clock"],
+            "mfma_util": c["mfma_util_at_2p4GHz"], "clock": "priced at 2.4 GHz (the chip's maximum)",
             "wave_state": waits, "capping_state": max(waits, key=waits.get),
             "what": "SQ_VALU_MFMA_BUSY_CYCLES over the conv kernels' device time x 256 CUs x 4 SIMDs x clock "
                     "(64 busy cycles per f32 32x32x2 MFMA); wave_state = fractions of SQ_WAVE_CYCLES"}
@@ -938,7 +1007,10 @@ def check_world(gpus: int) -> None:
 def dry_run(args) -> None:
     """--dry-run: the multi-rank plumbing without a GPU — the same launch (torchrun env or spawn_ranks),
     process group (gloo), barrier-bracketed timed region, max over ranks and rank-0 JSON line as the
-    real bench, with an empty step.  Every rank reports (rank, pid, world size of the process group)."""
+    real bench, with an empty step; then the post-timed-region legs with the real line's keys: an
+    ``exchange`` block from a phased gloo all-reduce of a small flat buffer (host-timed), a ``roofline``
+    placeholder (no kernels ran) and — rank 0 only, every N, the other ranks waiting in a gloo barrier — the
+    oracle's CPU train step for ``--cpu-budget`` seconds.  Every rank reports (rank, pid, world size)."""
     from tspm_amd import ddp
     rank, world, _ = ddp.init_from_env("gloo")
     B = args.batch_per_rank
@@ -958,12 +1030,38 @@ def dry_run(args) -> None:
     else:
         allr = [me]
     el = max(float(t[3]) for t in allr)
+    ms_per_step = el / max(args.steps, 1) * 1e3
+    exchange = None
+    if world > 1 and args.exchange_steps > 0:
+        flat = torch.ones(3 * 1024)
+        ar = ddp.PhasedGradAllReduce([[flat[:1024]], [flat[1024:2048]], [flat[2048:]]], bucket_mb=0.002)
+        tails = []
+        for _ in range(args.exchange_steps):
+            t1 = time.perf_counter()
+            for k in range(3):
+                ar.wait(ar.launch(k))
+            tails.append((time.perf_counter() - t1) * 1e3)
+        vals = torch.tensor([0.0, sum(tails) / len(tails), max(tails), 0.0, 0.0], dtype=torch.float64)
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        exchange = exchange_summary(vals.tolist(), [v.numel() * 4 for ph in ar.phases for v in ph[:1]],
+                                    [len(ph) for ph in ar.phases], world, ms_per_step, args.exchange_steps)
+        exchange["dry_run"] = "gloo all-reduce of a 12 KB flat buffer in 3 phases, host-timed; no step ran"
+    res = None
     if rank == 0:
-        emit({"metric": METRIC, "value": round(world * B * args.steps / el, 2), "unit": "samples/sec",
-              "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-              "process_group_world_size": int(allr[0][2]),
-              "ranks": [{"rank": int(t[0]), "pid": int(t[1]), "pg_world_size": int(t[2])} for t in allr],
-              "config": {"per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"}})
+        res = {"metric": METRIC, "value": round(world * B * args.steps / el, 2), "unit": "samples/sec",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+               "process_group_world_size": int(allr[0][2]),
+               "ranks": [{"rank": int(t[0]), "pid": int(t[1]), "pg_world_size": int(t[2])} for t in allr],
+               "config": {"per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+               "roofline": {"bound": "mfma", "achieved": None, "frac": None, "r34_3x3": None,
+                            "dry_run": "no kernels ran (the GPU bench's rank 0 profiles its local step here)"},
+               "exchange": exchange}
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(B, args.cpu_budget)
+    if world > 1:
+        dist.barrier()  # gloo: the other ranks sleep here while rank 0 times the CPU baseline
+    if rank == 0:
+        emit(res)
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -1000,6 +1098,8 @@ def main() -> None:
     ap.add_argument("--mosi-corpus", type=int, default=4096, help="samples in the HBM-resident MOSI corpus")
     ap.add_argument("--profile-steps", type=int, default=10,
                     help="step replays profiled after the timed region for the roofline (0: skip)")
+    ap.add_argument("--exchange-steps", type=int, default=20,
+                    help="DP exchange probe: phased steps probed + local steps timed after the timed region (0: skip)")
     ap.add_argument("--pcie-steps", type=int, default=20,
                     help="steps of the secondary PCIe-inclusive measurement (0: skip)")
     ap.add_argument("--kernel-table", default=None, help="write the per-launch conv durations (JSON) here")
@@ -1080,10 +1180,21 @@ def main() -> None:
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
+    # ---- after the timed region: how much of the DP exchange the step hides (every rank) -----------
+    exchange = None
+    if isinstance(step.allreduce, ddp.PhasedGradAllReduce) and step.use_graph and args.exchange_steps > 0:
+        exchange = exchange_block(step, one, args, world, ms_per_step)
+    # from here on every rank runs the LOCAL step (same kernels, no collective), so rank 0 can profile and
+    # time the CPU baseline alone; the other ranks wait on a CPU (gloo) barrier, which sleeps in a socket read
+    # instead of spinning on the GPU or a host core
+    if step.allreduce is not None:
+        step.allreduce, step.graph, step.graph_opt = None, None, None
+    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+
     # ---- roofline: device kernel durations of further step replays (outside the timed region) ----
     R = args.profile_steps
     roof = None
-    if R > 0 and world == 1 and step.use_graph:
+    if R > 0 and rank == 0 and step.use_graph:
         seq = []
         concurrent = lambda: one(0)  # noqa: E731  (the benched graph)
         step.graph, step.serial = None, True  # re-capture on ONE stream, recording the launch order
@@ -1099,7 +1210,7 @@ def main() -> None:
 
     # ---- secondary: the PCIe-inclusive step (a pinned host batch copied H2D each step) -----------
     pcie = None
-    if args.pcie_steps > 0:
+    if args.pcie_steps > 0 and rank == 0:
         import numpy as np
         from tspm_amd.data import default_lut, synthetic_corpus
         hc = synthetic_corpus(B, seed=4321 + rank)  # a host batch in the collated layout (input data, untimed)
@@ -1205,14 +1316,29 @@ def main() -> None:
                        "per_rank_batch": B, "global_batch": B * world, "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "roofline": rl,
+            "exchange": exchange,
             "pcie_inclusive": pcie,
             "final_loss": round(loss, 5),
             "process_group": process_group_info(),
         }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if world > 1:
+            rl["timing"] += ("; at N > 1 rank 0 profiles its local step (the same conv launches without the "
+                             "collective) after the timed region while the other ranks wait")
+    if rank == 0 and not args.no_cpu_baseline:
+        # the reference CPU train step on this host (rank 0 only, every N: north_star's 'alongside the reference
+        # CPU train step'); the other ranks sleep in the gloo barrier below meanwhile
         result["cpu_baseline"] = cpu_baseline(B, args.cpu_budget)
+        if world > 1:
+            result["cpu_baseline"]["note"] = (f"timed on rank 0's host after the timed region, the other {world - 1} "
+                                              "ranks idle in a gloo barrier")
     if rank == 0:
         emit(result)
+    if cpu_group is not None:
+        dist.barrier(group=cpu_group)
+    # explicit teardown order: every stream idle, graphs and step flags released, THEN the
+    # process group
+    step.close()
+    torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -36,8 +36,10 @@ enum {
   TSPM_ERR_WORKSPACE = 3, /* caller-provided workspace too small */
 };
 
-/* Version of this ABI (bumped on any signature change). */
-#define TSPM_ABI_VERSION 17
+/* Version of this ABI (bumped on any signature change; 18 = round 5: the entry points no step calls removed —
+ * tspm_conv_fwd_bnin, tspm_conv_wgrad_t, tspm_conv_dgrad_bnfuse / _bwd_bnfuse / _dgrad_bn_tiles,
+ * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles). */
+#define TSPM_ABI_VERSION 18
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -121,24 +123,6 @@ typedef struct tspm_bn_fuse {
 int tspm_conv_fwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
                   const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
                   void* workspace, size_t workspace_bytes, tspm_stream_t stream);
-/* ABI 15: tspm_conv_fwd whose input is the PRE-BatchNorm output of the previous conv (BasicBlock's
- * conv1 -> bn1 -> relu -> conv2, resnet.py:41-45): the operand loader applies relu(x * scale + shift) with
- * scale = gamma * invstd, shift = beta - mean * scale per input channel (train-mode batch statistics —
- * exactly tspm_bn_apply's arithmetic, so the results are bitwise those of tspm_bn_apply + tspm_conv_fwd),
- * and writes the activation it formed to x_out (same HWNC layout as x; each element once, by the
- * workgroups that load it as the centre tap of the first output-channel block).  Replaces one
- * tspm_bn_apply launch and its pass over the activation.  Variant 1 (LDS-staged), stride 1, square
- * odd kernel with pad = r / 2 only; otherwise TSPM_ERR_INVALID (the caller keeps tspm_bn_apply). */
-typedef struct tspm_bn_input {
-  const float* mean;    /* save_mean of the BatchNorm over x */
-  const float* invstd;  /* save_invstd */
-  const float* gamma;
-  const float* beta;
-  float* x_out;         /* relu(bn(x)), HWNC like x */
-} tspm_bn_input;
-int tspm_conv_fwd_bnin(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x,
-                       const tspm_strides4* x_strides, const float* w, float* y, const tspm_bn_fuse* bn,
-                       const tspm_bn_input* bn_in, void* workspace, size_t workspace_bytes, tspm_stream_t stream);
 int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 /* Buffer sizes that enable the two-level in-launch BN merge (tspm_bn_fuse.counters_len /
@@ -165,16 +149,6 @@ int tspm_conv_wgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, co
                     size_t workspace_bytes, tspm_stream_t stream);
 size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
-/* Transposed copies.  tspm_bn_apply (out_t), tspm_bn_bwd (dy_t, dy2_t) and tspm_maxpool_fwd (y_t)
- * can also write their HWNC output transposed: t[c][ld_t] with the m = (h*W + w)*N + n rows of
- * channel c contiguous (ld_t >= m, ld_t % 4 == 0, m % 4 == 0, 16-byte aligned).  That is the
- * operand layout of tspm_conv_wgrad_t: both GEMM operands of the weight gradient become 16-byte
- * loads of 4 consecutive rows.  Same result as tspm_conv_wgrad (same reduction order up to the
- * fp32 rounding of the split sums); needs n % 8 == 0.  Workspace: tspm_conv_wgrad_workspace. */
-int tspm_conv_wgrad_t(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* x_t,
-                      int64_t ldx, const float* dy_t, int64_t ldy, float* dw, void* workspace,
-                      size_t workspace_bytes, tspm_stream_t stream);
-
 /* Input AND weight gradient of one convolution in ONE launch (both algos variant 1): the dgrad and
  * wgrad implicit GEMMs read the same dy and are independent, and at batch 128 either alone leaves
  * most of the 256 CUs idle, so their workgroups share one grid.  Results are bitwise those of
@@ -188,30 +162,6 @@ int tspm_conv_bwd(const tspm_conv_shape* shape, const tspm_conv_algo* algo_dgrad
                   const tspm_conv_algo* algo_wgrad, const float* x, const tspm_strides4* x_strides,
                   const float* dy, const float* w, float* dx, int32_t beta, float* dw, void* ws_dgrad,
                   size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, tspm_stream_t stream);
-/* BatchNorm-backward partial sums in the data-gradient epilogue (ABI 13): when the conv's input
- * gradient dx is the FINAL gradient g of a `relu(BN(y) [+ BN2(y2)])` output `out` (beta = 1: dx
- * accumulates onto the other contributions first), the epilogue also writes, per row tile of
- * tspm_conv_dgrad_bn_tiles rows-tiles and channel, sum g', sum g'(y - mean) [, sum g'(y2 - mean2)]
- * with g' = g * (out > 0) into `partial` (3 planes of [tiles][c]; out / y2 / mean2 nullable) —
- * the input of tspm_bn_bwd_apply.  LDS-staged (variant 1) algorithms only. */
-typedef struct tspm_bn_bwd_fuse {
-  float* partial;
-  const float* out;
-  const float* y;
-  const float* mean;
-  const float* y2;
-  const float* mean2;
-} tspm_bn_bwd_fuse;
-int32_t tspm_conv_dgrad_bn_tiles(const tspm_conv_shape* shape, const tspm_conv_algo* algo);  /* 0: unsupported */
-int tspm_conv_dgrad_bnfuse(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy, const float* w,
-                           float* dx, int32_t beta, void* workspace, size_t workspace_bytes,
-                           const tspm_bn_bwd_fuse* bn, tspm_stream_t stream);
-int tspm_conv_bwd_bnfuse(const tspm_conv_shape* shape, const tspm_conv_algo* dgrad_algo,
-                         const tspm_conv_algo* wgrad_algo, const float* x, const tspm_strides4* x_strides,
-                         const float* dy, const float* w, float* dx, int32_t beta, float* dw, void* ws_dgrad,
-                         size_t ws_dgrad_bytes, void* ws_wgrad, size_t ws_wgrad_bytes, const tspm_bn_bwd_fuse* bn,
-                         tspm_stream_t stream);
-
 /* ------------------------------------------------------------------------------------------------
  * BatchNorm2d, training mode (batch statistics over N*H*W, biased variance for normalisation,
  * unbiased for running_var, momentum 0.1, eps 1e-5) — resnet.py:26,31,138,177.
@@ -264,11 +214,10 @@ int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const
  *   dgamma = sum(g' * xhat), dbeta = sum(g')          (written, not accumulated)
  *   dy  = gamma*invstd*(g' - dbeta/M - xhat*dgamma/M)
  *   dy2 likewise for the second BN; if dres != NULL it receives g' (identity residual grad).
- * dy_t / dy2_t (nullable): also write dy / dy2 transposed, [c][ld_t] (see "transposed copies").
- * Workspace: tspm_bn_bwd_workspace bytes; its first 256 bytes hold the barrier counters of the
- * single-launch path (ABI 13: layers whose [rows x 64-channel] grid fits 256 workgroups run partial
- * sums, merge and apply in ONE launch) — zero them before the first call; every call leaves them zero.
- * One workspace must not be used by two launches in flight at once. */
+ * dy_t / dy2_t (nullable): also write dy / dy2 transposed, [c][ld_t] with the m = (h*W + w)*N + n rows of
+ * channel c contiguous (ld_t >= m, ld_t % 4 == 0, 16-byte aligned); no step uses them.
+ * Workspace: tspm_bn_bwd_workspace bytes (per-tile partial sums); one workspace must not be used by two
+ * launches in flight at once. */
 int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y,
                 const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                 float* dy, const float* y2, const float* mean2, const float* invstd2,
@@ -276,22 +225,6 @@ int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const fl
                 float* dy_t, float* dy2_t, int64_t ld_t, void* workspace, size_t workspace_bytes,
                 tspm_stream_t stream);
 size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
-/* BN backward with the partial sums already computed (ABI 13): by the producing conv's data-gradient
- * epilogue (tspm_conv_dgrad_bnfuse / tspm_conv_bwd_bnfuse) as `tiles` row tiles, 3 planes of
- * [tiles][c] floats (sum g', sum g'(y - mean), sum g'(y2 - mean2)).  Merges them per channel in double
- * (fixed order) and applies — one launch instead of tspm_bn_bwd's two.  Same arguments and results
- * as tspm_bn_bwd otherwise (no transposed copies).  tiles <= tspm_bn_bwd_apply_max_tiles(). */
-int tspm_bn_bwd_apply(int64_t m, int32_t c, int32_t tiles, const float* partial, const float* g, const float* out,
-                      const float* y, const float* mean, const float* invstd, const float* gamma, float* dgamma,
-                      float* dbeta, float* dy, const float* y2, const float* mean2, const float* invstd2,
-                      const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres,
-                      tspm_stream_t stream);
-int32_t tspm_bn_bwd_apply_max_tiles(void);
-/* Diagnostics (ABI 13): how many in-launch barrier waits of the single-launch BN backward timed out
- * since the library was loaded (0 in a healthy run; a timed-out launch writes NaN gradients instead
- * of hanging).  0xffffffff if the counter cannot be read. */
-uint32_t tspm_debug_barrier_timeouts(void);
-
 /* ------------------------------------------------------------------------------------------------
  * Pooling — nn.MaxPool2d(3, 2, 1) (resnet.py:140,208) and AdaptiveAvgPool2d(1)+flatten (:149,215-216)
  * ----------------------------------------------------------------------------------------------*/
@@ -571,11 +504,6 @@ int tspm_bn1d_fwd(int32_t m, int32_t c, const float* x, const float* gamma, cons
  * dx = gamma*invstd*(g - dbeta/m - xhat*dgamma/m). */
 int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* x, const float* mean, const float* invstd,
                   const float* gamma, float* dgamma, float* dbeta, float* dx, tspm_stream_t stream);
-/* tspm_bn1d_bwd fused with the backward of the MaxOut(2)+Dropout that produced x (ABI 11): instead of
- * dx, writes da[m, 2c] exactly as tspm_maxout_bwd(dx, a, keep, keep_scale) would (bitwise). */
-int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
-                         const float* invstd, const float* gamma, float* dgamma, float* dbeta, const float* a,
-                         const uint8_t* keep, float keep_scale, float* da, tspm_stream_t stream);
 /* BatchNorm1d followed by Dropout (FcClassifier(use_bn=True): Linear -> ReLU -> BatchNorm1d -> Dropout,
  * models/msa/networks/classifier.py:98-104; ABI 14): tspm_bn1d_fwd, then y *= keep ? keep_scale : 0
  * (keep uint8 [m, c], nullable = no dropout). */

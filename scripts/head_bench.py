@@ -68,9 +68,9 @@ def main():
             torch.cuda.synchronize()
             L.check(lib.tspm_head_train_step(ctypes.byref(d), torch.cuda.current_stream().cuda_stream), "head")
             torch.cuda.synchronize()
-            buf = np.zeros((1 << 18) * 8, dtype=np.uint64)
+            buf = np.zeros((1 << 18) * 12, dtype=np.uint64)
             assert lib.tspm_debug_stamps_misc(buf.ctypes.data, buf.nbytes) == 0
-            st = buf.reshape(-1, 8).astype(np.int64)
+            st = buf.reshape(-1, 12).astype(np.int64)
             st = st[st[:, 0] > 0]
             rel = (st[:, :6] - st[:, 0].min()) * 0.01
             names = ["entry", "staged", "fc0", "fc3+fc5", "CE", "bwd (dz3, dz0, dx)"]

@@ -5,9 +5,10 @@ scripts/pmc_mfma.sh (verdict r3 item 3).
 
 Units (calibrated here, not assumed): SQ_VALU_MFMA_BUSY_CYCLES advances 64 per v_mfma_f32_32x32x2_f32
 (= its issue cycles on one SIMD; the conv family's per-step sum equals 64 x the valid-tap FLOPs / 4096
-within 0.5 %), so MFMA utilisation = MFMA_BUSY / (dispatch duration x clock x 1,024 SIMDs).  The clock
-under the counter pass is GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md "DVFS give-back";
-reads high on short dispatches), so both the 2.4 GHz figure and the measured-clock figure are given.
+within 0.5 %), so MFMA utilisation = MFMA_BUSY / (dispatch duration x 2.4 GHz x 1,024 SIMDs).  No
+measured-clock figure: GRBM_GUI_ACTIVE / 8 / duration reads high on dispatches shorter than ~0.3 ms
+(MI355X_MICROARCH.md "DVFS give-back") and gave 2.3-6.7 GHz on these 5-60 us kernels,
+so the utilisation is priced at the chip's maximum clock only (a lower bound on the in-kernel rate).
 SQ_WAVE_CYCLES = SQ_WAIT_ANY (parked at s_waitcnt / s_barrier) + SQ_WAIT_INST_ANY (issue-stalled: MFMA
 pipe / dependency / LDS issue) + SQ_ACTIVE_INST_ANY (issuing); the fractions are of SQ_WAVE_CYCLES over
 ALL waves of the kernel (loader waves included).  A step = the dispatches from one input gather to the next (else between consecutive k_adam
@@ -99,12 +100,9 @@ def summarise(issue_dir, lds_dir):
         dur = c["dur_ns"] * 1e-9
         wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
-        clk = c.get("GRBM_GUI_ACTIVE", 0.0) / 8 / dur if dur else None
         out = {"launches": int(c["launches"]), "device_us": round(c["dur_ns"] / 1e3, 2),
                "mfma_busy_cycles": busy, "mfma_count_f32_32x32x2": busy / 64,
                "mfma_util_at_2p4GHz": round(busy / (dur * CLOCK_MAX_HZ * SIMDS), 4) if dur else None,
-               "clock_GHz_from_GRBM": round(clk / 1e9, 3) if clk else None,
-               "mfma_util_at_measured_clock": round(busy / (dur * clk * SIMDS), 4) if dur and clk else None,
                "wave_cycles": c.get("SQ_WAVE_CYCLES"),
                "frac_wait_any": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 4),
                "frac_wait_inst_any": round(c.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4),

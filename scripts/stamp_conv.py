@@ -27,7 +27,7 @@ from tspm_amd import _lib as L  # noqa: E402
 from conv_bench import step_ops  # noqa: E402
 from tune_convs import Bufs, launcher  # noqa: E402
 
-SLOTS = 8
+SLOTS = 12  # TSPM_STAMP_SLOTS (common.h)
 
 
 def main():
@@ -94,6 +94,14 @@ def report(lib, kind, key, s, xs, b, algo):
             clk = (st[ok, 7] - st[ok, 6]) / ((st[ok, 5] - st[ok, 0]) * 0.01)  # cycles per us = MHz
             print(f"   in-kernel clock: p10 {np.percentile(clk, 10):.0f}  p50 {np.percentile(clk, 50):.0f}  "
                   f"p90 {np.percentile(clk, 90):.0f} MHz")
+        lc = st[:, 11] > 0  # compute waves of the LDS kernels: per-stage shader cycles (conv_lds.hip LoopClock)
+        if lds_variant and lc.any():
+            n = st[lc, 11].astype(np.float64)
+            per = {nm: st[lc, k] / n for k, nm in ((8, "barrier"), (9, "frag rd"), (10, "mfma"))}
+            tot = per["barrier"] + per["frag rd"] + per["mfma"]
+            print(f"   loop, cycles/stage (compute waves, {int(lc.sum())}; stages p50 {np.percentile(n, 50):.0f}): " +
+                  "  ".join(f"{k} p50 {np.percentile(v, 50):.0f}" for k, v in per.items()) +
+                  f"  -> mfma share p50 {np.percentile(per['mfma'] / tot, 50):.2f}")
         for i, j, nm in pairs:
             d = st[:, i] - st[:, j]
             ok = (st[:, i] > 0) & (st[:, j] > 0)

@@ -60,9 +60,9 @@ def stamps(lib, fn, names):
     torch.cuda.synchronize()
     fn()
     torch.cuda.synchronize()
-    buf = np.zeros((1 << 18) * 8, dtype=np.uint64)
+    buf = np.zeros((1 << 18) * 12, dtype=np.uint64)
     assert lib.tspm_debug_stamps_stem(buf.ctypes.data, buf.nbytes) == 0
-    st = buf.reshape(-1, 8).astype(np.int64)
+    st = buf.reshape(-1, 12).astype(np.int64)
     st = st[st[:, 0] > 0]
     t0 = st[:, 0].min()
     out = {"waves": int(len(st)), "span_us": round(float((st[:, :len(names)].max() - t0) * 0.01), 2),

@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 17
+ABI_VERSION = 18
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -38,12 +38,6 @@ class ConvAlgo(Structure):
     _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits", "variant")]
 
 
-class BnBwdFuse(Structure):
-    """tspm_bn_bwd_fuse: BN-backward partial sums written by a dgrad epilogue."""
-    _fields_ = [("partial", c_void_p), ("out", c_void_p), ("y", c_void_p), ("mean", c_void_p), ("y2", c_void_p),
-                ("mean2", c_void_p)]
-
-
 class Strides4(Structure):
     _fields_ = [(n, c_int64) for n in ("sn", "sh", "sw", "sc")]
 
@@ -54,12 +48,6 @@ class BnFuse(Structure):
                 ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float), ("save_mean", c_void_p),
                 ("save_invstd", c_void_p), ("counters_len", c_int32), ("reserved_", c_int32),
                 ("partial_floats", c_int64)]
-
-
-class BnInput(Structure):
-    """tspm_bn_input (ABI 15): the BatchNorm + ReLU a tspm_conv_fwd_bnin applies to its input operand."""
-    _fields_ = [("mean", c_void_p), ("invstd", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
-                ("x_out", c_void_p)]
 
 
 class AdamHyper(Structure):
@@ -104,8 +92,6 @@ _SIGS = {
     "tspm_status_string": (ctypes.c_char_p, [c_int32]),
     "tspm_conv_fwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, POINTER(BnFuse),
                                 _P, c_size_t, _P]),
-    "tspm_conv_fwd_bnin": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P,
-                                     POINTER(BnFuse), POINTER(BnInput), _P, c_size_t, _P]),
     "tspm_conv_fwd_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_tile_rows": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_fwd_bn_counters": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
@@ -115,8 +101,6 @@ _SIGS = {
     "tspm_conv_dgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
     "tspm_conv_wgrad": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P, _P, c_size_t, _P]),
     "tspm_conv_wgrad_workspace": (c_size_t, [POINTER(ConvShape), POINTER(ConvAlgo)]),
-    "tspm_conv_wgrad_t": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, c_int64, _P, c_int64, _P, _P, c_size_t,
-                                    _P]),
     "tspm_conv_bwd_supported": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), POINTER(Strides4)]),
     "tspm_conv_bwd": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), _P, POINTER(Strides4), _P, _P,
                                 _P, c_int32, _P, _P, c_size_t, _P, c_size_t, _P]),
@@ -134,14 +118,6 @@ _SIGS = {
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
-    "tspm_bn_bwd_apply": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 18 + [_P]),
-    "tspm_bn_bwd_apply_max_tiles": (c_int32, []),
-    "tspm_conv_dgrad_bn_tiles": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo)]),
-    "tspm_conv_dgrad_bnfuse": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), _P, _P, _P, c_int32, _P, c_size_t,
-                                         POINTER(BnBwdFuse), _P]),
-    "tspm_conv_bwd_bnfuse": (c_int32, [POINTER(ConvShape), POINTER(ConvAlgo), POINTER(ConvAlgo), _P, POINTER(Strides4),
-                                       _P, _P, _P, c_int32, _P, _P, c_size_t, _P, c_size_t, POINTER(BnBwdFuse), _P]),
-    "tspm_debug_barrier_timeouts": (ctypes.c_uint32, []),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),
@@ -191,7 +167,6 @@ _SIGS = {
     "tspm_bn1d_fwd_drop": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P, c_float, _P,
                                      _P]),
     "tspm_bn1d_bwd_drop_relu": (c_int32, [c_int32, c_int32, _P, _P, c_float, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "tspm_bn1d_bwd_maxout": (c_int32, [c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, c_float, _P, _P]),
     "tspm_bn1d_fwd_pair": (c_int32, [c_int32] + ([c_int32, _P, _P, _P, _P, _P, c_float, c_float, _P, _P, _P] * 2)
                            + [_P]),
     "tspm_bn1d_bwd_pair": (c_int32, [c_int32] + ([c_int32] + [_P] * 8) * 2 + [_P]),
@@ -318,9 +293,27 @@ class DeviceFlag:
         check(lib().tspm_flag_bump(self.handle, sh), "flag_bump")
 
     def host_wait(self, value: int, timeout_ms: int = 60000) -> None:
+        if not self.handle:
+            raise TspmError("DeviceFlag used after close()")
         check(lib().tspm_flag_host_wait(self.handle, int(value), int(timeout_ms)), "flag_host_wait (timeout)")
 
-    def __del__(self):
+    def close(self) -> None:
+        """Free the flag's device word and pinned host word.  Only call this once no captured graph that
+        bumps the flag can run again and the device is idle (``FusedTrainStep.close`` does both first):
+        ``tspm_flag_destroy`` synchronises the device and frees memory."""
         h, self.handle = getattr(self, "handle", None), None
         if h and _lib is not None:
-            _lib.tspm_flag_destroy(h)
+            check(_lib.tspm_flag_destroy(h), "flag_destroy")
+
+    def __del__(self):
+        # No HIP call at garbage-collection time: a collection can run while another stream is being
+        # captured (where hipFree / hipHostFree are illegal), while a graph that bumps this flag is still
+        # alive, or during the process group's teardown.  A flag nobody closed leaks its 128 bytes.
+        self.handle = None
+
+
+def linear_bwd(n, fin, fout, x, ldx, dy, ldy, w, dw, db, dx, lddx, stream) -> None:
+    """Backward of one nn.Linear (AVMNIST head / encoder fc, monomodal classifier, MMIMDb, MOSI): dw = dy^T @ x
+    (+ db = column sums of dy) and, if dx is given, dx = dy @ w — ONE ``tspm_linear_bwd`` launch (bitwise the two
+    separate products; 2.88 -> 2.81 ms per AVMNIST step when introduced)."""
+    check(lib().tspm_linear_bwd(n, fin, fout, x, ldx, dy, ldy, w, dw, db, dx, lddx, stream), "linear_bwd")

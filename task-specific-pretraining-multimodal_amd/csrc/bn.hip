@@ -566,238 +566,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int 
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Single-launch backward (partial sums + merge + apply) with an in-launch barrier per channel block.
-// Workgroup = [16*U rows x 64 channels]; its g' (= g masked by out > 0), y [, y2] stay in registers
-// across the barrier, so HBM sees every operand once (the two-launch path reads them twice) and the
-// partial-sum launch disappears.  Barrier: every workgroup of a channel block publishes its partial
-// sums (agent-scope stores), draws an arrival ticket, and waits until all Gx row blocks of the block
-// have arrived; the last to leave re-arms the counters.  All workgroups of the grid must be able to
-// be resident together: the host only takes this path for grids <= kBarrierMaxWgs of these
-// workgroups (>= 2 fit per CU by VGPRs, 6 by LDS), so two such launches on concurrent streams still
-// fit every XCD with room to spare.  The wait is bounded (kBarrierSpinLimit polls): a launch that cannot complete it writes
-// NaN gradients and counts tspm_g_barrier_timeouts instead of hanging.  The merge reads the Gx
-// partials in a fixed order in double (thread (lane, rg) sums row blocks rg, rg+16, ... then a fixed
-// 16-way LDS tree), so every workgroup derives bitwise the same coefficients.
-// ------------------------------------------------------------------------------------------------
-constexpr int kBarrierMaxWgs = 192;
-constexpr int kBarrierSpinLimit = 1 << 20;  // ~1 s of polling
-__device__ unsigned tspm_g_barrier_timeouts;
-
-// Thread 0: arrive, wait for `total` arrivals, leave (the last to leave re-arms both counters).
-// Returns false (in every thread) when the wait timed out.
-TSPM_DEV bool block_barrier(unsigned* arrive, unsigned* depart, unsigned total, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // The data exchanged across the barrier is written and read with agent-scope (cache-bypassing)
-  // atomics, completed by the vmcnt wait above: no L2 writeback / invalidate fences needed.
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1, it = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it > kBarrierSpinLimit) {
-        ok = 0;
-        __hip_atomic_fetch_add(&tspm_g_barrier_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    const unsigned prev = __hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == total - 1) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = ok;
-  }
-  __syncthreads();
-  const bool ok = *flag != 0;
-  __syncthreads();
-  return ok;
-}
-
-TSPM_DEV void st4_agent(float* p, const f32x4& v) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-TSPM_DEV f32x4 ld4_agent(const float* p) {
-  f32x4 v;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v;
-}
-
-template <bool HAS_OUT, bool TWO, bool DRES, int U>
-__global__ __launch_bounds__(256) void k_bn_bwd_fused(long long M, int C, int Gx, const float* __restrict__ g,
-                                                      const float* __restrict__ out, const float* __restrict__ y,
-                                                      const float* __restrict__ mean, const float* __restrict__ inv,
-                                                      const float* __restrict__ gamma, const float* __restrict__ y2,
-                                                      const float* __restrict__ mean2, const float* __restrict__ inv2,
-                                                      const float* __restrict__ gamma2, float* __restrict__ dgamma,
-                                                      float* __restrict__ dbeta, float* __restrict__ dgamma2,
-                                                      float* __restrict__ dbeta2, float* __restrict__ dy,
-                                                      float* __restrict__ dy2, float* __restrict__ dres,
-                                                      float* __restrict__ part, unsigned* __restrict__ bar) {
-  __shared__ double red[3][4][256];  // the partial-sum staging (sh) aliases it before the barrier
-  __shared__ f32x4 scoef[6][16];
-  __shared__ int flag;
-  f32x4(*sh)[256] = reinterpret_cast<f32x4(*)[256]>(&red[0][0][0]);
-  const int t = threadIdx.x, lane = t & 15, rg = t >> 4;
-  const int c4 = blockIdx.y * 16 + lane;
-  const bool cok = 4 * c4 < C;
-  constexpr long long RPB = 16LL * U;
-  const long long r_begin = blockIdx.x * RPB;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 mu = cok ? ld4(mean + 4 * c4) : z4;
-  const f32x4 mu2 = (TWO && cok) ? ld4(mean2 + 4 * c4) : z4;
-  f32x4 gv[U], yv[U], y2v[U];
-  f32x4 sg = z4, sx = z4, sx2 = z4;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const long long row = r_begin + rg + 16 * u;
-    if (cok && row < M) {
-      const long long off = row * C + 4 * c4;
-      gv[u] = ld4(g + off);
-      if (HAS_OUT) {
-        const f32x4 ov = ld4(out + off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gv[u][j] = ov[j] > 0.f ? gv[u][j] : 0.f;
-      }
-      yv[u] = ld4(y + off);
-      if (TWO) y2v[u] = ld4(y2 + off);
-    } else {
-      gv[u] = z4;
-      yv[u] = mu;
-      if (TWO) y2v[u] = mu2;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    sg += gv[u];
-    sx += gv[u] * (yv[u] - mu);
-    if (TWO) sx2 += gv[u] * (y2v[u] - mu2);
-  }
-  sh[0][t] = sg;
-  sh[1][t] = sx;
-  if (TWO) sh[2][t] = sx2;
-  __syncthreads();
-  const long long plane = (long long)Gx * C;
-  if (rg == 0 && cok) {
-    for (int k = 1; k < kRowGroups; ++k) {
-      sg += sh[0][k * 16 + lane];
-      sx += sh[1][k * 16 + lane];
-      if (TWO) sx2 += sh[2][k * 16 + lane];
-    }
-    st4_agent(part + (long long)blockIdx.x * C + 4 * c4, sg);
-    st4_agent(part + plane + (long long)blockIdx.x * C + 4 * c4, sx);
-    if (TWO) st4_agent(part + 2 * plane + (long long)blockIdx.x * C + 4 * c4, sx2);
-  }
-  const bool ok = block_barrier(bar + 2 * blockIdx.y, bar + 2 * blockIdx.y + 1, (unsigned)Gx, &flag);
-  // merge the Gx partials of this channel block (fixed order, double)
-  {
-    double a[3][4] = {};
-    if (cok) {
-#pragma unroll 2
-      for (int gt = rg; gt < Gx; gt += 16) {
-        const long long off = (long long)gt * C + 4 * c4;
-        const f32x4 v0 = ld4_agent(part + off), v1 = ld4_agent(part + plane + off);
-        const f32x4 v2 = TWO ? ld4_agent(part + 2 * plane + off) : z4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[0][j] += (double)v0[j];
-          a[1][j] += (double)v1[j];
-          a[2][j] += (double)v2[j];
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[k][j][t] = a[k][j];
-  }
-  __syncthreads();
-  if (rg == 0 && cok) {
-    double s0[4], s1[4], s2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s0[j] = red[0][j][lane];
-      s1[j] = red[1][j][lane];
-      s2[j] = red[2][j][lane];
-    }
-#pragma unroll 1
-    for (int k = 1; k < 16; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s0[j] += red[0][j][k * 16 + lane];
-        s1[j] += red[1][j][k * 16 + lane];
-        s2[j] += red[2][j][k * 16 + lane];
-      }
-    const double n = (double)M;
-    f32x4 ca, cb, cm, ca2 = z4, cb2 = z4, cm2 = z4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 4 * c4 + j;
-      const double iv = inv[c], ga = gamma[c];
-      const double dg = s1[j] * iv;
-      const double a_ = ga * iv;
-      ca[j] = (float)a_;
-      cb[j] = (float)(a_ * iv * dg / n);
-      cm[j] = (float)(a_ * s0[j] / n);
-      if (blockIdx.x == 0) {
-        if (dgamma) dgamma[c] = (float)dg;
-        if (dbeta) dbeta[c] = (float)s0[j];
-      }
-      if (TWO) {
-        const double iv2 = inv2[c], ga2 = gamma2[c];
-        const double dg2 = s2[j] * iv2;
-        const double a2 = ga2 * iv2;
-        ca2[j] = (float)a2;
-        cb2[j] = (float)(a2 * iv2 * dg2 / n);
-        cm2[j] = (float)(a2 * s0[j] / n);
-        if (blockIdx.x == 0) {
-          if (dgamma2) dgamma2[c] = (float)dg2;
-          if (dbeta2) dbeta2[c] = (float)s0[j];
-        }
-      }
-    }
-    if (!ok) {
-      const float nan = __builtin_nanf("");
-      ca = f32x4{nan, nan, nan, nan};
-      ca2 = ca;
-    }
-    scoef[0][lane] = ca; scoef[1][lane] = cb; scoef[2][lane] = cm;
-    scoef[3][lane] = ca2; scoef[4][lane] = cb2; scoef[5][lane] = cm2;
-  }
-  __syncthreads();
-  if (!cok) return;
-  const f32x4 ca = scoef[0][lane], cb = scoef[1][lane], cm = scoef[2][lane];
-  const f32x4 ca2 = scoef[3][lane], cb2 = scoef[4][lane], cm2 = scoef[5][lane];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const long long row = r_begin + rg + 16 * u;
-    if (row < M) {
-      const long long off = row * C + 4 * c4;
-      st4(dy + off, ca * gv[u] - cm - cb * (yv[u] - mu));
-      if (TWO) st4(dy2 + off, ca2 * gv[u] - cm2 - cb2 * (y2v[u] - mu2));
-      if (DRES) st4(dres + off, gv[u]);
-    }
-  }
-}
-
-// rows per workgroup (16*U) for the fused backward: the smallest U keeping the grid at <=
-// kBarrierMaxWgs workgroups (>= 3 of them fit per CU by VGPRs and LDS, so two such grids on
-// concurrent streams are resident together); 0 = too large for the fused path (two launches)
-int bwd_fused_u(long long m, int c) {
-  const long long cb = cdiv64(c, kChanPerBlock);
-  for (int u = 1; u <= 8; u *= 2)
-    if (cdiv64(m, 16LL * u) * cb <= kBarrierMaxWgs) return u;
-  return 0;
-}
-
-// Off: measured on MI355X (scripts/bn_bench.py, graph-timed) the barrier round trips cost more than the
-// launch they save — 8.0 vs 7.0 us at 128 x 512, 11.5 vs 7.3 us at 512 x 256, 22.6 vs 18.5 us at 24576 x 64.
-// Not reachable (kept as the measured alternative: DESIGN §7).
-constexpr bool bwd_fused_enabled() { return false; }
-
 // Tiled backward apply: [64 rows x 64 channels] per workgroup; also writes dy_t (and dy2_t) in
 // the transposed wgrad operand layout through LDS.
 template <bool HAS_OUT, bool TWO, bool DRES>
@@ -863,46 +631,6 @@ int ew_blocks(long long n4) {
 bool c_ok(int C) { return C >= 4 && C % 4 == 0; }
 
 }  // namespace
-
-extern "C" int32_t tspm_bn_bwd_apply_max_tiles(void) { return kMergeTiles; }
-
-extern "C" int tspm_bn_bwd_apply(int64_t m, int32_t c, int32_t tiles, const float* partial, const float* g,
-                                 const float* out, const float* y, const float* mean, const float* invstd,
-                                 const float* gamma, float* dgamma, float* dbeta, float* dy, const float* y2,
-                                 const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
-                                 float* dbeta2, float* dy2, float* dres, tspm_stream_t stream) {
-  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > kMergeTiles || !partial || !g || !y || !mean || !invstd || !gamma ||
-      !dy)
-    return TSPM_ERR_INVALID;
-  const bool two = y2 != nullptr;
-  if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const bool ho = out != nullptr, dr = dres != nullptr;
-  const int cblk = cdiv(c, kChanPerBlock);
-  long long rb = cdiv64(m, std::max(1, 512 / cblk));  // ~512 workgroups, >= 64 rows each
-  if (rb < 64) rb = 64;
-  const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
-#define BNB_A(HO, TW, DR)                                                                                       \
-  hipLaunchKernelGGL((k_bn_bwd_apply_m<HO, TW, DR>), agrid, dim3(256), 0, st, (long long)m, c, tiles, partial, invstd, \
-                     gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, g, out, y, mean, y2, mean2, rb, dy, dy2, dres)
-  if (ho) {
-    if (two) { if (dr) BNB_A(true, true, true); else BNB_A(true, true, false); }
-    else { if (dr) BNB_A(true, false, true); else BNB_A(true, false, false); }
-  } else {
-    if (two) { if (dr) BNB_A(false, true, true); else BNB_A(false, true, false); }
-    else { if (dr) BNB_A(false, false, true); else BNB_A(false, false, false); }
-  }
-#undef BNB_A
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
-}
-
-extern "C" uint32_t tspm_debug_barrier_timeouts(void) {
-  unsigned v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(tspm_g_barrier_timeouts), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
-    return 0xffffffffu;
-  return v;
-}
 
 extern "C" int tspm_bn_finalize(int64_t m, int32_t c, int32_t ntiles, int64_t rows_per_tile, const float* partial,
                                 float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
@@ -1041,14 +769,9 @@ extern "C" int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const floa
   return TSPM_OK;
 }
 
-constexpr size_t kBwdBarrierBytes = 256;  // counters of the fused path (2 per channel block; zero before first use)
-
 extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
   if (m <= 0 || !c_ok(c)) return 0;
-  const size_t two_launch = ((size_t)3 * row_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
-  const int u = bwd_fused_u(m, c);
-  const size_t fused = u ? (size_t)3 * cdiv64(m, 16LL * u) * c * sizeof(float) : 0;
-  return kBwdBarrierBytes + std::max(two_launch, fused);
+  return ((size_t)3 * row_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
 }
 
 extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y, const float* mean,
@@ -1063,31 +786,7 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool ho = out != nullptr;
   const bool dr = dres != nullptr;
-  unsigned* bar = static_cast<unsigned*>(ws);
-  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + kBwdBarrierBytes);
-  const int fu = bwd_fused_u(m, c);
-  if (!dy_t && !dy2_t && fu && bwd_fused_enabled() && cdiv(c, kChanPerBlock) * 2 * sizeof(unsigned) <= kBwdBarrierBytes) {
-    const int gx = (int)cdiv64(m, 16LL * fu);
-    const dim3 fgrid(gx, cdiv(c, kChanPerBlock));
-#define BNB_F(HO, TW, DR, UU)                                                                                 \
-  hipLaunchKernelGGL((k_bn_bwd_fused<HO, TW, DR, UU>), fgrid, dim3(256), 0, st, (long long)m, c, gx, g, out, y, \
-                     mean, invstd, gamma, y2, mean2, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, dy, dy2, dres, \
-                     part, bar)
-#define BNB_FU(HO, TW, DR) \
-  switch (fu) { case 1: BNB_F(HO, TW, DR, 1); break; case 2: BNB_F(HO, TW, DR, 2); break; \
-                case 4: BNB_F(HO, TW, DR, 4); break; default: BNB_F(HO, TW, DR, 8); break; }
-    if (ho) {
-      if (two) { if (dr) BNB_FU(true, true, true) else BNB_FU(true, true, false) }
-      else { if (dr) BNB_FU(true, false, true) else BNB_FU(true, false, false) }
-    } else {
-      if (two) { if (dr) BNB_FU(false, true, true) else BNB_FU(false, true, false) }
-      else { if (dr) BNB_FU(false, false, true) else BNB_FU(false, false, false) }
-    }
-#undef BNB_FU
-#undef BNB_F
-    TSPM_LAUNCH_CHECK();
-    return TSPM_OK;
-  }
+  float* part = static_cast<float*>(ws);
   // the merged path (no dy_t) keeps the partial tiles few enough for every apply workgroup to
   // merge them in its prologue; the transposed-copy path keeps the separate final pass
   const int G = dy_t ? row_blocks(m, c) : std::min(row_blocks(m, c), kMergeTiles);
@@ -1100,9 +799,6 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   // 64-rows-per-thread threshold ran at 8 (half the loads in flight: 39.7 vs 31.6 us with 64 tiles of 16;
   // 20.4 us with 128 tiles of 16, profiles/r4/r4l_serial_step.txt; step 2.597 vs 2.599 ms, r4m2_pu*)
   const int pu = !bn_wide() ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
-  // 1,024-thread workgroups for the 64-channel layers' tiles (TSPM_BN_PART_RG64=1; off by default: measured
-  // BN device time 1.020 -> 0.972 ms per step but the step 2.778 -> 2.786 ms — the wider workgroups
-  // crowd the other encoder's stream)
   // (1,024-thread workgroups for the C = 64 partial pass: BN 1.020 -> 0.972 ms of device time but the step
   // 2.778 -> 2.786 ms — the wide workgroups crowd the other encoder's stream; off)
   constexpr bool wide_rg = false;

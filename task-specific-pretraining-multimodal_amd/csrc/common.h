@@ -59,7 +59,7 @@ static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // records s_memrealtime (100 MHz, chip-global) at numbered points of a kernel into a per-TU device
 // buffer read back by tspm_debug_stamps().  The product build compiles these to nothing.
 #ifdef TSPM_STAMPS
-#define TSPM_STAMP_SLOTS 8
+#define TSPM_STAMP_SLOTS 12  // 0-7 phase stamps, 8-11 conv_lds.hip LoopClock
 #define TSPM_STAMP_WAVES (1 << 18)
 #define TSPM_STAMP(buf, slot)                                                                             \
   do {                                                                                                    \

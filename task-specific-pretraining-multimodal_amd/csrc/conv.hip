@@ -440,105 +440,6 @@ __global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad(ConvArgs g, const f
   if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
 }
 
-// =============================================================================================
-// Weight gradient from TRANSPOSED operands (the layout tspm_bn_apply / tspm_bn_bwd /
-// tspm_maxpool_fwd write as their optional *_t outputs): xT[c][ldx] holds input rows (h,w,n)
-// contiguously per channel, dyT[co][ldy] output rows (p,q,n).  Both MFMA operands are then one
-// 16-byte load of 4 consecutive rows per lane (MFMA j reduces rows {mbase+j, mbase+4+j}), like the
-// forward kernel — instead of 8 gathered dwords per 4 MFMAs.  Requires N % 8 == 0: an 8-row
-// chunk shares one output position, so a 32-column tile inside one tap skips invalid chunks whole.
-// =============================================================================================
-template <int TM, int TN, int WN, int WK, bool F_>
-__global__ __launch_bounds__(64 * WN * WK) void k_conv_wgrad_t(ConvArgs g, const float* __restrict__ xT, long long ldx,
-                                                              const float* __restrict__ dyT, long long ldy,
-                                                              float* __restrict__ dw, float* __restrict__ dw_final) {
-  extern __shared__ float lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = wave % WN, wk = wave / WN;
-  const int K = g.k, C = g.c, N = g.n;
-  const int RSC = g.r * g.s * C;
-  const int row0 = blockIdx.x * (TM * 32);              // co
-  const int col0 = (blockIdx.y * WN + wn) * (TN * 32);  // kidx
-  const bool active = col0 < RSC;
-  const int z = blockIdx.z;
-  const int li = lane & 31, hh = lane >> 5;
-  const int Mout = g.p * g.q * N;
-
-  Acc<TM, TN> acc;
-  acc.zero();
-  if (active) {
-    const float* ap[TM];
-#pragma unroll
-    for (int a = 0; a < TM; ++a) ap[a] = dyT + (long long)min(row0 + a * 32 + li, K - 1) * ldy + 4 * hh;
-    int kr[TN], ks[TN];
-    bool kok[TN];
-    const float* bp[TN];
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      int kidx = col0 + b * 32 + li;
-      kok[b] = kidx < RSC;
-      kidx = min(kidx, RSC - 1);
-      const int tap = kidx / C, kc = kidx - tap * C;
-      kr[b] = tap / g.s;
-      ks[b] = tap - kr[b] * g.s;
-      bp[b] = xT + (long long)kc * ldx + 4 * hh;
-    }
-    const int tap_first = col0 / C, tap_last = (min(col0 + TN * 32, RSC) - 1) / C;
-    const bool one_tap = tap_first == tap_last;
-    const int r1 = tap_first / g.s, s1 = tap_first - r1 * g.s;
-    const int T = Mout / 8;
-    const int S = g.splits * WK, zz = z * WK + wk;
-    const int it0 = split_lo(T, zz, S), it1 = split_lo(T, zz + 1, S);
-    // first chunk >= it whose (uniform) tap is inside the input, for one-tap tiles
-    auto advance = [&](int it) -> int {
-      if (!one_tap) return it;
-      while (it < it1) {
-        const int pos = (it * 8) / N;
-        const int pp = pos / g.q, qq = pos - pp * g.q;
-        const int hi = pp * g.st - g.pad + r1, wi = qq * g.st - g.pad + s1;
-        if (hi >= 0 && hi < g.h && wi >= 0 && wi < g.w) break;
-        it = (pos + 1) * N / 8;  // next position
-      }
-      return it;
-    };
-    auto load = [&](int it, f32x4 (&A)[TM], f32x4 (&B)[TN]) {
-      const int mbase = it * 8;
-      const int pos = mbase / N, n0 = mbase - pos * N;
-      const int pp = pos / g.q, qq = pos - pp * g.q;
-#pragma unroll
-      for (int a = 0; a < TM; ++a) A[a] = ld4(ap[a] + mbase);
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int hi = pp * g.st - g.pad + kr[b], wi = qq * g.st - g.pad + ks[b];
-        const bool ok = kok[b] && hi >= 0 && hi < g.h && wi >= 0 && wi < g.w;
-        B[b] = ok ? ld4(bp[b] + ((long long)hi * g.w + wi) * N + n0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-    int it = advance(it0);
-    f32x4 A[TM], B[TN];
-    if (it < it1) load(it, A, B);
-    while (it < it1) {
-      const int nit = advance(it + 1);
-      f32x4 An[TM], Bn[TN];
-      if (nit < it1) load(nit, An, Bn);
-      acc.mma4(A, B);
-#pragma unroll
-      for (int a = 0; a < TM; ++a) A[a] = An[a];
-#pragma unroll
-      for (int b = 0; b < TN; ++b) B[b] = Bn[b];
-      it = nit;
-    }
-  }
-  acc.template combine<WN, WK>(lds, wn, wk, lane, active);
-  if (wk == 0 && active) {
-    float* out = g.splits > 1 ? dw + (long long)z * g.slab : dw;
-    acc.store(out, row0, col0, K, RSC, RSC, lane, false, g.cnt != nullptr);
-  }
-  if (g.splits > 1 && g.cnt) slab_tail<TM, TN, WN>(g, dw, dw_final, RSC, lds);
-}
-
-
 __global__ __launch_bounds__(256) void k_reduce_slabs(long long count, int nslab, long long slab_stride,
                                                       const float* __restrict__ slabs, float* __restrict__ out,
                                                       int beta) {
@@ -698,7 +599,6 @@ ConvArgs make_args(const tspm_conv_shape* s) {
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = (long long)s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
-  g.bnb = BnbFuse{};
   g.xcd = 0;
   g.acq = 1;  // register-direct kernels: acquire-based hand-offs (conv_common.h tails)
   return g;
@@ -796,7 +696,7 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
-    return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), nullptr);
+    return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream));
   }
   if (is_stem(user)) {  // per-band partials, merged by tspm_bn_finalize when the caller asked for the merge
     if (!tspm_detail::stem_supported(s)) return TSPM_ERR_INVALID;
@@ -831,22 +731,6 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   return TSPM_OK;
 }
 
-extern "C" int tspm_conv_fwd_bnin(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
-                                  const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn,
-                                  const tspm_bn_input* bi, void* ws, size_t ws_bytes, tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !w || !y || !bi) return TSPM_ERR_INVALID;
-  if (!is_lds(user) || !lds_of(user).fwd_bnin_supported(s)) return TSPM_ERR_INVALID;
-  tspm_bn_fuse bf{};
-  if (bn) {
-    bf = *bn;
-    if (!bf.partial && bf.counters) return TSPM_ERR_INVALID;
-    if (bf.counters && (!bf.save_mean || !bf.save_invstd)) return TSPM_ERR_INVALID;
-  }
-  const tspm_detail::LdsAlgo la = lds_algo(user);
-  if (!lds_of(user).fwd_supported(s, xs, la)) return TSPM_ERR_INVALID;
-  return lds_of(user).fwd(s, la, x, w, y, bn ? &bf : nullptr, ws, ws_bytes, static_cast<hipStream_t>(stream), bi);
-}
-
 extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user)) return 0;
   return lds_of(user).dgrad_workspace(s, lds_algo(user));
@@ -859,7 +743,7 @@ extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* u
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).dgrad_supported(s, la)) return TSPM_ERR_INVALID;
-    return lds_of(user).dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), nullptr);
+    return lds_of(user).dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream));
   }
   (void)ws; (void)ws_bytes;
   if (s->k % 8 != 0) return TSPM_ERR_INVALID;
@@ -943,81 +827,7 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
   if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w, ws_w_bytes,
-                        static_cast<hipStream_t>(stream), nullptr);
-}
-
-// ---- dgrad epilogue with BatchNorm-backward partial sums (ABI 13, variant 1 only) --------------
-extern "C" int32_t tspm_conv_dgrad_bn_tiles(const tspm_conv_shape* s, const tspm_conv_algo* user) {
-  if (!shape_ok(s) || !is_lds(user) || s->c % 32 != 0) return 0;  // whole 32-channel fragments
-  const tspm_detail::LdsAlgo la = lds_algo(user);
-  if (!lds_of(user).dgrad_supported(s, la)) return 0;
-  return lds_of(user).dgrad_tiles(s, la);
-}
-
-static bool bnb_of(const tspm_conv_shape* s, const tspm_conv_algo* user, const tspm_bn_bwd_fuse* f, BnbFuse& out) {
-  if (!f || !f->partial || !f->y || !f->mean) return false;
-  if ((f->y2 == nullptr) != (f->mean2 == nullptr)) return false;
-  const int tiles = tspm_conv_dgrad_bn_tiles(s, user);
-  if (tiles <= 0) return false;
-  out = BnbFuse{f->partial, f->out, f->y, f->mean, f->y2, f->mean2, tiles};
-  return true;
-}
-
-extern "C" int tspm_conv_dgrad_bnfuse(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* dy,
-                                      const float* w, float* dx, int32_t beta, void* ws, size_t ws_bytes,
-                                      const tspm_bn_bwd_fuse* bn, tspm_stream_t stream) {
-  if (!shape_ok(s) || !dy || !w || !dx || !is_lds(user)) return TSPM_ERR_INVALID;
-  BnbFuse b;
-  if (!bnb_of(s, user, bn, b)) return TSPM_ERR_INVALID;
-  const tspm_detail::LdsAlgo la = lds_algo(user);
-  return lds_of(user).dgrad(s, la, dy, w, dx, beta, ws, ws_bytes, static_cast<hipStream_t>(stream), &b);
-}
-
-extern "C" int tspm_conv_bwd_bnfuse(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
-                                    const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
-                                    int32_t beta, float* dw, void* ws_d, size_t ws_d_bytes, void* ws_w,
-                                    size_t ws_w_bytes, const tspm_bn_bwd_fuse* bn, tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
-  if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
-  BnbFuse b;
-  if (!bnb_of(s, dg, bn, b)) return TSPM_ERR_INVALID;
-  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w, ws_w_bytes,
-                        static_cast<hipStream_t>(stream), &b);
-}
-
-extern "C" int tspm_conv_wgrad_t(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x_t, int64_t ldx,
-                                 const float* dy_t, int64_t ldy, float* dw, void* ws, size_t ws_bytes,
-                                 tspm_stream_t stream) {
-  if (!shape_ok(s) || !x_t || !dy_t || !dw) return TSPM_ERR_INVALID;
-  if (s->n % 8 != 0) return TSPM_ERR_INVALID;
-  if (ldx < (int64_t)s->h * s->w * s->n || ldy < (int64_t)s->p * s->q * s->n || (ldx & 3) || (ldy & 3))
-    return TSPM_ERR_INVALID;
-  if ((reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(dy_t)) & 15) return TSPM_ERR_INVALID;
-  Algo al = wgrad_algo(s, user);
-  if (!algo_supported(al)) return TSPM_ERR_INVALID;
-  ConvArgs g = make_args(s);
-  const int RSC = s->r * s->s * s->c;
-  g.m = s->k;
-  g.splits = al.splits;
-  g.slab = (long long)s->k * RSC;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  float* out = dw;
-  dim3 grid(cdiv(s->k, al.tm * 32), cdiv(RSC, al.wn * al.tn * 32), al.splits);
-  if (al.splits > 1) {
-    if (!ws || ws_bytes < tspm_conv_wgrad_workspace(s, user)) return TSPM_ERR_WORKSPACE;
-    out = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
-    if (al.splits <= kMaxFusedSplits && (size_t)grid.x * grid.y <= TSPM_COUNTER_BYTES / sizeof(unsigned) &&
-        inlaunch_enabled())
-      g.cnt = static_cast<unsigned*>(ws);
-  }
-  const size_t lds = std::max(lds_bytes(al), (size_t)16);
-  TSPM_DISPATCH(k_conv_wgrad_t, false, g, x_t, (long long)ldx, dy_t, (long long)ldy, out, dw);
-  TSPM_LAUNCH_CHECK();
-  if (al.splits > 1 && !g.cnt) {
-    launch_reduce_slabs(g.slab, al.splits, g.slab, static_cast<const float*>(out), dw, 0, st);
-    TSPM_LAUNCH_CHECK();
-  }
-  return TSPM_OK;
+                        static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs,

@@ -5,19 +5,6 @@
 #pragma once
 #include "common.h"
 
-// BatchNorm-backward partial sums produced by a dgrad epilogue (tspm_bn_bwd_fuse): the dgrad output
-// is the final gradient g of a BN + ReLU output `out`; per row tile and channel the epilogue writes
-// part[0] = sum g', part[1] = sum g'(y - mean), part[2] = sum g'(y2 - mean2), g' = g * (out > 0).
-struct BnbFuse {
-  float* part;          // null: no BN partials
-  const float* out;     // ReLU output (mask), or null
-  const float* y;
-  const float* mean;
-  const float* y2;      // second BN (downsample branch), or null
-  const float* mean2;
-  int tiles;            // partial tiles (plane = tiles * C)
-};
-
 namespace {
 
 struct ConvArgs {
@@ -28,7 +15,6 @@ struct ConvArgs {
   long long slab;            // elements per split slab
   int beta;                  // dgrad accumulate
   unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
-  BnbFuse bnb;               // dgrad epilogue: BN-backward partial sums (variant 1 only)
   int xcd;                   // LDS-staged kernels: XCD-aware workgroup -> tile mapping (1) or identity (0)
   int acq;                   // LDS-staged kernels: agent acquire before reading split-K slabs / BN partials
                              // (1), or sc1 loads only (0, default; TSPM_HANDOFF_ACQUIRE=1 for A/B)
@@ -80,63 +66,6 @@ struct Acc {
           }
         }
       }
-  }
-  // v += src[row][col] (the accumulate of a beta = 1 store, done first so the epilogue sees the final
-  // values; same fp32 sum as store(..., accumulate = true)).  Every row of the tile must be valid
-  // (the LDS-staged dgrad's row blocks divide the rows exactly): the 16 loads of a fragment are
-  // issued back to back, one memory latency per fragment.
-  TSPM_DEV void add_from(const float* src, int row0, int col0, int cols, long long ld, int lane) {
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = col0 + b * 32 + (lane & 31);
-        if (col >= cols) continue;
-        float o[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[i] = src[(long long)(row0 + a * 32 + acc_row(i, lane)) * ld + col];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[a][b][i] = o[i] + v[a][b][i];
-      }
-  }
-  // BatchNorm-backward partial sums of this tile (BnbFuse), tile index mt; all rows valid (as above)
-  TSPM_DEV void bnb_partials(const BnbFuse& f, int mt, int row0, int col0, int cols, int lane) const {
-    const long long plane = (long long)f.tiles * cols;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int col = col0 + b * 32 + (lane & 31);
-      if (col >= cols) continue;  // wave-uniform (cols % 32 == 0)
-      const float mu = f.mean[col];
-      const float mu2 = f.y2 ? f.mean2[col] : 0.f;
-      float sg = 0.f, sx = 0.f, sx2 = 0.f;
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        float ov[16], yv[16], y2v[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const long long off = (long long)(row0 + a * 32 + acc_row(i, lane)) * cols + col;
-          ov[i] = f.out ? f.out[off] : 1.f;
-          yv[i] = f.y[off];
-          y2v[i] = f.y2 ? f.y2[off] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float gv = ov[i] > 0.f ? v[a][b][i] : 0.f;
-          sg += gv;
-          sx += gv * (yv[i] - mu);
-          sx2 += gv * (y2v[i] - mu2);
-        }
-      }
-      sg += __shfl_xor(sg, 32, 64);
-      sx += __shfl_xor(sx, 32, 64);
-      sx2 += __shfl_xor(sx2, 32, 64);
-      if (lane < 32) {
-        float* p0 = f.part + (long long)mt * cols + col;
-        p0[0] = sg;
-        p0[plane] = sx;
-        if (f.y2) p0[2 * plane] = sx2;
-      }
-    }
   }
   // split-K combine of the WK waves of one tile through LDS (wave wk > 0 writes, wave 0 sums in
   // order).  Every wave of the workgroup must call this (it contains barriers).
@@ -307,17 +236,15 @@ struct LdsImpl {
   size_t (*dgrad_workspace)(const tspm_conv_shape* s, const LdsAlgo& a);
   size_t (*wgrad_workspace)(const tspm_conv_shape* s, const LdsAlgo& a);
   int (*fwd)(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-             const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi);
-  bool (*fwd_bnin_supported)(const tspm_conv_shape* s);
+             const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st);
   int (*dgrad)(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
-               void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb);
+               void* ws, size_t ws_bytes, hipStream_t st);
   int (*wgrad)(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
                size_t ws_bytes, hipStream_t st);
   bool (*bwd_built)(const LdsAlgo& ad, const LdsAlgo& aw);
   int (*bwd)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
              const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-             hipStream_t st, const BnbFuse* bnb);
-  int (*dgrad_tiles)(const tspm_conv_shape* s, const LdsAlgo& a);
+             hipStream_t st);
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();

@@ -63,29 +63,27 @@ namespace {
 
 constexpr int kThreads = 256;  // compute (MFMA) threads: 4 waves, one per SIMD
 
-// Loader waves (TSPM_LOADER_WAVES, default on): 4 more waves per workgroup that only issue the LDS-DMA
-// of the operand ring.  Measured on MI355X (stamped builds, round 2): a global_load_lds blocks its wave
-// ~170 cycles at issue, and with one wave per SIMD doing both, the DMA issue path and the MFMA path of a
-// stage added up (one stage of a 32x64 tile: 0.36 + 0.45 us).  With a loader wave beside each compute
-// wave on the same SIMD, the compute wave's MFMA stream no longer stops at the DMA issues.  The loader
-// waves leave after the ring loop (s_barrier then counts only the surviving waves, as the ISA defines),
-// so the epilogues, split-K hand-offs and BN merges run on the 256 compute threads as before: results
-// are bitwise those of the single-role kernel (same MFMA order).
-// TSPM_LOADER_WAVES=2 (default): the loader waves stage through registers — full-line 16-B global loads two
-// stages ahead, then ds_write_b128 to the same LDS image the LDS-DMA would write (lane-linear per
-// 1-KiB piece) — instead of global_load_lds; =1: loader waves issuing global_load_lds; =0: one role.
+// Loader waves (variant 1, TSPM_LOADER_WAVES=2, the default build): 4 more waves per workgroup that only move
+// operands — full-line 16-B global loads RS stages ahead into registers, then ds_write_b128 to the stage's LDS
+// slot (lane-linear per 1-KiB piece).  Measured on MI355X (stamped builds, round 2): a global_load_lds blocks
+// its wave ~170 cycles at issue, and with one wave per SIMD doing both, the load issue path and the MFMA path
+// of a stage added up (one stage of a 32x64 tile: 0.36 + 0.45 us).  With a loader wave beside each compute
+// wave on the same SIMD, the compute wave's MFMA stream no longer stops at the load issues.  The loader waves
+// leave after the ring loop (s_barrier then counts only the surviving waves, as the ISA defines), so the
+// epilogues, split-K hand-offs and BN merges run on the 256 compute threads: results are bitwise those of the
+// single-role kernel (same MFMA order).  TSPM_LOADER_WAVES=0 (variant 2, the second build of this file):
+// single-role waves issuing their own LDS-DMA (global_load_lds) into a 2-4-slot ring.
 #ifndef TSPM_LOADER_WAVES
 #define TSPM_LOADER_WAVES 2
 #endif
-constexpr int kLoaderThreads = (TSPM_LOADER_WAVES == 1 || TSPM_LOADER_WAVES == 2) ? 256 : 0;
-// TSPM_LOADER_WAVES=3: no loader waves; the four compute waves stage through registers themselves (global
-// loads two stages ahead, ds_write, barrier, MFMAs): 256-thread workgroups, two LDS slots
-constexpr bool kRegStage = TSPM_LOADER_WAVES == 2 || TSPM_LOADER_WAVES == 3;
+static_assert(TSPM_LOADER_WAVES == 0 || TSPM_LOADER_WAVES == 2, "variant 1 (2) or variant 2 (0)");
+constexpr int kLoaderThreads = TSPM_LOADER_WAVES == 2 ? 256 : 0;
+constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
 // minimum waves per SIMD the register allocation must allow (__launch_bounds__ second argument): with
 // loader waves, 4 (two 512-thread workgroups per CU, so the two encoder streams' conv launches can share
 // CUs) for the one-block-per-wave tiles, 2 for the larger wave tiles (128 VGPRs would spill them)
 #ifndef TSPM_LDS_WAVES_SMALL
-#define TSPM_LDS_WAVES_SMALL (TSPM_LOADER_WAVES == 3 ? 2 : TSPM_LOADER_WAVES ? 4 : 1)
+#define TSPM_LDS_WAVES_SMALL (TSPM_LOADER_WAVES ? 4 : 1)
 #endif
 template <class C>
 constexpr int min_waves() { return C::TM * C::TN == 1 ? TSPM_LDS_WAVES_SMALL : (kLoaderThreads ? 2 : 1); }
@@ -140,7 +138,7 @@ TSPM_DEV void glds16(const float* src, float* dst) {
 #ifndef TSPM_RING_BYTES
 #define TSPM_RING_BYTES (64 * 1024)
 #endif
-// register-staged operand stages in flight per loader thread (TSPM_LOADER_WAVES == 2).  Measured in the
+// register-staged operand stages in flight per loader thread (variant 1).  Measured in the
 // batch-128 step (A/B, 2 runs each, same box): 2 stages 2.684-2.691 ms (2.697-2.706 with the previous loop,
 // which drained every load at each trip), 3 stages 2.677-2.681, 4 stages (3 for the large tiles)
 // 2.705-2.707; TSPM_REG_STAGES overrides (A/B builds)
@@ -255,103 +253,64 @@ TSPM_DEV void mma_plain(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM],
 // Returns true in loader waves, which must then leave the kernel (they take no part in what follows).
 // With loader waves the roles split: the loaders issue every DMA and wait for it (counted vmcnt) before
 // each stage barrier; the compute waves only pass the barriers, read fragments and multiply.
-// Optional operand hooks (register-staging loader waves only, TSPM_LOADER_WAVES == 2; the forward's
-// BatchNorm-input prologue, tspm_conv_fwd_bnin).  With HOOKS the loader waves call pro_issue() before
-// the first two stages' loads (its global loads are then ahead of them in the vmcnt order), pro_finish()
-// after them (it waits only for its own loads) and every wave passes one extra barrier before the first
-// stage (pro_finish's LDS writes are then visible to every loader wave); xfp(st, i, S, H) reads piece i's
-// per-stage constants from LDS when the stage's loads are issued, and xfa(st, i, v, S, H) transforms the
-// first NXF loaded 16-B pieces of stage st in registers before they are written to LDS — so neither adds
-// a memory or LDS round trip to the loader's store of a stage.
-struct NoHook {
-  TSPM_DEV void operator()() const {}
-  TSPM_DEV void operator()(int, int, f32x4&, f32x4&) const {}
-  TSPM_DEV void operator()(int, int, f32x4&, const f32x4&, const f32x4&) const {}
+// With loader waves the loader's per-stage path is: LDS write of the stage, lgkmcnt(0), barrier, next loads.
+// Per-stage loop diagnostics (stamped build only, TSPM_STAMPS): the compute waves accumulate shader cycles
+// (s_memtime) spent waiting at the stage barrier, reading + waiting for the stage's fragments and issuing
+// its MFMAs, into stamp slots 8-10 (slot 11: stages).  The reads of the clock add waits of their own (an
+// s_memtime result is counted in lgkmcnt), so these profile a perturbed loop, not the product.
+#if defined(TSPM_STAMPS) && !defined(TSPM_LDS_SECONDARY)
+struct LoopClock {
+  unsigned long long bar = 0, lds = 0, mma = 0, t = 0;
+  int n = 0;
+  TSPM_DEV void start() { t = __builtin_amdgcn_s_memtime(); }
+  TSPM_DEV void lap(unsigned long long& acc) {
+    const unsigned long long u = __builtin_amdgcn_s_memtime();
+    acc += u - t;
+    t = u;
+  }
+  TSPM_DEV void flush() {
+    const unsigned long long w = ((unsigned long long)blockIdx.x +
+                                  (unsigned long long)gridDim.x * (blockIdx.y + (unsigned long long)gridDim.y * blockIdx.z)) *
+                                     (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < TSPM_STAMP_WAVES) {
+      tspm_g_stamps_lds[w * TSPM_STAMP_SLOTS + 8] = bar;
+      tspm_g_stamps_lds[w * TSPM_STAMP_SLOTS + 9] = lds;
+      tspm_g_stamps_lds[w * TSPM_STAMP_SLOTS + 10] = mma;
+      tspm_g_stamps_lds[w * TSPM_STAMP_SLOTS + 11] = n;
+    }
+  }
 };
-template <class C, class Prep, class Src, class Dst, class Frags>
-TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
-                        Frags&& frags);
-template <class C, bool HOOKS, int NXF, class Prep, class Src, class Dst, class Frags, class PI, class PF, class XP,
-          class XA>
-TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
-                          Frags&& frags, PI&& pro_issue, PF&& pro_finish, XP&& xfp, XA&& xfa);
+#define TSPM_LOOP_CLOCK_DECL LoopClock lc__; lc__.start()
+#define TSPM_LOOP_LAP(field) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); lc__.lap(lc__.field); } while (0)
+#define TSPM_LOOP_STAGE() (++lc__.n)
+#define TSPM_LOOP_FLUSH() lc__.flush()
+#else
+#define TSPM_LOOP_CLOCK_DECL do {} while (0)
+#define TSPM_LOOP_LAP(field) do {} while (0)
+#define TSPM_LOOP_STAGE() do {} while (0)
+#define TSPM_LOOP_FLUSH() do {} while (0)
+#endif
+
 template <class C, class Prep, class Src, class Dst, class Frags>
 TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags) {
-  return ring_loop_x<C, false, 0>(acc, lds, st0, st1, prep, src_i, dst_i, frags, NoHook{}, NoHook{}, NoHook{},
-                                  NoHook{});
-}
-template <class C, bool HOOKS, int NXF, class Prep, class Src, class Dst, class Frags, class PI, class PF, class XP,
-          class XA>
-TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
-                          Frags&& frags, PI&& pro_issue, PF&& pro_finish, XP&& xfp, XA&& xfa) {
   constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
   const int n = st1 - st0;
   const bool loader = is_loader_wave();
   if (n <= 0) return loader;
-  // this thread's i-th 16-B piece of a stage: global source src_i(off, i), LDS destination dst_i(slot, i) + 4*lane
-  // (the lane-linear image one global_load_lds of the wave writes)
-  auto issue_i = [&](const Off& off, float* slot, int i) { glds16(src_i(off, i), dst_i(slot, i)); };
-  if constexpr (TSPM_LOADER_WAVES == 3) {
-    const int lane4 = (threadIdx.x & 63) * 4;
-    f32x4 R0[NI], R1[NI];
-    f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
-    auto load = [&](int st, f32x4 (&R)[NI]) {
-      const Off off = prep(st);
-#pragma unroll
-      for (int i = 0; i < NI; ++i) R[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
-    };
-    // stage it: registers -> LDS slot it % 2, barrier, fragments, MFMAs.  Slot it % 2 last held stage it-2,
-    // whose fragments every wave read before barrier it-1 (the MFMAs of it-2 consumed them).
-    auto stage = [&](int it, const f32x4 (&R)[NI]) {
-      float* slot = lds + (it & 1) * SF;
-#pragma unroll
-      for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(slot, i) + lane4) = R[i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
-      frags(slot, A, B);
-    };
-    load(st0, R0);
-    if (n > 1) load(st0 + 1, R1);
-    for (int it = 0; it < n; it += 2) {
-      stage(it, R0);
-      if (it + 2 < n) load(st0 + it + 2, R0);
-      mma_plain<C>(acc, A, B);
-      if (it + 1 >= n) break;
-      stage(it + 1, R1);
-      if (it + 3 < n) load(st0 + it + 3, R1);
-      mma_plain<C>(acc, A, B);
-    }
-    __syncthreads();
-    return false;
-  }
-  if constexpr (kLoaderThreads > 0 && TSPM_LOADER_WAVES == 2) {
+  if constexpr (kLoaderThreads > 0) {
     if (loader) {
       const int lane4 = (threadIdx.x & 63) * 4;
       // RS stages of operand loads in flight in registers (two LDS slots): a stage's loads are issued RS
       // stages before its LDS write, which covers more of the memory latency than two stages of MFMA work
       constexpr int RS = reg_stages<NI>();
       f32x4 R[RS][NI];
-      constexpr int NX = NXF > 0 ? NXF : 1;
-      f32x4 S[RS][NX], H[RS][NX];  // per-piece transform constants (HOOKS only)
       auto load = [&](int st, f32x4 (&Rb)[NI]) {
         const Off off = prep(st);
 #pragma unroll
         for (int i = 0; i < NI; ++i) Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
       };
-      auto consts = [&](int st, f32x4 (&Sb)[NX], f32x4 (&Hb)[NX]) {
-        if constexpr (HOOKS) {
-#pragma unroll
-          for (int i = 0; i < NXF; ++i) xfp(st, i, Sb[i], Hb[i]);
-        }
-      };
-      auto store = [&](int it, f32x4 (&Rb)[NI], const f32x4 (&Sb)[NX], const f32x4 (&Hb)[NX]) {
-        if constexpr (HOOKS) {
-#pragma unroll
-          for (int i = 0; i < NXF; ++i) xfa(st0 + it, i, Rb[i], Sb[i], Hb[i]);
-        }
+      auto store = [&](int it, f32x4 (&Rb)[NI]) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(dst_i(lds + (it & 1) * SF, i) + lane4) = Rb[i];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage is in LDS before the barrier
@@ -363,16 +322,8 @@ TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, 
       // stages stay in flight.  (With the loads conditional it merged the paths conservatively and
       // drained ALL loads at every trip: one exposed memory latency per trip.)
       const int last = st1 - 1;
-      if constexpr (HOOKS) pro_issue();
 #pragma unroll
       for (int j = 0; j < RS; ++j) load(min(st0 + j, last), R[j]);
-      if constexpr (HOOKS) {
-        pro_finish();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#pragma unroll
-        for (int j = 0; j < RS; ++j) consts(min(st0 + j, last), S[j], H[j]);
-      }
       // RS stages per trip, buffers indexed statically; (D = 2: slot it % 2 was last read before barrier it-1).
       // Full trips are one basic block (each buffer keeps its registers across the back-edge — a copy of a
       // buffer whose loads are in flight would force a wait for them), the last partial trip stores only.
@@ -380,58 +331,31 @@ TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, 
       for (; it + RS <= n; it += RS) {
 #pragma unroll
         for (int j = 0; j < RS; ++j) {
-          store(it + j, R[j], S[j], H[j]);
-          const int nx = min(st0 + it + j + RS, last);
-          load(nx, R[j]);
-          consts(nx, S[j], H[j]);
+          store(it + j, R[j]);
+          load(min(st0 + it + j + RS, last), R[j]);
         }
       }
 #pragma unroll
       for (int j = 0; j < RS - 1; ++j)
-        if (it + j < n) store(it + j, R[j], S[j], H[j]);
+        if (it + j < n) store(it + j, R[j]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       return true;
     }
     f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
-    if constexpr (HOOKS) __builtin_amdgcn_s_barrier();  // the loaders' prologue barrier
+    TSPM_LOOP_CLOCK_DECL;
     for (int it = 0; it < n; ++it) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      TSPM_LOOP_LAP(bar);
       if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
       frags(lds + (it % D) * SF, A, B);
+      TSPM_LOOP_LAP(lds);
       mma_plain<C>(acc, A, B);
+      TSPM_LOOP_LAP(mma);
+      TSPM_LOOP_STAGE();
     }
-    __builtin_amdgcn_s_barrier();
-    return false;
-  }
-  if constexpr (kLoaderThreads > 0 && TSPM_LOADER_WAVES == 1) {
-    if (loader) {
-#pragma unroll
-      for (int d = 0; d < D - 1; ++d) {
-        const Off off = prep(min(st0 + d, st1 - 1));
-#pragma unroll
-        for (int i = 0; i < NI; ++i) issue_i(off, lds + d * SF, i);
-      }
-      for (int it = 0; it < n; ++it) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * NI) : "memory");
-        __builtin_amdgcn_s_barrier();
-        const Off off = prep(min(st0 + it + D - 1, st1 - 1));
-        float* nslot = lds + ((it + D - 1) % D) * SF;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) issue_i(off, nslot, i);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // the ring's last (re-)loads have landed: LDS is free for the epilogue
-      return true;
-    }
-    f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
-    for (int it = 0; it < n; ++it) {
-      __builtin_amdgcn_s_barrier();
-      if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
-      frags(lds + (it % D) * SF, A, B);
-      mma_plain<C>(acc, A, B);
-    }
+    TSPM_LOOP_FLUSH();
     __builtin_amdgcn_s_barrier();
     return false;
   }
@@ -439,7 +363,7 @@ TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, 
   for (int d = 0; d < D - 1; ++d) {
     const Off off = prep(min(st0 + d, st1 - 1));
 #pragma unroll
-    for (int i = 0; i < NI; ++i) issue_i(off, lds + d * SF, i);
+    for (int i = 0; i < NI; ++i) glds16(src_i(off, i), dst_i(lds + d * SF, i));
   }
   f32x4 A[C::KGW][C::TM], B[C::KGW][C::TN];
   for (int it = 0; it < n; ++it) {
@@ -449,7 +373,7 @@ TSPM_DEV bool ring_loop_x(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, 
     const Off off = prep(min(st0 + it + D - 1, st1 - 1));
     float* nslot = lds + ((it + D - 1) % D) * SF;
     frags(lds + (it % D) * SF, A, B);
-    mma_interleaved<C, NI>(acc, A, B, [&](int i) { issue_i(off, nslot, i); });
+    mma_interleaved<C, NI>(acc, A, B, [&](int i) { glds16(src_i(off, i), dst_i(nslot, i)); });
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -539,11 +463,10 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 // Forward: y[(p,q,n), k] = sum_{valid (r,s), c} x[(p*st-pad+r, q*st-pad+s, n), c] w[k, r, s, c]
 // A image: BM rows (n) x 32 channels (swizzled); B image: BN rows (output channel) x 32 channels.
 // =============================================================================================
-template <class C, bool BNIN = false>
+template <class C>
 __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
                                                      const float* __restrict__ w, float* __restrict__ y,
-                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng,
-                                                     tspm_bn_input bi) {
+                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
   extern __shared__ float lds[];
   TSPM_STAMP(tspm_g_stamps_lds, 0);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -583,15 +506,7 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
     const int r = r_lo + tr, s = s_lo + (tap - tr * ns);
     return Off{((long long)(h0 + r) * g.w + (w0 + s)) * N * Cc + cc, (long long)(r * g.s + s) * Cc + cc};
   };
-  // BatchNorm-input prologue (tspm_conv_fwd_bnin, BNIN): the loader waves form scale / shift for all Cc
-  // input channels in LDS behind the ring (tspm_bn_apply's arithmetic: one loader thread per 4 channels),
-  // then transform every activation piece in registers; the workgroups of the first output-channel block
-  // also store the centre tap's pieces (input position == output position at stride 1: every activation
-  // element exactly once) to x_out.
-  float* tab = lds + C::D * C::STAGE;
-  const int c4 = tid - kThreads;
-  f32x4 t_mu, t_iv, t_g, t_b;
-  if (ring_loop_x<C, BNIN, NA>(
+  if (ring_loop<C>(
       acc, lds, st0, st1, prep,
       [&](const Off& off, int i) -> const float* { return i < NA ? xa[i] + off.a : wb[i - NA] + off.b; },
       [&](float* slot, int i) -> float* {
@@ -607,45 +522,6 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
           for (int b = 0; b < C::TN; ++b)
             B[kk][b] = frag_row(img + C::BM * 32, (id.wn * C::TN + b) * 32 + (lane & 31), q);
         }
-      },
-      [&]() {
-        if (c4 < (Cc >> 2)) {
-          t_mu = ld4(bi.mean + 4 * c4);
-          t_iv = ld4(bi.invstd + 4 * c4);
-          t_g = ld4(bi.gamma + 4 * c4);
-          t_b = ld4(bi.beta + 4 * c4);
-        }
-      },
-      [&]() {
-        if (c4 < (Cc >> 2)) {
-          const f32x4 sc = t_g * t_iv;
-          const f32x4 sf = t_b - t_mu * sc;
-          *reinterpret_cast<f32x4*>(tab + 4 * c4) = sc;
-          *reinterpret_cast<f32x4*>(tab + Cc + 4 * c4) = sf;
-        }
-      },
-      [&](int st, int i, f32x4& S, f32x4& H) {
-#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 3  // diagnostic builds only: which part of the hook costs
-        return;
-#endif
-        const int cc = (st % cb) << 5;
-        const int row = (i * 4 + wv) * 8 + (lane >> 3);
-        const int ch = cc + (((lane & 7) ^ swz(row)) << 2);
-        S = *reinterpret_cast<const f32x4*>(tab + ch);
-        H = *reinterpret_cast<const f32x4*>(tab + Cc + ch);
-      },
-      [&](int st, int i, f32x4& v, const f32x4& S, const f32x4& H) {
-#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 2
-        return;
-#endif
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = relu_f(fmaf(v[j], S[j], H[j]));
-#if defined(TSPM_FOLD_EXP) && TSPM_FOLD_EXP >= 1
-        return;
-#endif
-        const int tap = st / cb, tr = tap / ns;
-        if (bk.y == 0 && r_lo + tr == g.pad && s_lo + (tap - tr * ns) == g.pad)
-          *reinterpret_cast<f32x4*>(bi.x_out + (xa[i] - x) + prep(st).a) = v;
       }))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 2);
@@ -774,15 +650,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk, g.acq != 0))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
-  if (id.wk == 0 && col0 < Cc) {
-    if (g.bnb.part) {  // the final gradient, then the BN-backward partial sums of its row tile
-      if (g.beta) acc.add_from(dx, row0, col0, Cc, Cc, lane);
-      acc.store(dx, row0, col0, g.m, Cc, Cc, lane, false);
-      acc.bnb_partials(g.bnb, bk.x * C::WM + id.wm, row0, col0, Cc, lane);
-    } else {
-      acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
-    }
-  }
+  if (id.wk == 0 && col0 < Cc) acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
   TSPM_STAMP(tspm_g_stamps_lds, 5);
 }
 template <class C>
@@ -908,7 +776,9 @@ __global__ __launch_bounds__(kBlock, (min_waves2<CD, CW>())) void k_bwd_lds(Conv
 using tspm_detail::LdsAlgo;
 
 bool algo_ok(const LdsAlgo& a) {
-  if (!((a.tm == 1 || a.tm == 2) && (a.tn == 1 || a.tn == 2))) return false;
+  // (tm, tn) in {(1,1), (1,2), (2,1)}: the 2x2 wave tiles spilled and no tuned table selected them (removed
+  // in round 5 with the round-3 fragment-prefetch experiment that raced on them)
+  if (!((a.tm == 1 && (a.tn == 1 || a.tn == 2)) || (a.tm == 2 && a.tn == 1))) return false;
   if (!(a.wm >= 1 && a.wn >= 1 && a.wk >= 1 && a.wm * a.wn * a.wk == 4)) return false;
   return a.splits >= 1 && a.splits <= 256;
 }
@@ -950,7 +820,6 @@ ConvArgs args_of(const tspm_conv_shape* s) {
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
-  g.bnb = BnbFuse{};
   g.xcd = xcd_enabled();
   g.acq = acquire_enabled();
   return g;
@@ -978,7 +847,6 @@ size_t splitk_ws(int splits, long long rows, long long cols) {
   TSPM_LDS_WAVES(1, 1, FN)      \
   TSPM_LDS_WAVES(1, 2, FN)      \
   TSPM_LDS_WAVES(2, 1, FN)      \
-  TSPM_LDS_WAVES(2, 2, FN)      \
   return TSPM_ERR_INVALID;
 
 // BN merge plan of a forward launch: ng == 0 one level (<= 16 tiles per merging thread); ng > 0
@@ -1037,19 +905,8 @@ size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, s->k, (long long)s->r * s->s * s->c);
 }
 
-bool lds_fwd_bnin_supported(const tspm_conv_shape* s) {
-  return TSPM_LOADER_WAVES == 2 && s->stride == 1 && s->r == s->s && (s->r & 1) && s->pad == s->r / 2 &&
-         s->p == s->h && s->q == s->w && s->c % 4 == 0 && s->c <= 4 * kLoaderThreads;
-}
-
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st, const tspm_bn_input* bi) {
-  tspm_bn_input bin{};
-  if (bi) {
-    if (!lds_fwd_bnin_supported(s) || !bi->mean || !bi->invstd || !bi->gamma || !bi->beta || !bi->x_out)
-      return TSPM_ERR_INVALID;
-    bin = *bi;
-  }
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
   ConvArgs g = args_of(s);
   g.m = s->p * s->q * s->n;
   g.splits = a.splits;
@@ -1075,15 +932,8 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
     if (!room) bf.counters = nullptr;
   }
   const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
-  size_t lds = lds_bytes(a, bf.counters != nullptr);
-  if (bi) {  // scale / shift table behind the two register-staging ring slots
-    const size_t ring = (size_t)2 * (bm_of(a) + bn_of(a)) * 32 * sizeof(float);
-    lds = std::max(lds, ring + (size_t)2 * s->c * sizeof(float));
-    if (lds > 160 * 1024) return TSPM_ERR_INVALID;
-  }
-#define TSPM_FWD(CFG)                                                                                         \
-  if (bi) hipLaunchKernelGGL((k_fwd_lds<CFG, true>), grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin); \
-  else hipLaunchKernelGGL((k_fwd_lds<CFG, false>), grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng, bin)
+  const size_t lds = lds_bytes(a, bf.counters != nullptr);
+#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;
@@ -1094,15 +944,12 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
   return TSPM_OK;
 }
 
-int lds_dgrad_tiles(const tspm_conv_shape* s, const LdsAlgo& a) { return s->h * s->w * s->n / (a.tm * 32); }
-
 int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
-              void* ws, size_t ws_bytes, hipStream_t st, const BnbFuse* bnb) {
+              void* ws, size_t ws_bytes, hipStream_t st) {
   ConvArgs g = args_of(s);
   g.m = s->h * s->w * s->n;
   g.splits = a.splits;
   g.beta = beta ? 1 : 0;
-  if (bnb) g.bnb = *bnb;
   float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_dgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
@@ -1193,14 +1040,13 @@ bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(a
 
 int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
             const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-            hipStream_t st, const BnbFuse* bnb) {
+            hipStream_t st) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
   BwdLaunch L{};
   L.gd = args_of(s);
   L.gd.m = s->h * s->w * s->n;
   L.gd.splits = ad.splits;
   L.gd.beta = beta ? 1 : 0;
-  if (bnb) L.gd.bnb = *bnb;
   if (ad.splits > 1) {
     if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
     L.gd.cnt = static_cast<unsigned*>(wsd);
@@ -1237,8 +1083,8 @@ const LdsImpl& TSPM_LDS_IMPL() {
   namespace v = TSPM_LDS_NS;
   static const LdsImpl t{&v::lds_fwd_supported, &v::lds_dgrad_supported, &v::lds_wgrad_supported,
                          &v::lds_fwd_workspace, &v::lds_fwd_bn_counters, &v::lds_fwd_bn_partial_floats,
-                         &v::lds_dgrad_workspace, &v::lds_wgrad_workspace, &v::lds_fwd, &v::lds_fwd_bnin_supported,
-                         &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd, &v::lds_dgrad_tiles};
+                         &v::lds_dgrad_workspace, &v::lds_wgrad_workspace, &v::lds_fwd,
+                         &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd};
   return t;
 }
 }  // namespace tspm_detail

@@ -717,10 +717,12 @@ extern "C" int tspm_flag_create(tspm_flag** flag) {
 }
 extern "C" int tspm_flag_destroy(tspm_flag* f) {
   if (!f) return TSPM_ERR_INVALID;
-  (void)hipFree(f->dev);
-  (void)hipHostFree(f->host);
+  // every bump kernel that may still be queued has finished before the words go away
+  const bool synced = hipDeviceSynchronize() == hipSuccess;
+  const bool freed = hipFree(f->dev) == hipSuccess;
+  const bool hfreed = hipHostFree(f->host) == hipSuccess;
   delete f;
-  return TSPM_OK;
+  return synced && freed && hfreed ? TSPM_OK : TSPM_ERR_LAUNCH;
 }
 extern "C" int tspm_flag_bump(tspm_flag* f, tspm_stream_t stream) {
   if (!f) return TSPM_ERR_INVALID;

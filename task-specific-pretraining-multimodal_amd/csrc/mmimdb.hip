@@ -312,10 +312,6 @@ struct Bn1dBwd {
   float* dgamma;
   float* dbeta;
   float* dx;
-  const float* mo_a;       // optional fused MaxOut/Dropout backward (tspm_bn1d_bwd_maxout)
-  const uint8_t* mo_keep;
-  float mo_scale;
-  float* mo_da;
   const uint8_t* g_keep;  // tspm_bn1d_bwd_drop_relu: g is the gradient of Dropout(BN(x)) -> g*keep*g_scale,
   float g_scale;          // and x is a ReLU output: dx = 0 where x <= 0
   int relu_x;
@@ -350,10 +346,6 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
   float* __restrict__ dgamma = p.dgamma;
   float* __restrict__ dbeta = p.dbeta;
   float* __restrict__ dx = p.dx;
-  const float* __restrict__ mo_a = p.mo_a;
-  const uint8_t* __restrict__ mo_keep = p.mo_keep;
-  const float mo_scale = p.mo_scale;
-  float* __restrict__ mo_da = p.mo_da;
   const int ch = bid * kBnCh + threadIdx.x % kBnCh, grp = threadIdx.x / kBnCh;
   const bool ok = ch < c;
   const float mean = ok ? mean_[ch] : 0.f, invstd = ok ? invstd_[ch] : 0.f;
@@ -376,20 +368,13 @@ TSPM_DEV void bn1d_bwd_body(int m, const Bn1dBwd& p, int bid, double* red) {
     dgamma[ch] = (float)tgx;
     dbeta[ch] = (float)tg;
   }
-  if (!dx && !mo_da) return;
+  if (!dx) return;
   const double k = (double)gamma[ch] * (double)invstd, mg = tg / (double)m, mgx = tgx / (double)m;
   for (int r = grp; r < m; r += kBnGroups) {
     const long long i = (long long)r * c + ch;
     float v = (float)(k * ((double)gval(i) - mg - ((double)x[i] - (double)mean) * (double)invstd * mgx));
     if (DR && p.relu_x && !(x[i] > 0.f)) v = 0.f;
-    if (dx) dx[i] = v;
-    if (mo_da) {  // x was MaxOut(2)+Dropout of a[m, 2c]: route v as k_maxout_bwd does
-      const float gv = mo_keep ? v * (mo_keep[i] ? mo_scale : 0.f) : v;
-      const float a0 = mo_a[(long long)r * 2 * c + ch], a1 = mo_a[(long long)r * 2 * c + c + ch];
-      const float half = 0.5f * gv;
-      mo_da[(long long)r * 2 * c + ch] = a0 == a1 ? half : (a0 < a1 ? 0.f : gv);
-      mo_da[(long long)r * 2 * c + c + ch] = a0 == a1 ? half : (a1 < a0 ? 0.f : gv);
-    }
+    dx[i] = v;
   }
 }
 
@@ -605,20 +590,7 @@ extern "C" int tspm_bn1d_bwd(int32_t m, int32_t c, const float* g, const float* 
                              const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dx,
                              tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
-  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr};
-  hipLaunchKernelGGL(k_bn1d_bwd<false>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
-                     m, p);
-  TSPM_LAUNCH_CHECK();
-  return TSPM_OK;
-}
-
-extern "C" int tspm_bn1d_bwd_maxout(int32_t m, int32_t c, const float* g, const float* x, const float* mean,
-                                    const float* invstd, const float* gamma, float* dgamma, float* dbeta,
-                                    const float* a, const uint8_t* keep, float keep_scale, float* da,
-                                    tspm_stream_t stream) {
-  if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta || !a || !da)
-    return TSPM_ERR_INVALID;
-  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, nullptr, a, keep, keep_scale, da};
+  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx};
   hipLaunchKernelGGL(k_bn1d_bwd<false>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
@@ -641,7 +613,7 @@ extern "C" int tspm_bn1d_bwd_drop_relu(int32_t m, int32_t c, const float* g, con
                                        const float* x, const float* mean, const float* invstd, const float* gamma,
                                        float* dgamma, float* dbeta, float* dx, tspm_stream_t stream) {
   if (m <= 0 || c <= 0 || !g || !x || !mean || !invstd || !gamma || !dgamma || !dbeta) return TSPM_ERR_INVALID;
-  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, nullptr, nullptr, 1.f, nullptr, g_keep, g_scale, 1};
+  const Bn1dBwd p{c, g, x, mean, invstd, gamma, dgamma, dbeta, dx, g_keep, g_scale, 1};
   hipLaunchKernelGGL(k_bn1d_bwd<true>, dim3(cdiv(c, kBnCh)), dim3(kBnCh * kBnGroups), 0, static_cast<hipStream_t>(stream),
                      m, p);
   TSPM_LAUNCH_CHECK();
@@ -674,8 +646,8 @@ extern "C" int tspm_bn1d_bwd_pair(int32_t m, int32_t c0, const float* g0, const 
   if (m <= 0 || c0 <= 0 || c1 <= 0 || !g0 || !x0 || !mean0 || !invstd0 || !gamma0 || !dgamma0 || !dbeta0 || !g1 ||
       !x1 || !mean1 || !invstd1 || !gamma1 || !dgamma1 || !dbeta1)
     return TSPM_ERR_INVALID;
-  const Bn1dBwd p0{c0, g0, x0, mean0, invstd0, gamma0, dgamma0, dbeta0, dx0, nullptr, nullptr, 1.f, nullptr};
-  const Bn1dBwd p1{c1, g1, x1, mean1, invstd1, gamma1, dgamma1, dbeta1, dx1, nullptr, nullptr, 1.f, nullptr};
+  const Bn1dBwd p0{c0, g0, x0, mean0, invstd0, gamma0, dgamma0, dbeta0, dx0};
+  const Bn1dBwd p1{c1, g1, x1, mean1, invstd1, gamma1, dgamma1, dbeta1, dx1};
   const int nb0 = cdiv(c0, kBnCh);
   hipLaunchKernelGGL(k_bn1d_bwd2, dim3(nb0 + cdiv(c1, kBnCh)), dim3(kBnCh * kBnGroups), 0,
                      static_cast<hipStream_t>(stream), m, p0, p1, nb0);

@@ -18,7 +18,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 
 from . import _lib as L
-from .linear import linear_bwd
+from ._lib import linear_bwd
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1

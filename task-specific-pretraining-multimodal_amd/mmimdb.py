@@ -29,15 +29,11 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .linear import linear_bwd
+from ._lib import linear_bwd
 from .optim import FusedAdam
 from .step import shared_batches_tracked
 
 _BN_MOMENTUM_DEFAULT = 0.1
-# BatchNorm1d backward + MaxOut backward in one launch (tspm_bn1d_bwd_maxout, bitwise equal) measured slower:
-# 618k vs 653k samples/s at batch 256 — the BN kernel's 8 workgroups (64 channels each) take on the routing
-# that the wide element-wise kernel spreads over the chip.  Off.
-_FUSE_BN_MAXOUT = False
 # the independent image / text launches (input BatchNorm1d forward and backward, the GMU projections) as
 # merged pairs (bitwise the separate launches; 665-670k -> 756k samples/s)
 _PAIRS = True
@@ -308,17 +304,13 @@ class MMIMDbEngine:
                                       L.ptr(dx), sh), "bn1d_bwd")
 
     def _bn_bwd_maxout(self, key, bn, g_in, x, width, A, keep, scale, dA, sh):
-        mean, inv = self.stat[key]
-        if not _FUSE_BN_MAXOUT:
-            dx = self.dY1 if key == "b1" else self.dY2
-            self._bn_bwd(key, bn, g_in, x, width, dx, sh)
-            L.check(L.lib().tspm_maxout_bwd(self.n, width, dx.data_ptr(), width, A.data_ptr(), 2 * width, keep, scale,
-                                            dA.data_ptr(), 2 * width, sh), "maxout bwd")
-            return
-        L.check(L.lib().tspm_bn1d_bwd_maxout(self.n, width, g_in.data_ptr(), x.data_ptr(), mean.data_ptr(),
-                                             inv.data_ptr(), bn.weight.data_ptr(), bn.weight.grad.data_ptr(),
-                                             bn.bias.grad.data_ptr(), A.data_ptr(), keep, scale, dA.data_ptr(), sh),
-                "bn1d_bwd_maxout")
+        """BatchNorm1d backward, then the backward of the MaxOut(2) + Dropout that produced its input (two
+        launches: one fused launch was measured slower, 618k vs 653k samples/s at batch 256 — its 8 workgroups
+        took on routing the wide element-wise kernel spreads over the chip; removed in round 5)."""
+        dx = self.dY1 if key == "b1" else self.dY2
+        self._bn_bwd(key, bn, g_in, x, width, dx, sh)
+        L.check(L.lib().tspm_maxout_bwd(self.n, width, dx.data_ptr(), width, A.data_ptr(), 2 * width, keep, scale,
+                                        dA.data_ptr(), 2 * width, sh), "maxout bwd")
 
     # -- forward ------------------------------------------------------------------------------------
     def forward(self, sh: int, train: bool) -> None:
@@ -483,11 +475,11 @@ class MMIMDbEngine:
         # output Linear
         linear_bwd(n, h, c, self.Y2n.data_ptr(), h, self.dlogits.data_ptr(), c, net[7].weight.data_ptr(),
                    g(net[7].weight), g(net[7].bias), self.dY2n.data_ptr(), h, sh)
-        # BatchNorm1d + MaxOut 2 (+ dropout) backward in one launch
+        # BatchNorm1d + MaxOut 2 (+ dropout) backward
         self._bn_bwd_maxout("b2", net[6], self.dY2n, self.Y2, h, self.A2, k2, scale, self.dA2, sh)
         linear_bwd(n, h, 2 * h, self.Y1n.data_ptr(), h, self.dA2.data_ptr(), 2 * h, net[4].layers[0].weight.data_ptr(),
                    g(net[4].layers[0].weight), None, self.dY1n.data_ptr(), h, sh)
-        # BatchNorm1d + MaxOut 1 (+ dropout) backward in one launch
+        # BatchNorm1d + MaxOut 1 (+ dropout) backward
         self._bn_bwd_maxout("b1", net[3], self.dY1n, self.Y1, h, self.A1, k1, scale, self.dA1, sh)
         linear_bwd(n, d, 2 * h, self.Zn.data_ptr(), d, self.dA1.data_ptr(), 2 * h, net[1].layers[0].weight.data_ptr(),
                    g(net[1].layers[0].weight), None, self.dZn.data_ptr(), d, sh)

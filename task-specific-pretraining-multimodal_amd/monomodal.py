@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .linear import linear_bwd
+from ._lib import linear_bwd
 from .engine import EncoderEngine, prepare_encoder_layout
 from .metrics import ClassificationLog, DeviceMetricRecorder
 from .optim import FusedAdam

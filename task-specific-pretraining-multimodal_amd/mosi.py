@@ -39,7 +39,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .linear import linear_bwd
+from ._lib import linear_bwd
 from .optim import FusedAdam
 
 NUM_CLASSES = 3  # data/mosi.py:26 (classification_labels)

@@ -17,6 +17,7 @@ zero_grad pass); with world_size > 1 the flat buffer is all-reduced between back
 from __future__ import annotations
 
 import os
+import time
 from typing import Dict, Optional
 
 import torch
@@ -67,6 +68,31 @@ def shared_batches_tracked(model: torch.nn.Module, dev: torch.device,
     return nbt
 
 
+# tspm_head_train_step's shape limits (csrc/misc.hip: HEAD_MAXIN / HEAD_MAXH / HEAD_MAXH2 / HEAD_MAXC, sizes % 4,
+# weights + the 4-row block in at most 160 KiB of LDS — head_lds_floats)
+HEAD_MAX_IN, HEAD_MAX_HIDDEN, HEAD_MAX_HIDDEN2, HEAD_MAX_CLASSES = 256, 256, 128, 16
+
+
+def head_supported(model) -> bool:
+    """Python mirror of tspm_head_train_step's argument checks for this model's fusion head: a
+    head the kernel would refuse routes AVMNIST.train_step to the autograd path (linear kernels + CE) instead
+    of raising on the first fused step."""
+    try:
+        F = int(model.embd_size_A) + int(model.embd_size_I)
+        H = int(model.hidden_dim)
+        H2 = H // 2
+    except (AttributeError, TypeError):
+        return False
+    C = NUM_CLASSES
+    if not (0 < F <= HEAD_MAX_IN and 0 < H <= HEAD_MAX_HIDDEN and 0 < H2 <= HEAD_MAX_HIDDEN2 and 0 < C <= HEAD_MAX_CLASSES):
+        return False
+    if F % 4 or H % 4 or H2 % 4:
+        return False
+    rb = 4  # HEAD_RB
+    floats = H * (F + 4) + H2 * (H + 4) + C * (H2 + 4) + rb * ((F + 4) + (H + 4) + (H2 + 4) + (C + 4)) + (H + H2 + C + rb)
+    return floats * 4 <= 160 * 1024
+
+
 def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: torch.Tensor) -> bool:
     if os.environ.get("TSPM_DISABLE_FUSED_STEP"):
         return False
@@ -75,6 +101,8 @@ def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: t
     if _ce_weight(loss_functions) is None:
         return False
     if not (A.is_cuda and I.is_cuda):
+        return False
+    if not head_supported(model):
         return False
     return A.shape[0] == I.shape[0]
 
@@ -86,6 +114,9 @@ class FusedTrainStep:
         self.opt = optimizer
         self.loss_functions = loss_functions
         self.ce_weight = _ce_weight(loss_functions)
+        if not head_supported(model):
+            raise L.TspmError("FusedTrainStep: the fusion head's shape is outside tspm_head_train_step's limits "
+                              "(use AVMNIST.train_step, which routes such heads to the autograd path)")
         self.N = batch
         self.use_graph = use_graph and not os.environ.get("TSPM_NO_GRAPH")
         self.allreduce = allreduce
@@ -140,6 +171,9 @@ class FusedTrainStep:
         # the two chains (e.g. the audio layer3/4 update moved to the image stream) serialised the replayed
         # graph: 3.55 ms vs 2.64 (profiles/r4/r4f_ab_adam_schedules.json)
         self.adam_split = adam_split
+        # bench.py's exchange block: when a list, the phased DP step appends per step the host's waits for
+        # the two step flags and a pair of events (graph end, step end) bracketing the exposed exchange tail
+        self.exchange_probe: Optional[list] = None
         self._split_ranges = None
         self._graph_gen_keep = True
         self.calls = 0
@@ -278,6 +312,10 @@ class FusedTrainStep:
         ranges of the same parameters (phase 2's backward reads none of the phase-0/1 parameters).  Adam is
         element-wise, so the per-phase ranges give bitwise the one-launch update."""
         ar = self.allreduce
+        if getattr(self.opt, "clip_coef", None) is not None:
+            # the per-phase Adam ranges have no clip-coefficient form (ADVICE r4): refuse instead of ignoring it
+            raise L.TspmError("phased DP step: FusedAdam.clip_coef is set, but the per-phase Adam ranges cannot "
+                              "apply a clip coefficient; use the plain DP step (allreduce=GradAllReduce)")
         eager = not self.use_graph or self.calls == 0
         if getattr(self, "_marks", None) is None:
             self._marks = (L.DeviceFlag(), L.DeviceFlag())
@@ -300,18 +338,50 @@ class FusedTrainStep:
         for f in self._marks:
             f.count += 1
         main, comm, r = torch.cuda.current_stream(), self.comm, self._phase_ranges
+        probe = self.exchange_probe
+        if probe is not None:  # the graph's end on main (the side stream joined it inside the graph)
+            ev_graph = torch.cuda.Event(enable_timing=True)
+            ev_graph.record(main)
+            t0 = time.perf_counter()
         self._marks[0].host_wait(self._marks[0].count)
+        if probe is not None:
+            t1 = time.perf_counter()
         with torch.cuda.stream(comm):
             ar.wait(ar.launch(0))
             self.opt.launch_begin(comm.cuda_stream)  # one step-count increment, before every range
             self.opt.launch_ranges(comm.cuda_stream, r[0])
+        if probe is not None:
+            t2 = time.perf_counter()
         self._marks[1].host_wait(self._marks[1].count)
+        if probe is not None:
+            t3 = time.perf_counter()
         with torch.cuda.stream(comm):
             ar.wait(ar.launch(1))
             self.opt.launch_ranges(comm.cuda_stream, r[1])
         ar.wait(ar.launch(2))  # on main, behind the graph: no stream hop before the last exchange
         main.wait_stream(comm)  # the step-count increment and the phase-0/1 updates before the step ends
         self.opt.launch_ranges(main.cuda_stream, r[2])
+        if probe is not None:
+            ev_end = torch.cuda.Event(enable_timing=True)
+            ev_end.record(main)
+            probe.append({"host_wait_ms": ((t1 - t0) * 1e3, (t3 - t2) * 1e3), "events": (ev_graph, ev_end)})
+
+    def close(self) -> None:
+        """Release the step's device-side resources in a safe order, before the process group goes away
+        (bench.py, the DP tests): wait for every stream (the graph's two, the exchange stream, RCCL's via the
+        device), drop the captured graphs (they bump the step flags), then free the flags.  Idempotent; the
+        step is unusable afterwards."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        torch.cuda.synchronize(self.device)
+        self.graph, self.graph_opt = None, None
+        marks, self._marks = getattr(self, "_marks", None), None
+        if marks is not None:
+            for f in marks:
+                f.close()
+        self.allreduce = None
+        self.exchange_probe = None
 
     def _classify(self, sh: int) -> None:
         log = self.log
@@ -350,6 +420,8 @@ class FusedTrainStep:
 
     def run(self) -> None:
         """One training step on the batch currently in the static input buffers."""
+        if getattr(self, "_closed", False):
+            raise L.TspmError("FusedTrainStep.run after close()")
         self.model.train()
         self.opt.sync_hyper()
         if self._graph_log is not self.log:  # the metrics log is baked into the captured graphs

@@ -20,6 +20,8 @@ def _env(**kw):
 
 
 def _run(args, env=None, timeout=120):
+    if "--dry-run" in args and "--cpu-budget" not in args:
+        args = args + ["--no-cpu-baseline"]
     return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
                           env=env if env is not None else _env(), cwd=REPO)
 
@@ -58,7 +60,8 @@ def test_torchrun_env_is_honoured():
         port = s.getsockname()[1]
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2", "--dry-run",
-                        "--steps", "2"], capture_output=True, text=True, timeout=120, env=_env(), cwd=REPO)
+                        "--steps", "2", "--no-cpu-baseline"], capture_output=True, text=True, timeout=120, env=_env(),
+                       cwd=REPO)
     assert p.returncode == 0, p.stderr[-3000:]
     res = _one_json(p.stdout)
     assert res["n_gpus"] == 2 and "launch" not in res
@@ -74,3 +77,21 @@ def test_failing_rank_fails_the_launch():
     # unknown flag passed through to both children -> argparse exits 2 in each, the parent must fail
     p = _run(["--gpus", "2", "--dry-run", "--no-such-flag"])
     assert p.returncode != 0
+
+
+def test_gpus2_line_carries_roofline_cpu_baseline_and_exchange():
+    """the N > 1 line has the same post-timed-region keys as N = 1 — roofline (rank 0
+    profiles its local step), cpu_baseline (rank 0 while the other ranks sleep in a gloo barrier) and the
+    exchange block (per-phase host wait, exposed tail, local step time, RCCL world size)."""
+    p = _run(["--gpus", "2", "--dry-run", "--steps", "2", "--cpu-budget", "1", "--exchange-steps", "3"],
+             timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = _one_json(p.stdout)
+    assert res["n_gpus"] == 2
+    assert "roofline" in res and {"frac", "r34_3x3"} <= set(res["roofline"])
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    ex = res["exchange"]
+    assert ex["rccl_world_size"] == 2 and ex["phases"] == 3 and ex["steps_probed"] == 3
+    assert {"exposed_tail_ms_per_step", "host_wait_ms_per_step", "local_step_ms",
+            "exchange_exposed_ms_per_step"} <= set(ex)

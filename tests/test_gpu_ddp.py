@@ -108,7 +108,10 @@ def _worker(rank, world, port, q):
             other = [torch.empty_like(t) for _ in range(world)]
             dist.all_gather(other, t)
             same.append(bool(torch.equal(other[0], other[1])))
-        q.put((rank, (ok_sum, replay_sums), ok_adam, same, st.graph is not None))
+        had_graph = st.graph is not None
+        st.close()  # streams idle, graph and step flags released before the process group goes away
+        s_loc.close()
+        q.put((rank, (ok_sum, replay_sums), ok_adam, same, had_graph))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - surfaced by the parent
         import traceback

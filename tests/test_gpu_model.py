@@ -238,6 +238,12 @@ def test_phased_allreduce_step_equals_plain_step(gpu):
                 assert isinstance(st.graph, torch.cuda.CUDAGraph) and st.graph_opt is None
             bufs = [m.running_var.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)]
             results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs).cpu())
+            # explicit teardown before the process group goes: streams idle, graph and step
+            # flags released in that order; a closed step refuses to run
+            st.close()
+            st.close()  # idempotent
+            with pytest.raises(tspm_amd.TspmError):
+                st.run()
         bad = (results[0] != results[1]).nonzero().reshape(-1)
         assert bad.numel() == 0, (bad.numel(), bad[:8].tolist(), (results[0] - results[1]).abs().max().item())
     finally:

@@ -39,10 +39,11 @@ ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1,
          (1, 1, 1, 16, 1), (1, 2, 1, 16, 1)]
 # variant 1 (LDS-staged): (tm, tn, wn, wk, splits, 1) with wm = 4 / (wn*wk); every (wm, wn, wk) wave
 # arrangement, both tile sizes and split-K over workgroups
-LDS_ALGOS = [(1, 1, 1, 1, 1, 1), (1, 1, 2, 1, 1, 1), (1, 1, 4, 1, 1, 1), (2, 2, 2, 1, 1, 1), (1, 1, 1, 4, 1, 1),
-             (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 2, 1, 1, 2, 1),
+# (the 2x2 wave tiles were removed in round 5: no tuned table selected them)
+LDS_ALGOS = [(1, 1, 1, 1, 1, 1), (1, 1, 2, 1, 1, 1), (1, 1, 4, 1, 1, 1), (1, 1, 1, 4, 1, 1),
+             (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 1, 2, 1, 2, 1),
              # variant 2: the same kernels with single-role waves and an LDS-DMA ring (the batch-256 / 1024 tables)
-             (1, 1, 2, 1, 1, 2), (2, 1, 1, 4, 2, 2), (1, 1, 2, 2, 5, 2), (2, 2, 1, 1, 2, 2)]
+             (1, 1, 2, 1, 1, 2), (2, 1, 1, 4, 2, 2), (1, 1, 2, 2, 5, 2), (1, 2, 1, 1, 2, 2)]
 
 
 def _check(out, ref, bound, what):
@@ -332,14 +333,12 @@ def test_bn_block_fwd_bwd(gpu, m, c, mode):
         assert torch.allclose(dy2o.double().cpu(), leaves[3].grad, rtol=1e-3, atol=2e-5)
         assert torch.allclose(gw2.double().cpu(), leaves[4].grad, rtol=1e-4, atol=1e-3)
         assert torch.allclose(gb2.double().cpu(), leaves[5].grad, rtol=1e-4, atol=1e-3)
-    assert lib.tspm_debug_barrier_timeouts() == 0
-    assert not ws[:256].any()  # barrier counters re-armed
 
 
-def test_bn_bwd_fused_concurrent_streams(gpu):
+def test_bn_bwd_concurrent_streams(gpu):
     """Two BN backwards (partial-sum launch + apply launch each) in flight at once on two streams (as the
-    two encoders' backward passes run), many times: no barrier wait times out, workspaces do not alias,
-    and the results equal the same launches run one after the other."""
+    two encoders' backward passes run), many times: workspaces do not alias, and the results equal the same
+    launches run one after the other."""
     from tspm_amd import _lib as L
     lib = L.lib()
     g = torch.Generator().manual_seed(11)
@@ -370,10 +369,8 @@ def test_bn_bwd_fused_concurrent_streams(gpu):
         launch(bufs[0], s1)
         launch(bufs[1], s2)
     torch.cuda.synchronize()
-    assert lib.tspm_debug_barrier_timeouts() == 0
     for b, (dy, gw, gb) in zip(bufs, want):
         assert torch.equal(b["dy"], dy) and torch.equal(b["gw"], gw) and torch.equal(b["gb"], gb)
-        assert not b["ws"][:256].any()
 
 
 # ------------------------------------------------------------------------------------------------
@@ -667,7 +664,7 @@ def test_wgrad_split_counters_rearm(gpu):
 @pytest.mark.parametrize("m,c", [(6272, 64), (512, 256), (128, 512), (96, 128)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_bn_transposed_copies(gpu, m, c, mode):
-    """The tiled kernels that also write transposed copies (the tspm_conv_wgrad_t operand layout)
+    """The tiled kernels that also write transposed copies ([c][rows], per channel)
     give the same HWNC outputs as the plain kernels (forward bitwise; backward within 1e-6: the
     plain path merges its <= 64 partial tiles inside the apply kernel, the transposed path keeps the
     separate final pass over more tiles, so the per-channel sums are added in a different fixed
@@ -723,36 +720,3 @@ def test_bn_transposed_copies(gpu, m, c, mode):
         assert torch.equal(dy2t[:, :m], b[1].t())
 
 
-@pytest.mark.parametrize("case", [CONV_CASES[i] for i in range(len(CONV_CASES))])
-@pytest.mark.parametrize("algo", [(0, 0, 0, 0, 0), (1, 1, 1, 4, 1), (2, 2, 1, 2, 3), (1, 2, 2, 2, 1), (1, 1, 1, 16, 6),
-                                  (1, 1, 1, 8, 20)])
-def test_conv_wgrad_transposed(gpu, case, algo):
-    """tspm_conv_wgrad_t (operands in the transposed [C][rows] layout) vs fp64."""
-    import ctypes
-    from abi_helpers import shape, to_hwnc
-    from tspm_amd import _lib as L
-    n, c, h, w, k, r, s_, st, pad = case
-    if n % 8:
-        pytest.skip("wgrad_t needs n % 8 == 0")
-    lib = L.lib()
-    g = torch.Generator().manual_seed(23)
-    x = torch.randn(n, c, h, w, generator=g)
-    p = (h + 2 * pad - r) // st + 1
-    q = (w + 2 * pad - s_) // st + 1
-    dy = torch.randn(n, k, p, q, generator=g)
-    ref = torch.nn.grad.conv2d_weight(x.double(), (k, c, r, s_), dy.double(), st, pad)
-    bound = torch.nn.grad.conv2d_weight(x.double().abs(), (k, c, r, s_), dy.double().abs(), st, pad)
-    shp = shape(n, h, w, c, k, r, s_, st, pad)
-    ldx, ldy = h * w * n + 4, p * q * n + 12
-    xt = torch.zeros(c, ldx, device=gpu)
-    xt[:, :h * w * n] = to_hwnc(x.to(gpu)).t()
-    dyt = torch.zeros(k, ldy, device=gpu)
-    dyt[:, :p * q * n] = to_hwnc(dy.to(gpu)).t()
-    a = L.ConvAlgo(*algo)
-    wsb = lib.tspm_conv_wgrad_workspace(ctypes.byref(shp), ctypes.byref(a))
-    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
-    dw = torch.empty(k, c, r, s_, device=gpu).contiguous(memory_format=torch.channels_last)
-    L.check(lib.tspm_conv_wgrad_t(ctypes.byref(shp), ctypes.byref(a), xt.data_ptr(), ldx, dyt.data_ptr(), ldy,
-                                  dw.data_ptr(), ws.data_ptr(), wsb, sh()), "wgrad_t")
-    torch.cuda.synchronize()
-    _check(dw.contiguous(), ref, bound, f"wgrad_t {case} {algo}")
