@@ -5,6 +5,7 @@
 #   bash scripts/gpu_r5.sh suite TAG    smoke + the whole GPU suite
 #   bash scripts/gpu_r5.sh bench TAG    two default bench lines (no CPU baseline) + --phased
 #   bash scripts/gpu_r5.sh stamps TAG [--only ...]   loop-clock stamps of single conv launches
+#   bash scripts/gpu_r5.sh dp TAG       the capture / phased / DP tests (-s), --phased bench line, loop stamps
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -35,5 +36,10 @@ case $MODE in
     ;;
   stamps)
     stamps "$1"
+    ;;
+  dp)  # the DP / capture tests with their output visible (-s), the phased bench line, then loop stamps
+    timeout -k 10 400 python -u -m pytest tests/test_gpu_capture.py tests/test_gpu_phased.py tests/test_gpu_ddp.py "tests/test_gpu_model.py::test_phased_allreduce_step_equals_plain_step" -x -q -s --timeout 300 --timeout-method thread > gpurun_out/${T}_dp_tests.log 2>&1
+    bench1 --phased --no-cpu-baseline --pcie-steps 0 --profile-steps 0 --steps 100 > gpurun_out/${T}_phased.json 2> gpurun_out/${T}_phased.err
+    stamps
     ;;
 esac

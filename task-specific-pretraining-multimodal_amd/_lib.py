@@ -317,3 +317,14 @@ def linear_bwd(n, fin, fout, x, ldx, dy, ldy, w, dw, db, dx, lddx, stream) -> No
     (+ db = column sums of dy) and, if dx is given, dx = dy @ w — ONE ``tspm_linear_bwd`` launch (bitwise the two
     separate products; 2.88 -> 2.81 ms per AVMNIST step when introduced)."""
     check(lib().tspm_linear_bwd(n, fin, fout, x, ldx, dy, ldy, w, dw, db, dx, lddx, stream), "linear_bwd")
+
+
+def graph_capture(graph: "torch.cuda.CUDAGraph"):
+    """``torch.cuda.graph(graph)`` in thread-local capture mode — every captured step of this package uses it.
+    In torch's default global mode any HIP call from ANOTHER thread during the capture is illegal, and
+    torch.distributed's NCCL watchdog thread polls the end events of outstanding collectives with
+    hipEventQuery: a step captured while an all-reduce of the previous (eager) step is still in the watchdog's
+    list made that query fail with "operation not permitted when stream is capturing", the watchdog threw and
+    the process aborted (round 4's abort in destroy_process_group, reproduced and read in round 5:
+    gpurun_out/r5a_phased.err).  Thread-local mode forbids the unsafe calls only in the capturing thread."""
+    return torch.cuda.graph(graph, capture_error_mode="thread_local")

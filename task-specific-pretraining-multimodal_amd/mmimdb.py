@@ -713,7 +713,7 @@ class FusedMMIMDbStep:
             if self.graph is None:
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._all()
                 self.graph = g
             self.graph.replay()

@@ -177,7 +177,7 @@ class _MonoBuffers:
             if self.graph is None:
                 torch.cuda.synchronize(self.device)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._enqueue()
                 self.graph = g
             self.graph.replay()

@@ -611,7 +611,7 @@ class FusedMosiStep:
             if self.graph is None:
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._all()
                 self.graph = g
             self.graph.replay()
@@ -661,7 +661,7 @@ class FusedMosiEvalStep:
             if self.graph is None:
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._all()
                 self.graph = g
             self.graph.replay()

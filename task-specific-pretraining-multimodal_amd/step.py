@@ -327,7 +327,7 @@ class FusedTrainStep:
             if self.graph is None:
                 torch.cuda.synchronize(self.device)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._fwd_bwd(marks=self._marks)
                 self.graph, self.graph_opt = g, None
                 self._graph_gen_keep = self.keep_override is None
@@ -455,7 +455,7 @@ class FusedTrainStep:
     def _capture(self) -> None:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with L.graph_capture(g):
             if self.allreduce is None:
                 self._enqueue_all()
             else:
@@ -464,7 +464,7 @@ class FusedTrainStep:
         self._graph_gen_keep = self.keep_override is None
         if self.allreduce is not None:
             go = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(go):
+            with L.graph_capture(go):
                 self._opt()
             self.graph_opt = go
 
@@ -552,7 +552,7 @@ class FusedEvalStep:
             if self.graph is None or self._graph_log is not self.log:
                 torch.cuda.synchronize(self.device)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with L.graph_capture(g):
                     self._enqueue()
                 self.graph, self._graph_log = g, self.log
             self.graph.replay()
