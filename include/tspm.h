@@ -326,7 +326,8 @@ int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const in
  * Dropout(p) → Linear(hidden, hidden2) → ReLU → Linear(hidden2, classes) (models/avmnist.py:219-230,
  * forward :267), the LossFunctionGroup's weighted cross-entropy (experiment_utils/loss.py:98-148) and
  * the head's whole backward, in TWO launches instead of ten:
- *   (1) row blocks of 4 samples per workgroup, the three weight matrices staged in LDS: dropout keep
+ *   (1) one sample per workgroup (512 threads; round 5 — TSPM_HEAD_RB=4 selects round 4's blocks of 4
+ *       samples on 256 threads), the three weight matrices staged in LDS: dropout keep
  *       mask (same counter-hash bits as
  *       tspm_dropout_mask, or read from `keep` when gen_keep == 0), h1, hh, logits, per-row CE,
  *       dlogits, dz3 = (dlogits @ w5) * (hh > 0), dz0 = (dz3 @ w3) * (h1 > 0 ? 1/(1-p) : 0) and
@@ -338,8 +339,9 @@ int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const in
  * tspm_linear_fwd/_bwd + tspm_act_bwd + tspm_dropout_mask + tspm_cross_entropy (out-of-range label →
  * NaN loss and gradients), up to summation order.  Limits: in <= 256, hidden <= 256, hidden2 <= 128,
  * classes <= 16; in, hidden, hidden2 multiples of 4; w0 / w3 / x rows 16-byte aligned; the three
- * weight matrices plus the row blocks within 160 KiB of LDS (floats: hidden*(in+4) + hidden2*(hidden+4)
- * + classes*(hidden2+4) + 4*(in+hidden+hidden2+classes+16)); otherwise TSPM_ERR_INVALID. */
+ * weight matrices plus the row blocks within 160 KiB of LDS (floats, RB = rows per workgroup, logits rows
+ * padded to a multiple of 4: hidden*(in+4) + hidden2*(hidden+4) + classes*(hidden2+4)
+ * + RB*(in+hidden+hidden2+12+round_up4(classes)) + hidden+hidden2+classes+RB); otherwise TSPM_ERR_INVALID. */
 typedef struct tspm_head_desc {
   int32_t n, in, hidden, hidden2, classes, ldx, lddx, gen_keep;
   const float* x;                  /* [n, ldx] the fused embeddings (concat of the two encoders) */

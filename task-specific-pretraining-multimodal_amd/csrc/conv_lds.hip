@@ -85,8 +85,17 @@ constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
 #ifndef TSPM_LDS_WAVES_SMALL
 #define TSPM_LDS_WAVES_SMALL (TSPM_LOADER_WAVES ? 4 : 1)
 #endif
+// The 2-block wave tiles (TM * TN == 2) with at most 6 loader pieces per stage (BM + BN <= 192): 4 as well once
+// the split-K epilogue keeps 32-bit offsets (no spill at 128 VGPRs; TSPM_LDS_WAVES_LARGE=2 restores one
+// workgroup per CU for A/B); the larger tiles (9 pieces: 108 loader VGPRs) stay at 2.
+#ifndef TSPM_LDS_WAVES_LARGE
+#define TSPM_LDS_WAVES_LARGE (TSPM_LOADER_WAVES ? 2 : 1)
+#endif
 template <class C>
-constexpr int min_waves() { return C::TM * C::TN == 1 ? TSPM_LDS_WAVES_SMALL : (kLoaderThreads ? 2 : 1); }
+constexpr int min_waves() {
+  return C::TM * C::TN == 1 ? TSPM_LDS_WAVES_SMALL
+                            : (C::BM + C::BN <= 192 ? TSPM_LDS_WAVES_LARGE : (kLoaderThreads ? 2 : 1));
+}
 template <class C1, class C2>
 constexpr int min_waves2() { return min_waves<C1>() < min_waves<C2>() ? min_waves<C1>() : min_waves<C2>(); }
 constexpr int kBlock = kThreads + kLoaderThreads;
@@ -429,31 +438,31 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
     // Every slab's TM*TN*16 loads are issued together before its in-order adds (the summation order is
     // unchanged: slab z is added after slab z-1), so one slab costs one memory round trip instead of a
     // chain of them (phase stamps: the R34 layer3 forward's slab read took 7-15 us as a load-add chain).
+    // 32-bit offsets (a slab is rows * ld < 2^31 floats: checked on the host) and one 32x32 fragment's loads
+    // in flight at a time: the epilogue sets the kernel's VGPR count, and at <= 128 VGPRs the 2-block wave
+    // tiles fit two workgroups per CU (round 5)
     acc.zero();
-    long long off[C::TM][C::TN][16];
+    int off[C::TM][C::TN][16];
 #pragma unroll
     for (int a = 0; a < C::TM; ++a)
 #pragma unroll
       for (int b = 0; b < C::TN; ++b) {
         const int col = min(col0 + b * 32 + (lane & 31), cols - 1);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) off[a][b][i] = (long long)min(row0 + a * 32 + acc_row(i, lane), rows - 1) * ld + col;
+        for (int i = 0; i < 16; ++i) off[a][b][i] = min(row0 + a * 32 + acc_row(i, lane), rows - 1) * (int)ld + col;
       }
     for (int z = 0; z < splits; ++z) {
       const float* src = slabs + (long long)z * slab;
-      float v[C::TM][C::TN][16];
 #pragma unroll
       for (int a = 0; a < C::TM; ++a)
 #pragma unroll
-        for (int b = 0; b < C::TN; ++b)
+        for (int b = 0; b < C::TN; ++b) {
+          float v[16];
 #pragma unroll
-          for (int i = 0; i < 16; ++i) v[a][b][i] = ld_sc1(src + off[a][b][i]);
+          for (int i = 0; i < 16; ++i) v[i] = ld_sc1(src + off[a][b][i]);
 #pragma unroll
-      for (int a = 0; a < C::TM; ++a)
-#pragma unroll
-        for (int b = 0; b < C::TN; ++b)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc.v[a][b][i] += v[a][b][i];
+          for (int i = 0; i < 16; ++i) acc.v[a][b][i] += v[i];
+        }
     }
   }
   return true;
@@ -828,6 +837,8 @@ ConvArgs args_of(const tspm_conv_shape* s) {
 size_t splitk_ws(int splits, long long rows, long long cols) {
   return splits > 1 ? TSPM_COUNTER_BYTES + (size_t)splits * rows * cols * sizeof(float) : 0;
 }
+// the split-K reduction addresses one slab with 32-bit offsets
+bool slab_fits(int splits, long long rows, long long cols) { return splits <= 1 || rows * cols < (1LL << 31); }
 
 // dispatch over the supported (tm, tn, wm, wn, wk) combinations
 #define TSPM_LDS_CASE(TM_, TN_, WM_, WN_, WK_, FN)                                      \
@@ -910,6 +921,7 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
   ConvArgs g = args_of(s);
   g.m = s->p * s->q * s->n;
   g.splits = a.splits;
+  if (!slab_fits(a.splits, g.m, s->k)) return TSPM_ERR_INVALID;
   float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_fwd_workspace(s, a)) return TSPM_ERR_WORKSPACE;
@@ -950,6 +962,7 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
   g.m = s->h * s->w * s->n;
   g.splits = a.splits;
   g.beta = beta ? 1 : 0;
+  if (!slab_fits(a.splits, g.m, s->c)) return TSPM_ERR_INVALID;
   float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_dgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
@@ -972,6 +985,7 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
   ConvArgs g = args_of(s);
   g.m = s->k;
   g.splits = a.splits;
+  if (!slab_fits(a.splits, s->k, (long long)s->r * s->s * s->c)) return TSPM_ERR_INVALID;
   float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_wgrad_workspace(s, a)) return TSPM_ERR_WORKSPACE;
@@ -1042,6 +1056,9 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
             const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
             hipStream_t st) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
+  if (!slab_fits(ad.splits, (long long)s->h * s->w * s->n, s->c) ||
+      !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
+    return TSPM_ERR_INVALID;
   BwdLaunch L{};
   L.gd = args_of(s);
   L.gd.m = s->h * s->w * s->n;

@@ -758,7 +758,7 @@ extern "C" const char* tspm_status_string(int status) {
 namespace {
 
 // ---- fusion head train step (tspm_head_train_step) ---------------------------------------------------
-// Launch 1: one workgroup per HEAD_RB samples runs the head's whole row-local chain with the three weight
+// Launch 1: one workgroup per RB samples runs the head's whole row-local chain with the three weight
 // matrices staged in LDS (w0 + w3 + w5 = 134 KB at 192 -> 128 -> 64 -> 10; read once per workgroup with
 // 16-byte loads, so the six dependent products below see LDS latency, not L2 latency):
 //   h1 = relu(x w0^T + b0) * keep/(1-p),  hh = relu(h1 w3^T + b3),  logits = hh w5^T + b5,  CE per row,
@@ -768,18 +768,21 @@ namespace {
 // backward products read consecutive columns across lanes; the row values are LDS broadcasts.
 // Launch 2 (k_head_wgrad): the weight gradients on the small-GEMM tiles + one workgroup reducing the
 // per-row losses in row order.
-constexpr int HEAD_RB = 4;
+// Row block per workgroup (RB) and threads: RB = 1 with 512 threads by default (round 5: 128 workgroups at batch
+// 128 instead of 32 — the head sits on the critical path where the image stream idles); TSPM_HEAD_RB=4 keeps the
+// round-4 shape (4 rows, 256 threads) for A/B.
 constexpr int HEAD_MAXIN = 256, HEAD_MAXH = 256, HEAD_MAXH2 = 128, HEAD_MAXC = 16;
+constexpr int head_ldc(int C) { return ((C + 3) & ~3) + 4; }  // logits rows 16-B aligned (ld4 reads of dlogits)
 
 struct HeadArgs {
   tspm_head_desc d;
   float scale;  // 1/(1-p), or 1
 };
 
-// LDS floats of k_head_rows for a shape (weights + row blocks, every row padded by 4 floats)
-size_t head_lds_floats(int F, int H, int H2, int C) {
+// LDS floats of k_head_rows for a shape (weights + row blocks, every row padded by 4 floats; logits rows to 4)
+size_t head_lds_floats(int F, int H, int H2, int C, int RB) {
   return (size_t)H * (F + 4) + (size_t)H2 * (H + 4) + (size_t)C * (H2 + 4) +
-         (size_t)HEAD_RB * ((F + 4) + (H + 4) + (H2 + 4) + (C + 4)) + (size_t)(H + H2 + C + HEAD_RB);
+         (size_t)RB * ((F + 4) + (H + 4) + (H2 + 4) + head_ldc(C)) + (size_t)(H + H2 + C + RB);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
@@ -789,9 +792,10 @@ TSPM_DEV void head_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" :::
 
 // Y[r][o] = sum_k X[r][k] W[o][k] (W in LDS [O][ldw], K % 4 == 0; X in LDS, ld ldx) for rows [0, RB) in
 // groups of RPT rows; epi(r, o, acc) consumes each result.
-template <int RPT, class Epi>
+template <int RB, int RPT, class Epi>
 TSPM_DEV void head_xwT(const float* X, int ldx, const float* W, int ldw, int K, int O, Epi epi) {
-  constexpr int G = HEAD_RB / RPT;
+  static_assert(RB % RPT == 0, "rows per thread divide the row block");
+  constexpr int G = RB / RPT;
   for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
     const int o = item % O, rg = item / O;
     const float* wp = W + o * ldw;
@@ -829,9 +833,10 @@ TSPM_DEV void head_xwT(const float* X, int ldx, const float* W, int ldw, int K, 
 }
 
 // Y[r][o] = sum_k X[r][k] W[k][o] (W in LDS [K][ldw]: consecutive o across lanes), rows in groups of RPT.
-template <int RPT, class Epi>
+template <int RB, int RPT, class Epi>
 TSPM_DEV void head_xW(const float* X, int ldx, const float* W, int ldw, int K, int O, Epi epi) {
-  constexpr int G = HEAD_RB / RPT;
+  static_assert(RB % RPT == 0, "rows per thread divide the row block");
+  constexpr int G = RB / RPT;
   for (int item = threadIdx.x; item < O * G; item += blockDim.x) {
     const int o = item % O, rg = item / O;
     const float* xp = X + rg * RPT * ldx;
@@ -908,24 +913,26 @@ TSPM_DEV void head_store(const HeadSeg& g, const f32x4 (&v)[U]) {
   for (int i = U * (int)blockDim.x + (int)threadIdx.x; i < g.total(); i += blockDim.x) g.store(i, g.load(i));
 }
 
-__global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
+template <int RB, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_head_rows(HeadArgs a) {
+  constexpr int R2 = RB < 2 ? RB : 2, R4 = RB < 4 ? RB : 4;  // rows per thread of the fc0 / dz0 / dx products
   const tspm_head_desc& d = a.d;
   extern __shared__ float lds[];
   const int F = d.in, H = d.hidden, H2 = d.hidden2, C = d.classes;
-  const int ldx = F + 4, ldh = H + 4, ldh2 = H2 + 4, ldc = C + 4;
+  const int ldx = F + 4, ldh = H + 4, ldh2 = H2 + 4, ldc = head_ldc(C);
   float* sw0 = lds;                      // [H][F + 4]
   float* sw3 = sw0 + H * ldx;            // [H2][H + 4]
   float* sw5 = sw3 + H2 * ldh;           // [C][H2 + 4]
   float* sx = sw5 + C * ldh2;            // [RB][F + 4]
-  float* sh1 = sx + HEAD_RB * ldx;       // [RB][H + 4]
-  float* shh = sh1 + HEAD_RB * ldh;      // [RB][H2 + 4]
-  float* sz = shh + HEAD_RB * ldh2;      // [RB][C + 4]
-  float* sb0 = sz + HEAD_RB * ldc;       // biases [H], [H2], [C]; labels of the row block [RB] (as int)
+  float* sh1 = sx + RB * ldx;       // [RB][H + 4]
+  float* shh = sh1 + RB * ldh;      // [RB][H2 + 4]
+  float* sz = shh + RB * ldh2;      // [RB][C + 4]
+  float* sb0 = sz + RB * ldc;       // biases [H], [H2], [C]; labels of the row block [RB] (as int)
   float* sb3 = sb0 + H;
   float* sb5 = sb3 + H2;
   int* slab = reinterpret_cast<int*>(sb5 + C);
-  const int n0 = blockIdx.x * HEAD_RB;
-  const int rows = min(HEAD_RB, d.n - n0);
+  const int n0 = blockIdx.x * RB;
+  const int rows = min(RB, d.n - n0);
   const int t = threadIdx.x;
   TSPM_STAMP(tspm_g_stamps_misc, 0);
   TSPM_STAMP_CLK(tspm_g_stamps_misc, 6);
@@ -933,19 +940,21 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   // global load is issued first (one memory round trip); x, w0, the biases and labels are stored before fc0,
   // w3 / w5 behind it (their loads land while fc0 runs)
   const HeadSeg g3{d.w3, sw3, H2, H / 4, H2, H}, g5{d.w5, sw5, C, H2 / 4, C, H2};
-  f32x4 v3[8], v5[1];  // the default head: 128 x 64 (8 per thread), 64 x 10 (1)
+  // the default head's weights in one round: 128 x 64 (2048 float4: 8 per thread at 256), 64 x 10 (160: 1)
+  constexpr int U0 = (128 * 192 / 4 + THREADS - 1) / THREADS, U3 = (64 * 128 / 4 + THREADS - 1) / THREADS;
+  f32x4 v3[U3], v5[1];
   uint64_t base = 0;
   {
-    const HeadSeg gx{d.x + (long long)n0 * d.ldx, sx, HEAD_RB, F / 4, rows, d.ldx};
+    const HeadSeg gx{d.x + (long long)n0 * d.ldx, sx, RB, F / 4, rows, d.ldx};
     const HeadSeg g0{d.w0, sw0, H, F / 4, H, F};
-    f32x4 vx[1], v0[24];  // 192 x 128: 24 per thread
+    f32x4 vx[(RB * 256 / 4 + THREADS - 1) / THREADS], v0[U0];  // x rows (F <= 256); 192 x 128
     const uint64_t ctr = (d.p > 0.f && d.gen_keep && d.counter) ? *d.counter : 0ULL;
     head_load(gx, vx);
     head_load(g0, v0);
     head_load(g3, v3);
     head_load(g5, v5);
     // biases [H], [H2], [C] and the row block's labels: element i = t, t + blockDim (unconditional loads)
-    const int NB = H + H2 + C + HEAD_RB;
+    const int NB = H + H2 + C + RB;
     float bv[2];
     long long lv[2];
 #pragma unroll
@@ -985,7 +994,7 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   head_sync();
   TSPM_STAMP(tspm_g_stamps_misc, 1);
   // fc0 + ReLU + dropout (tspm_linear_fwd's epilogue order: + bias, relu, * keep*scale)
-  head_xwT<2>(sx, ldx, sw0, ldx, F, H, [&](int r, int o, float acc) {
+  head_xwT<RB, R2>(sx, ldx, sw0, ldx, F, H, [&](int r, int o, float acc) {
     float v = relu_f(acc + sb0[o]);
     if (d.p > 0.f) {
       const long long i = (long long)(n0 + r) * H + o;
@@ -1005,13 +1014,13 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   head_store(g5, v5);
   head_sync();
   TSPM_STAMP(tspm_g_stamps_misc, 2);
-  head_xwT<1>(sh1, ldh, sw3, ldh, H, H2, [&](int r, int o, float acc) {
+  head_xwT<RB, 1>(sh1, ldh, sw3, ldh, H, H2, [&](int r, int o, float acc) {
     const float v = relu_f(acc + sb3[o]);
     shh[r * ldh2 + o] = v;
     if (r < rows) d.hh[(long long)(n0 + r) * H2 + o] = v;
   });
   head_sync();
-  head_xwT<1>(shh, ldh2, sw5, ldh2, H2, C, [&](int r, int o, float acc) {
+  head_xwT<RB, 1>(shh, ldh2, sw5, ldh2, H2, C, [&](int r, int o, float acc) {
     const float v = acc + sb5[o];
     sz[r * ldc + o] = v;
     if (r < rows) d.logits[(long long)(n0 + r) * C + o] = v;
@@ -1021,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   // cross-entropy per row (tspm_cross_entropy's arithmetic); sz becomes dlogits.  Wave 0: 16 lanes per row,
   // lane k owns class k — the exponentials in parallel, the max scan and the sum of exponentials in class
   // order by every lane of the row (the same operations and order as one thread per row)
-  if (t < 64) {
+  if (t < 16 * RB) {
     const int r = t >> 4, k = t & 15;
     float* z = sz + r * ldc;
     const bool kv = k < C;
@@ -1055,21 +1064,21 @@ __global__ __launch_bounds__(256) void k_head_rows(HeadArgs a) {
   TSPM_STAMP(tspm_g_stamps_misc, 4);
   // dz3 = (dlogits w5) * (hh > 0)   (w5 is [C][H2]: the transposed product) -> shh; item (r, o)'s hh value
   // is read and overwritten by its own thread only
-  head_xW<1>(sz, ldc, sw5, ldh2, C, H2, [&](int r, int o, float acc) {
+  head_xW<RB, 1>(sz, ldc, sw5, ldh2, C, H2, [&](int r, int o, float acc) {
     const float v = shh[r * ldh2 + o] > 0.f ? acc : 0.f;
     if (r < rows) d.dz3[(long long)(n0 + r) * H2 + o] = v;
     shh[r * ldh2 + o] = v;
   });
   head_sync();
   // dz0 = (dz3 w3) * (h1 > 0 ? scale : 0)   (w3 is [H2][H]) -> sh1
-  head_xW<2>(shh, ldh2, sw3, ldh, H2, H, [&](int r, int o, float acc) {
+  head_xW<RB, R2>(shh, ldh2, sw3, ldh, H2, H, [&](int r, int o, float acc) {
     const float v = sh1[r * ldh + o] > 0.f ? acc * a.scale : 0.f;
     if (r < rows) d.dz0[(long long)(n0 + r) * H + o] = v;
     sh1[r * ldh + o] = v;
   });
   head_sync();
   // dx = dz0 w0   (w0 is [H][F])
-  head_xW<4>(sh1, ldh, sw0, ldx, H, F, [&](int r, int o, float acc) {
+  head_xW<RB, R4>(sh1, ldh, sw0, ldx, H, F, [&](int r, int o, float acc) {
     if (r < rows) d.dx[(long long)(n0 + r) * d.lddx + o] = acc;
   });
   TSPM_STAMP(tspm_g_stamps_misc, 5);
@@ -1133,9 +1142,18 @@ extern "C" int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t st
   if (d.p < 0.f || d.p >= 1.f || (d.p > 0.f && !d.keep)) return TSPM_ERR_INVALID;
   hipStream_t st = static_cast<hipStream_t>(stream);
   HeadArgs a{d, d.p > 0.f ? 1.0f / (1.0f - d.p) : 1.0f};
-  const size_t lds_rows = head_lds_floats(d.in, d.hidden, d.hidden2, d.classes) * sizeof(float);
+  // one sample per workgroup up to 256 rows (batch 128: 21.2 vs 26.7 us graph-timed, step -9 us); blocks of 4
+  // beyond (batch 1024: 1,024 workgroups each staging the 134 KB of weights took 52.9 vs 21.1 us,
+  // gpurun_out/r5b_head*.txt); TSPM_HEAD_RB=1/4 forces one for A/B
+  static const int rb_env = [] {
+    const char* e = getenv("TSPM_HEAD_RB");
+    return (e && e[0] == '4') ? 4 : (e && e[0] == '1') ? 1 : 0;
+  }();
+  const int rb = rb_env ? rb_env : (d.n <= 256 ? 1 : 4);
+  const size_t lds_rows = head_lds_floats(d.in, d.hidden, d.hidden2, d.classes, rb) * sizeof(float);
   if (lds_rows > 160 * 1024) return TSPM_ERR_INVALID;
-  hipLaunchKernelGGL(k_head_rows, dim3(cdiv(d.n, HEAD_RB)), dim3(256), lds_rows, st, a);
+  if (rb == 4) hipLaunchKernelGGL((k_head_rows<4, 256>), dim3(cdiv(d.n, 4)), dim3(256), lds_rows, st, a);
+  else hipLaunchKernelGGL((k_head_rows<1, 512>), dim3(d.n), dim3(512), lds_rows, st, a);
   TSPM_LAUNCH_CHECK();
   // weight gradients: dw[o,i] = sum_n dz[n,o] in[n,i], db[o] = sum_n dz[n,o] (tspm_linear_bwd_weight's
   // operands), plus the loss workgroup

@@ -88,8 +88,9 @@ def head_supported(model) -> bool:
         return False
     if F % 4 or H % 4 or H2 % 4:
         return False
-    rb = 4  # HEAD_RB
-    floats = H * (F + 4) + H2 * (H + 4) + C * (H2 + 4) + rb * ((F + 4) + (H + 4) + (H2 + 4) + (C + 4)) + (H + H2 + C + rb)
+    rb = 4  # the larger of the kernel's row blocks (TSPM_HEAD_RB=4; the default is 1)
+    ldc = ((C + 3) & ~3) + 4
+    floats = H * (F + 4) + H2 * (H + 4) + C * (H2 + 4) + rb * ((F + 4) + (H + 4) + (H2 + 4) + ldc) + (H + H2 + C + rb)
     return floats * 4 <= 160 * 1024
 
 
