@@ -1,4 +1,5 @@
-"""Print one step of a rocprofv3 kernel trace (the dispatches between two k_adam launches) as
+"""Print one step of a rocprofv3 kernel trace (the dispatches from one input gather, k_avmnist_gather, to the next;
+between k_adam_begin launches when the trace has no gather) as
 index / start offset / duration / kernel / grid, plus per-kernel-name totals.
     python scripts/trace_step.py gpurun_out/<tag>_serial/run_kernel_trace.csv [step index, default -2]"""
 import csv
@@ -9,12 +10,15 @@ from collections import defaultdict
 
 def main(path, k=-2):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    # a step starts at the bench's input gather (one per step); the optimizer launches k_adam once per flat-buffer
+    # range (several per step, on two streams), so k_adam does not mark step ends
+    mark = "k_avmnist_gather" if any("k_avmnist_gather" in r["Kernel_Name"] for r in rows) else "k_adam_begin"
     steps, cur = [], []
     for r in rows:
-        cur.append(r)
-        if "k_adam(" in r["Kernel_Name"]:
+        if mark in r["Kernel_Name"] and cur:
             steps.append(cur)
             cur = []
+        cur.append(r)
     st = steps[k]
     t0 = int(st[0]["Start_Timestamp"])
     tot = defaultdict(lambda: [0, 0.0])
