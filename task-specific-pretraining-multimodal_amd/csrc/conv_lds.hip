@@ -85,11 +85,14 @@ constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
 #ifndef TSPM_LDS_WAVES_SMALL
 #define TSPM_LDS_WAVES_SMALL (TSPM_LOADER_WAVES ? 4 : 1)
 #endif
-// The 2-block wave tiles (TM * TN == 2) with at most 6 loader pieces per stage (BM + BN <= 192): 4 as well once
-// the split-K epilogue keeps 32-bit offsets (no spill at 128 VGPRs; TSPM_LDS_WAVES_LARGE=2 restores one
-// workgroup per CU for A/B); the larger tiles (9 pieces: 108 loader VGPRs) stay at 2.
+// The 2-block wave tiles (TM * TN == 2) with at most 6 loader pieces per stage (BM + BN <= 192): 4 waves per SIMD
+// as well (round 5) once the split-K epilogue keeps 32-bit offsets (no spill at 128 VGPRs), so two workgroups
+// share a CU.  Measured (library A/B, alternating processes, gpurun_out/r5c_ab_*.json): batch 128 2.6160 vs
+// 2.6165 ms (neutral), batch 1024 conv 8.71 vs 8.84 ms per step (frac 0.479 vs 0.472), step 9.80 vs 9.83 ms.
+// TSPM_LDS_WAVES_LARGE=2 (variant 1) / 1 (variant 2) restores one workgroup per CU; the larger tiles
+// (9 pieces: 108 loader VGPRs) stay at 2 / 1.
 #ifndef TSPM_LDS_WAVES_LARGE
-#define TSPM_LDS_WAVES_LARGE (TSPM_LOADER_WAVES ? 2 : 1)
+#define TSPM_LDS_WAVES_LARGE 4
 #endif
 template <class C>
 constexpr int min_waves() {
