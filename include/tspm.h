@@ -38,8 +38,9 @@ enum {
 
 /* Version of this ABI (bumped on any signature change; 18 = round 5: the entry points no step calls removed —
  * tspm_conv_fwd_bnin, tspm_conv_wgrad_t, tspm_conv_dgrad_bnfuse / _bwd_bnfuse / _dgrad_bn_tiles,
- * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles). */
-#define TSPM_ABI_VERSION 18
+ * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles;
+ * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward). */
+#define TSPM_ABI_VERSION 19
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -225,6 +226,28 @@ int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const fl
                 float* dy_t, float* dy2_t, int64_t ld_t, void* workspace, size_t workspace_bytes,
                 tspm_stream_t stream);
 size_t tspm_bn_bwd_workspace(int64_t m, int32_t c);
+/* ABI 19: the same BN backward with its incoming gradient g formed on the fly from a pooling layer's output
+ * gradient instead of read from a materialised [m, c] tensor (one launch and the g tensor's write + reads fewer):
+ *   kind TSPM_GSRC_AVGPOOL — the encoder's AdaptiveAvgPool2d(1) + flatten (resnet.py:59-60): g[(pos, n)] =
+ *     gp[n * ldg + c] / npos, exactly tspm_avgpool_bwd's value (npos = h * w);
+ *   kind TSPM_GSRC_MAXPOOL — the stem's MaxPool2d(3, 2, 1) (resnet.py:140): g = tspm_maxpool_bwd's dx from gp
+ *     [p][q][n][c] and its argmax taps idx (same window order, bitwise).
+ * Rows m = h * w * n (HWNC) < 2^24.  Otherwise as tspm_bn_bwd without the transposed copies. */
+enum { TSPM_GSRC_AVGPOOL = 1, TSPM_GSRC_MAXPOOL = 2 };
+typedef struct tspm_bn_gsrc {
+  int32_t kind;
+  int32_t n, h, w;     /* the BN input map: m = h * w * n rows */
+  int32_t p, q;        /* maxpool: the pooled map */
+  int32_t npos, ldg;   /* avgpool: positions (= h * w) and the row stride of gp [n][ldg] */
+  const float* gp;     /* the pooling layer's output gradient */
+  const uint8_t* idx;  /* maxpool: argmax taps [p][q][n][c] (tspm_maxpool_fwd) */
+} tspm_bn_gsrc;
+int tspm_bn_bwd_src(int64_t m, int32_t c, const tspm_bn_gsrc* src, const float* out, const float* y,
+                    const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                    float* dy, const float* y2, const float* mean2, const float* invstd2, const float* gamma2,
+                    float* dgamma2, float* dbeta2, float* dy2, float* dres, void* workspace, size_t workspace_bytes,
+                    tspm_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Pooling — nn.MaxPool2d(3, 2, 1) (resnet.py:140,208) and AdaptiveAvgPool2d(1)+flatten (:149,215-216)
  * ----------------------------------------------------------------------------------------------*/

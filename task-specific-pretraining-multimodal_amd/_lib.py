@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 18
+ABI_VERSION = 19
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -48,6 +48,15 @@ class BnFuse(Structure):
                 ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float), ("save_mean", c_void_p),
                 ("save_invstd", c_void_p), ("counters_len", c_int32), ("reserved_", c_int32),
                 ("partial_floats", c_int64)]
+
+
+class BnGSrc(Structure):
+    """tspm_bn_gsrc (ABI 19): a pooling layer's output gradient as the BN backward's gradient source."""
+    _fields_ = [(n, c_int32) for n in ("kind", "n", "h", "w", "p", "q", "npos", "ldg")] + \
+        [("gp", c_void_p), ("idx", c_void_p)]
+
+
+GSRC_AVGPOOL, GSRC_MAXPOOL = 1, 2
 
 
 class AdamHyper(Structure):
@@ -118,6 +127,8 @@ _SIGS = {
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
+    # ABI 19: the BN backward with its gradient formed from a pooling layer's output gradient
+    "tspm_bn_bwd_src": (c_int32, [c_int64, c_int32, POINTER(BnGSrc)] + [_P] * 17 + [c_size_t, _P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),

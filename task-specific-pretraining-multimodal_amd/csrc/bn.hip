@@ -302,8 +302,80 @@ __global__ __launch_bounds__(256) void k_bn_apply_t(long long M, int C, const fl
 // >= 64 tiles per channel block serialises on one CU), so pass 2 stays a launch.
 // RG row groups of 16 lanes: 16 (256 threads), or 64 (1,024 threads) for the long tiles of the 64-channel
 // layers, whose partial pass has only 64 workgroups — four times the loads in flight per CU.
-template <bool HAS_OUT, bool TWO, int U, int RG = kRowGroups>
-__global__ __launch_bounds__(16 * RG) void k_bn_bwd_partial(long long M, int C, const float* __restrict__ g,
+// ------------------------------------------------------------------------------------------------
+// Where the BN backward reads its incoming gradient g[row][4 channels] (row = (h*W + w)*N + n, HWNC):
+//   GDense — a materialised [M, C] tensor (every BN of the blocks);
+//   GAvg   — the adaptive average pool's backward folded in (the encoder's last BN): g = gp[n] / npos, exactly
+//            k_avgpool_bwd's value, so the pooled-gradient broadcast is never written (one launch fewer);
+//   GMax   — the stem's MaxPool2d(3, 2, 1) backward folded in: g = the sum, over the <= 2 x 2 pool windows that
+//            contain the element and chose it (argmax tap), of the pooled gradient, in k_maxpool_bwd's order
+//            (windows p then q ascending) — bitwise that kernel's dx, never written (one launch and a 25 MB
+//            write + two reads fewer on the audio stem).
+// Round 5 (tspm_bn_bwd_src).  Row decodes use a float reciprocal corrected by one step (rows < 2^24 are exact
+// floats), not integer divisions.
+TSPM_DEV int fdiv_row(long long a, int b, float inv_b) {
+  int q = (int)((float)a * inv_b);
+  q -= (long long)q * b > a ? 1 : 0;
+  q += (long long)(q + 1) * b <= a ? 1 : 0;
+  return q;
+}
+struct GDense {
+  const float* g;
+  int C;
+  TSPM_DEV f32x4 at(long long row, int c4) const { return ld4(g + row * C + 4 * c4); }
+};
+struct GAvg {
+  const float* gp;
+  int ldg, N, npos;
+  float invN;
+  TSPM_DEV f32x4 at(long long row, int c4) const {
+    const int q = fdiv_row(row, N, invN);
+    const int n = (int)(row - (long long)q * N);
+    const f32x4 v = ld4(gp + (long long)n * ldg + 4 * c4);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[j] / (float)npos;
+    return o;
+  }
+};
+struct GMax {  // 3x3, stride 2, pad 1 (the ResNet stem pool)
+  const float* gp;
+  const uint8_t* idx;
+  int N, W, P, Q, C;
+  float invN, invW;
+  TSPM_DEV f32x4 at(long long row, int c4) const {
+    const int pos = fdiv_row(row, N, invN);
+    const int n = (int)(row - (long long)pos * N);
+    const int h = fdiv_row(pos, W, invW), w = pos - h * W;
+    const int p_lo = max(0, (h + 1 - 3 + 2) / 2), p_hi = min(P - 1, (h + 1) / 2);
+    const int q_lo = max(0, (w + 1 - 3 + 2) / 2), q_hi = min(Q - 1, (w + 1) / 2);
+    uchar4 u4[4];
+    f32x4 g4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int pc = min(p_lo + (t >> 1), P - 1), qc = min(q_lo + (t & 1), Q - 1);
+      const long long o = (((long long)pc * Q + qc) * N + n) * C + 4 * c4;
+      u4[t] = *reinterpret_cast<const uchar4*>(idx + o);
+      g4[t] = ld4(gp + o);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int p = p_lo + (t >> 1), q = q_lo + (t & 1);
+      const int kh = h - (p * 2 - 1), kw = w - (q * 2 - 1);
+      if (p > p_hi || q > q_hi || kh < 0 || kh >= 3 || kw < 0 || kw >= 3) continue;
+      const int tap = kh * 3 + kw;
+      if (u4[t].x == tap) acc[0] += g4[t][0];
+      if (u4[t].y == tap) acc[1] += g4[t][1];
+      if (u4[t].z == tap) acc[2] += g4[t][2];
+      if (u4[t].w == tap) acc[3] += g4[t][3];
+    }
+    return acc;
+  }
+};
+
+template <bool HAS_OUT, bool TWO, int U, int RG = kRowGroups, class GS = GDense>
+__global__ __launch_bounds__(16 * RG) void k_bn_bwd_partial(long long M, int C, GS gs,
                                                         const float* __restrict__ out, const float* __restrict__ y,
                                                         const float* __restrict__ mean, const float* __restrict__ y2,
                                                         const float* __restrict__ mean2, long long rows_per_block,
@@ -327,8 +399,9 @@ __global__ __launch_bounds__(16 * RG) void k_bn_bwd_partial(long long M, int C, 
       f32x4 gv[U], ov[U], yv[U], y2v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long long off = min(rb + u * RG, r_end - 1) * C + 4 * c4;
-        gv[u] = ld4(g + off);
+        const long long row = min(rb + u * RG, r_end - 1);
+        const long long off = row * C + 4 * c4;
+        gv[u] = gs.at(row, c4);
         if (HAS_OUT) ov[u] = ld4(out + off);
         yv[u] = ld4(y + off);
         if (TWO) y2v[u] = ld4(y2 + off);
@@ -432,13 +505,13 @@ __global__ __launch_bounds__(256) void k_bn_bwd_final(long long M, int C, int G,
 #define TSPM_MERGE_TILES 128
 #endif
 constexpr int kMergeTiles = TSPM_MERGE_TILES;
-template <bool HAS_OUT, bool TWO, bool DRES>
+template <bool HAS_OUT, bool TWO, bool DRES, class GS = GDense>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int G, const float* __restrict__ part,
                                                         const float* __restrict__ inv, const float* __restrict__ gamma,
                                                         const float* __restrict__ inv2, const float* __restrict__ gamma2,
                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                         float* __restrict__ dgamma2, float* __restrict__ dbeta2,
-                                                        const float* __restrict__ g, const float* __restrict__ out,
+                                                        GS gs, const float* __restrict__ out,
                                                         const float* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ y2, const float* __restrict__ mean2,
                                                         long long rows_per_block, float* __restrict__ dy,
@@ -544,7 +617,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int 
     for (int u = 0; u < U; ++u) {
       const long long row = min(rb + u * kRowGroups, r_end - 1);
       const long long off = row * C + 4 * c4;
-      gv[u] = ld4(g + off);
+      gv[u] = gs.at(row, c4);
       if (HAS_OUT) {
         const f32x4 ov = ld4(out + off);
 #pragma unroll
@@ -774,6 +847,87 @@ extern "C" size_t tspm_bn_bwd_workspace(int64_t m, int32_t c) {
   return ((size_t)3 * row_blocks(m, c) * c + 6 * (size_t)c) * sizeof(float);
 }
 
+namespace {
+// The two launches of the merged BN backward (partial sums, then the apply with the merge in its prologue) for
+// a gradient source GS; returns false when the caller must take the transposed-copy path instead (dy_t).
+template <class GS>
+int bn_bwd_merged(int64_t m, int32_t c, const GS& gs, bool gather, const float* out, const float* y,
+                  const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dy,
+                  const float* y2, const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
+                  float* dbeta2, float* dy2, float* dres, float* part, int G, hipStream_t st) {
+  const bool two = y2 != nullptr, ho = out != nullptr, dr = dres != nullptr;
+  const long long rpb = cdiv64(m, G);
+  const int Greal = (int)cdiv64(m, rpb);
+  const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
+  // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide).  16 from
+  // 32 rows per thread on: with 128 tiles the audio stem's 96,256 rows give 752-row tiles, which the old
+  // 64-rows-per-thread threshold ran at 8 (half the loads in flight: 39.7 vs 31.6 us with 64 tiles of 16;
+  // 20.4 us with 128 tiles of 16, profiles/r4/r4l_serial_step.txt; step 2.597 vs 2.599 ms, r4m2_pu*).  A
+  // gathering source (GMax: 8 loads per row) keeps 4.  (1,024-thread workgroups for the C = 64 partial pass:
+  // BN 1.020 -> 0.972 ms of device time but the step 2.778 -> 2.786 ms — the wide workgroups crowd the other
+  // encoder's stream; not built)
+  const int pu = (!bn_wide() || gather) ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
+#define BNB_P(HO, TW, U)                                                                                       \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U, kRowGroups, GS>), pgrid, dim3(256), 0, st, (long long)m, c, gs, \
+                     out, y, mean, y2, mean2, rpb, part)
+#define BNB_PU(HO, TW) \
+  if (pu == 16) { BNB_P(HO, TW, 16); } else if (pu == 8) { BNB_P(HO, TW, 8); } else { BNB_P(HO, TW, 4); }
+  if (ho) { if (two) { BNB_PU(true, true) } else { BNB_PU(true, false) } }
+  else { if (two) { BNB_PU(false, true) } else { BNB_PU(false, false) } }
+#undef BNB_PU
+#undef BNB_P
+  TSPM_LAUNCH_CHECK();
+  const int cblk = cdiv(c, kChanPerBlock);
+  long long rb = cdiv64(m, std::max(1, 512 / cblk));  // ~512 workgroups, >= 64 rows each
+  if (rb < 64) rb = 64;
+  const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
+#define BNB_M(HO, TW, DR)                                                                                         \
+  hipLaunchKernelGGL((k_bn_bwd_apply_m<HO, TW, DR, GS>), agrid, dim3(256), 0, st, (long long)m, c, Greal, part,     \
+                     invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, gs, out, y, mean, y2, mean2, rb, \
+                     dy, dy2, dres)
+  if (ho) {
+    if (two) { if (dr) BNB_M(true, true, true); else BNB_M(true, true, false); }
+    else { if (dr) BNB_M(true, false, true); else BNB_M(true, false, false); }
+  } else {
+    if (two) { if (dr) BNB_M(false, true, true); else BNB_M(false, true, false); }
+    else { if (dr) BNB_M(false, false, true); else BNB_M(false, false, false); }
+  }
+#undef BNB_M
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+}  // namespace
+
+extern "C" int tspm_bn_bwd_src(int64_t m, int32_t c, const tspm_bn_gsrc* src, const float* out, const float* y,
+                               const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                               float* dy, const float* y2, const float* mean2, const float* invstd2,
+                               const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres, void* ws,
+                               size_t ws_bytes, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || !src || !src->gp || !y || !mean || !invstd || !gamma || !dy) return TSPM_ERR_INVALID;
+  const tspm_bn_gsrc& g = *src;
+  if (g.n <= 0 || g.h <= 0 || g.w <= 0 || (long long)g.h * g.w * g.n != m || m >= (1LL << 24)) return TSPM_ERR_INVALID;
+  const bool two = y2 != nullptr;
+  if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
+  if (!ws || ws_bytes < tspm_bn_bwd_workspace(m, c)) return TSPM_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(ws);
+  const int G = std::min(row_blocks(m, c), kMergeTiles);
+  if (g.kind == TSPM_GSRC_AVGPOOL) {
+    if (g.npos != g.h * g.w || g.ldg < c || g.ldg % 4) return TSPM_ERR_INVALID;
+    const GAvg gs{g.gp, g.ldg, g.n, g.npos, 1.0f / (float)g.n};
+    return bn_bwd_merged(m, c, gs, false, out, y, mean, invstd, gamma, dgamma, dbeta, dy, y2, mean2, invstd2, gamma2,
+                         dgamma2, dbeta2, dy2, dres, part, G, st);
+  }
+  if (g.kind == TSPM_GSRC_MAXPOOL) {
+    // MaxPool2d(3, 2, 1) of the h x w map into p x q (the ResNet stem pool)
+    if (!g.idx || g.p != (g.h + 2 - 3) / 2 + 1 || g.q != (g.w + 2 - 3) / 2 + 1) return TSPM_ERR_INVALID;
+    const GMax gs{g.gp, g.idx, g.n, g.w, g.p, g.q, c, 1.0f / (float)g.n, 1.0f / (float)g.w};
+    return bn_bwd_merged(m, c, gs, true, out, y, mean, invstd, gamma, dgamma, dbeta, dy, y2, mean2, invstd2, gamma2,
+                         dgamma2, dbeta2, dy2, dres, part, G, st);
+  }
+  return TSPM_ERR_INVALID;
+}
+
 extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* out, const float* y, const float* mean,
                            const float* invstd, const float* gamma, float* dgamma, float* dbeta, float* dy,
                            const float* y2, const float* mean2, const float* invstd2, const float* gamma2,
@@ -789,53 +943,24 @@ extern "C" int tspm_bn_bwd(int64_t m, int32_t c, const float* g, const float* ou
   float* part = static_cast<float*>(ws);
   // the merged path (no dy_t) keeps the partial tiles few enough for every apply workgroup to
   // merge them in its prologue; the transposed-copy path keeps the separate final pass
-  const int G = dy_t ? row_blocks(m, c) : std::min(row_blocks(m, c), kMergeTiles);
+  if (!dy_t) {
+    if (dy2_t) return TSPM_ERR_INVALID;
+    return bn_bwd_merged(m, c, GDense{g, c}, false, out, y, mean, invstd, gamma, dgamma, dbeta, dy, y2, mean2, invstd2,
+                         gamma2, dgamma2, dbeta2, dy2, dres, part, std::min(row_blocks(m, c), kMergeTiles), st);
+  }
+  const int G = row_blocks(m, c);
   const long long rpb = cdiv64(m, G);
   const int Greal = (int)cdiv64(m, rpb);
   float* coef = part + (size_t)3 * G * c;
   const dim3 pgrid(Greal, cdiv(c, kChanPerBlock));
-  // rows per thread per batch: 4, or 8 / 16 for the long tiles of the few-channel layers (bn_wide).  16 from
-  // 32 rows per thread on: with 128 tiles the audio stem's 96,256 rows give 752-row tiles, which the old
-  // 64-rows-per-thread threshold ran at 8 (half the loads in flight: 39.7 vs 31.6 us with 64 tiles of 16;
-  // 20.4 us with 128 tiles of 16, profiles/r4/r4l_serial_step.txt; step 2.597 vs 2.599 ms, r4m2_pu*)
-  const int pu = !bn_wide() ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
-  // (1,024-thread workgroups for the C = 64 partial pass: BN 1.020 -> 0.972 ms of device time but the step
-  // 2.778 -> 2.786 ms — the wide workgroups crowd the other encoder's stream; off)
-  constexpr bool wide_rg = false;
-#define BNB_P(HO, TW, U)                                                                                     \
-  if (wide_rg)                                                                                               \
-    hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, (U > 4 ? U / 2 : 4), 64>), pgrid, dim3(1024), 0, st,        \
-                       (long long)m, c, g, out, y, mean, y2, mean2, rpb, part);                              \
-  else                                                                                                       \
-    hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U>), pgrid, dim3(256), 0, st, (long long)m, c, g, out, y,   \
-                       mean, y2, mean2, rpb, part)
-#define BNB_PU(HO, TW) \
-  if (pu == 16) { BNB_P(HO, TW, 16); } else if (pu == 8) { BNB_P(HO, TW, 8); } else { BNB_P(HO, TW, 4); }
-  if (ho) { if (two) { BNB_PU(true, true) } else { BNB_PU(true, false) } }
-  else { if (two) { BNB_PU(false, true) } else { BNB_PU(false, false) } }
-#undef BNB_PU
+  const GDense gs{g, c};
+#define BNB_P(HO, TW) \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, 4>), pgrid, dim3(256), 0, st, (long long)m, c, gs, out, y, mean, y2, \
+                     mean2, rpb, part)
+  if (ho) { if (two) { BNB_P(true, true); } else { BNB_P(true, false); } }
+  else { if (two) { BNB_P(false, true); } else { BNB_P(false, false); } }
 #undef BNB_P
   TSPM_LAUNCH_CHECK();
-  if (!dy_t) {
-    if (dy2_t) return TSPM_ERR_INVALID;
-    const int cblk = cdiv(c, kChanPerBlock);
-    long long rb = cdiv64(m, std::max(1, 512 / cblk));  // ~512 workgroups, >= 64 rows each
-    if (rb < 64) rb = 64;
-    const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
-#define BNB_M(HO, TW, DR)                                                                                       \
-  hipLaunchKernelGGL((k_bn_bwd_apply_m<HO, TW, DR>), agrid, dim3(256), 0, st, (long long)m, c, Greal, part, invstd, \
-                     gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, g, out, y, mean, y2, mean2, rb, dy, dy2, dres)
-    if (ho) {
-      if (two) { if (dr) BNB_M(true, true, true); else BNB_M(true, true, false); }
-      else { if (dr) BNB_M(true, false, true); else BNB_M(true, false, false); }
-    } else {
-      if (two) { if (dr) BNB_M(false, true, true); else BNB_M(false, true, false); }
-      else { if (dr) BNB_M(false, false, true); else BNB_M(false, false, false); }
-    }
-#undef BNB_M
-    TSPM_LAUNCH_CHECK();
-    return TSPM_OK;
-  }
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(c, 8)), dim3(256), 0, st, (long long)m, c, Greal, two ? 1 : 0, part,
                      invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, coef);
   TSPM_LAUNCH_CHECK();

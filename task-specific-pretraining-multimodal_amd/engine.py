@@ -144,6 +144,9 @@ class EncoderEngine:
         # launch less at the tail of each encoder's forward
         self.fuse_pool = True
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
+        # the pooling backwards folded into the adjacent BN backward (tspm_bn_bwd_src, round 5); TSPM_BN_POOL_SRC=0
+        # restores the separate tspm_avgpool_bwd / tspm_maxpool_bwd launches for A/B
+        self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
         c1 = encoder.conv1
@@ -426,6 +429,24 @@ class EncoderEngine:
                                 L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), None, None, 0,
                                 self.ws_bn.data_ptr(), self.ws_bn_bytes, sh), "bn_bwd")
 
+    def _bn_bwd_src(self, bn: BNOp, src: "L.BnGSrc", out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None,
+                    dres=None, sh=0):
+        """_bn_bwd with the incoming gradient formed on the fly from a pooling layer's output gradient
+        (tspm_bn_bwd_src, ABI 19): the encoder's last BN reads the average pool's gradient, the stem's BN the
+        max pool's — the pooling backward's launch and its [rows, C] gradient tensor disappear."""
+        lib = L.lib()
+        m = bn.module
+        gw, gb = self._grad(m.weight), self._grad(m.bias)
+        if bn2 is not None:
+            m2 = bn2.module
+            gw2, gb2 = self._grad(m2.weight), self._grad(m2.bias)
+        L.check(lib.tspm_bn_bwd_src(bn.rows, bn.channels, ctypes.byref(src), L.ptr(out_mask), y.data_ptr(),
+                                    bn.mean.data_ptr(), bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(),
+                                    gb.data_ptr(), dy.data_ptr(), L.ptr(y2), L.ptr(bn2.mean) if bn2 else None,
+                                    L.ptr(bn2.invstd) if bn2 else None, L.ptr(bn2.module.weight) if bn2 else None,
+                                    L.ptr(gw2) if bn2 else None, L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres),
+                                    self.ws_bn.data_ptr(), self.ws_bn_bytes, sh), "bn_bwd_src")
+
     def _wgrad(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, sh: int) -> None:
         gw = self._grad(op.module.weight)
         if not gw.is_contiguous(memory_format=torch.channels_last):
@@ -510,8 +531,15 @@ class EncoderEngine:
                        self.final_c, sh)
             h, w = self.final_hw
             G, Gn = self.gA, self.gB
-            L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c, G.data_ptr(),
-                                         sh), "avgpool_bwd")
+            # the last BN reads the average pool's gradient directly (no broadcast tensor) unless a debug hook
+            # wants the materialised block-output gradient
+            pool_src = None
+            if self.pool_src and self.debug_hook is None:
+                pool_src = L.BnGSrc(kind=L.GSRC_AVGPOOL, n=N, h=h, w=w, p=0, q=0, npos=h * w, ldg=self.final_c,
+                                    gp=self.g_pooled.data_ptr(), idx=None)
+            else:
+                L.check(lib.tspm_avgpool_bwd(h * w, N, self.final_c, self.g_pooled.data_ptr(), self.final_c,
+                                             G.data_ptr(), sh), "avgpool_bwd")
             lo, hi = (self.split_block if phase == 1 else 0), len(self.blocks)
         else:
             G, Gn = self._bw_state
@@ -526,9 +554,15 @@ class EncoderEngine:
             Gv = G[:n_out]
             Gnv = Gn[:n_in]
             d2 = bp.g_y2
+            src = pool_src if (phase in (0, 1) and i == len(self.blocks) - 1) else None
             if bp.ds_conv is not None:
                 dd = bp.g_yd
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+                if src is not None:
+                    self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+                else:
+                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+            elif src is not None:
+                self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
                 self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
@@ -560,9 +594,14 @@ class EncoderEngine:
         # stem: maxpool -> relu/bn -> conv1 (weight grad only)
         p1, q1, p2, q2 = self.mp_shape
         C0 = self.stem.shape.k
-        L.check(lib.tspm_maxpool_bwd(N, p1, q1, C0, 3, 2, 1, p2, q2, G.data_ptr(), self.mp_idx.data_ptr(),
-                                     self.g_stem.data_ptr(), sh), "maxpool_bwd")
-        self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
+        if self.pool_src:  # the stem BN reads the max pool's gradient through its argmax taps (no g_stem tensor)
+            src = L.BnGSrc(kind=L.GSRC_MAXPOOL, n=N, h=p1, w=q1, p=p2, q=q2, npos=0, ldg=0, gp=G.data_ptr(),
+                           idx=self.mp_idx.data_ptr())
+            self._bn_bwd_src(self.stem_bn, src, self.a0, self.y0, self.dy_stem, sh=sh)
+        else:
+            L.check(lib.tspm_maxpool_bwd(N, p1, q1, C0, 3, 2, 1, p2, q2, G.data_ptr(), self.mp_idx.data_ptr(),
+                                         self.g_stem.data_ptr(), sh), "maxpool_bwd")
+            self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)
         self._wgrad(self.stem, self.x_in.data_ptr(), self.input_strides(self.x_in), self.dy_stem, sh)
 
 
