@@ -39,7 +39,8 @@ enum {
 /* Version of this ABI (bumped on any signature change; 18 = round 5: the entry points no step calls removed —
  * tspm_conv_fwd_bnin, tspm_conv_wgrad_t, tspm_conv_dgrad_bnfuse / _bwd_bnfuse / _dgrad_bn_tiles,
  * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles;
- * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward). */
+ * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward, and
+ * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch). */
 #define TSPM_ABI_VERSION 19
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
@@ -209,6 +210,14 @@ int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const
                        const float* gamma, const float* beta, int32_t res_mode, const float* res,
                        const float* res_mean, const float* res_inv, const float* res_gamma, const float* res_beta,
                        int32_t relu, int32_t eval, float eps, float* out, float* pooled, tspm_stream_t stream);
+
+/* ABI 19: the stem's BN apply + ReLU with the following MaxPool2d(3, 2, 1) in the same launch (resnet.py:138-140):
+ * pooled [p][q][n][c] and its argmax taps idx exactly as tspm_maxpool_fwd over tspm_bn_apply's output, and that
+ * output out [h][w][n][c] (nullable; the BN backward's ReLU mask) — bitwise the two launches.  eval != 0: inv is
+ * the running variance and eps applies (tspm_bn_apply_eval's arithmetic).  p = (h-1)/2+1, q = (w-1)/2+1. */
+int tspm_bn_apply_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y, const float* mean,
+                          const float* inv, const float* gamma, const float* beta, int32_t eval, float eps, float* out,
+                          float* pooled, uint8_t* idx, int32_t p, int32_t q, tspm_stream_t stream);
 
 /* BN backward through  out = relu(BN(y) [+ BN2(y2)])  (y2 / second BN optional, may be NULL):
  *   g' = g * (out > 0)  (out may be NULL: no ReLU)

@@ -127,7 +127,8 @@ _SIGS = {
     "tspm_bn_bwd": (c_int32, [c_int64, c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
-    # ABI 19: the BN backward with its gradient formed from a pooling layer's output gradient
+    # ABI 19: the stem's apply + ReLU + max pool in one launch; the BN backward reading a pooling layer's gradient
+    "tspm_bn_apply_maxpool": (c_int32, [c_int32] * 4 + [_P] * 5 + [c_int32, c_float, _P, _P, _P, c_int32, c_int32, _P]),
     "tspm_bn_bwd_src": (c_int32, [c_int64, c_int32, POINTER(BnGSrc)] + [_P] * 17 + [c_size_t, _P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),

@@ -160,6 +160,61 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
   }
 }
 
+// The stem's BN apply + ReLU with the MaxPool2d(3, 2, 1) that follows it folded in (resnet.py:138-140; round 5):
+// thread = (pooled output (p, q, n), 4 channels).  It forms relu(bn(y)) for the 3 x 3 window (k_bn_apply's
+// arithmetic), keeps the first maximum in row-major window order with NaN winning (k_maxpool_fwd's rule) and
+// writes the pooled value and its argmax tap; it also stores the activation `out` of the window elements it owns
+// — rows 2p, 2p+1 x columns 2q, 2q+1, which tile the map exactly once — for the BN backward's ReLU mask.  Bitwise
+// tspm_bn_apply + tspm_maxpool_fwd, one launch and one re-read of the activation fewer.
+template <bool EVAL>
+__global__ __launch_bounds__(256) void k_bn_apply_maxpool(int N, int H, int W, int C, int P, int Q,
+                                                          const float* __restrict__ y, const float* __restrict__ mean,
+                                                          const float* __restrict__ inv, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float* __restrict__ out, float* __restrict__ pooled,
+                                                          uint8_t* __restrict__ idx) {
+  const int L = C >> 2;
+  const long long total = (long long)P * Q * N * L;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % L);
+    const long long row = i / L;  // (p, q, n)
+    const int n = (int)(row % N);
+    const int pos = (int)(row / N);
+    const int p = pos / Q, q = pos - p * Q;
+    f32x4 mu = ld4(mean + 4 * c4), iv = ld4(inv + 4 * c4);
+    if (EVAL) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) iv[j] = 1.0f / sqrtf(iv[j] + eps);
+    }
+    const f32x4 sc = ld4(gamma + 4 * c4) * iv;
+    const f32x4 sf = ld4(beta + 4 * c4) - mu * sc;
+    f32x4 v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int h = min(max(2 * p - 1 + t / 3, 0), H - 1), w = min(max(2 * q - 1 + t % 3, 0), W - 1);
+      v[t] = ld4(y + (((long long)h * W + w) * N + n) * C + 4 * c4);
+    }
+    f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int h = 2 * p - 1 + t / 3, w = 2 * q - 1 + t % 3;
+      if (h < 0 || h >= H || w < 0 || w >= W) continue;
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = relu_f(fmaf(v[t][j], sc[j], sf[j]));
+      if (out && t / 3 >= 1 && t % 3 >= 1) st4(out + (((long long)h * W + w) * N + n) * C + 4 * c4, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (a[j] > best[j] || isnan(a[j])) { best[j] = a[j]; bi[j] = t; }
+    }
+    st4(pooled + row * C + 4 * c4, best);
+    uchar4 u;
+    u.x = (uint8_t)bi[0]; u.y = (uint8_t)bi[1]; u.z = (uint8_t)bi[2]; u.w = (uint8_t)bi[3];
+    *reinterpret_cast<uchar4*>(idx + row * C + 4 * c4) = u;
+  }
+}
+
 // The encoder's last BasicBlock apply with the adaptive average pool over its npos positions folded in
 // (resnet.py:55-57 then :59-60): thread = (sample n, 4 channels), looping the positions — out as k_bn_apply
 // writes it (the backward reads it) and pooled[n] = (sum over p in order) / npos, as k_avgpool_fwd computes it.
@@ -838,6 +893,26 @@ extern "C" int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const floa
     else if (res_mode == 1) { if (r) BN_APPLY_POOL_LAUNCH(1, true, true); else BN_APPLY_POOL_LAUNCH(1, false, true); }
     else { if (r) BN_APPLY_POOL_LAUNCH(2, true, true); else BN_APPLY_POOL_LAUNCH(2, false, true); }
   }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+extern "C" int tspm_bn_apply_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y, const float* mean,
+                                     const float* inv, const float* gamma, const float* beta, int32_t eval, float eps,
+                                     float* out, float* pooled, uint8_t* idx, int32_t p, int32_t q,
+                                     tspm_stream_t stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || !c_ok(c) || !y || !mean || !inv || !gamma || !beta || !pooled || !idx)
+    return TSPM_ERR_INVALID;
+  if (p != (h - 1) / 2 + 1 || q != (w - 1) / 2 + 1) return TSPM_ERR_INVALID;
+  const long long total = (long long)p * q * n * (c / 4);
+  const dim3 grid((unsigned)std::min<long long>(cdiv64(total, 256), 8192));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (eval)
+    hipLaunchKernelGGL(k_bn_apply_maxpool<true>, grid, dim3(256), 0, st, n, h, w, c, p, q, y, mean, inv, gamma, beta,
+                       eps, out, pooled, idx);
+  else
+    hipLaunchKernelGGL(k_bn_apply_maxpool<false>, grid, dim3(256), 0, st, n, h, w, c, p, q, y, mean, inv, gamma, beta,
+                       eps, out, pooled, idx);
   TSPM_LAUNCH_CHECK();
   return TSPM_OK;
 }

@@ -147,6 +147,8 @@ class EncoderEngine:
         # the pooling backwards folded into the adjacent BN backward (tspm_bn_bwd_src, round 5); TSPM_BN_POOL_SRC=0
         # restores the separate tspm_avgpool_bwd / tspm_maxpool_bwd launches for A/B
         self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
+        # the stem's BN apply + ReLU + max pool forward in one launch (A/B switch TSPM_STEM_FUSE=0)
+        self.stem_fuse = os.environ.get("TSPM_STEM_FUSE", "1") != "0"
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
         c1 = encoder.conv1
@@ -373,9 +375,17 @@ class EncoderEngine:
             self._conv_bn(self.stem, self.stem_bn, x.data_ptr(), xs, self.y0, sh)
         else:
             self._conv_fwd(self.stem, x.data_ptr(), xs, self.y0, sh)
-        self._apply(self.stem_bn, self.y0, self.a0, relu=True, sh=sh, train=train)
-        L.check(lib.tspm_maxpool_fwd(N, p1, q1, C0, 3, 2, 1, p2, q2, self.a0.data_ptr(), self.mp.data_ptr(),
-                                     self.mp_idx.data_ptr(), None, 0, sh), "maxpool_fwd")
+        if self.stem_fuse:  # BN apply + ReLU + max pool in one launch (tspm_bn_apply_maxpool, ABI 19)
+            m = self.stem_bn.module
+            mean, inv = ((self.stem_bn.mean, self.stem_bn.invstd) if train else (m.running_mean, m.running_var))
+            L.check(lib.tspm_bn_apply_maxpool(N, p1, q1, C0, self.y0.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                              m.weight.data_ptr(), m.bias.data_ptr(), 0 if train else 1, m.eps,
+                                              self.a0.data_ptr(), self.mp.data_ptr(), self.mp_idx.data_ptr(), p2, q2,
+                                              sh), "bn_apply_maxpool")
+        else:
+            self._apply(self.stem_bn, self.y0, self.a0, relu=True, sh=sh, train=train)
+            L.check(lib.tspm_maxpool_fwd(N, p1, q1, C0, 3, 2, 1, p2, q2, self.a0.data_ptr(), self.mp.data_ptr(),
+                                         self.mp_idx.data_ptr(), None, 0, sh), "maxpool_fwd")
         xin = self.mp
         for bp in self.blocks:
             pool = self.pooled if (bp is self.blocks[-1] and self.fuse_pool) else None

@@ -105,3 +105,44 @@ def test_bn_bwd_src_rejects_bad_sources(gpu):
            L.BnGSrc(kind=L.GSRC_MAXPOOL, n=4, h=3, w=4, p=2, q=2, gp=p, idx=None)]   # no argmax taps
     for src in bad:
         assert lib.tspm_bn_bwd_src(48, 4, ctypes.byref(src), *args) == 1
+
+
+@pytest.mark.parametrize("n,h,w,c", [(128, 16, 47, 64), (128, 14, 14, 64), (5, 7, 9, 8), (3, 2, 3, 4), (2, 1, 1, 4)])
+@pytest.mark.parametrize("ev", [0, 1])
+def test_bn_apply_maxpool_equals_apply_then_maxpool(gpu, n, h, w, c, ev):
+    """tspm_bn_apply_maxpool (ABI 19) == tspm_bn_apply[_eval] + tspm_maxpool_fwd, bitwise, NaN and ties included."""
+    lib = L.lib()
+    m = h * w * n
+    p2, q2 = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    g = torch.Generator().manual_seed(n + h + w + c + ev)
+    y = (torch.randn(m, c, generator=g) * 2).round(decimals=1)
+    y[torch.rand(m, c, generator=g) < 0.01] = float("nan")
+    y = y.to(gpu)
+    mean = torch.randn(c, generator=g).to(gpu)
+    inv = (torch.rand(c, generator=g) + 0.5).to(gpu)
+    gamma, beta = torch.randn(c, generator=g).to(gpu), torch.randn(c, generator=g).to(gpu)
+    s = L.stream_handle()
+    a_ref = torch.empty(m, c, device=gpu)
+    if ev:
+        L.check(lib.tspm_bn_apply_eval(m, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), 1e-5, gamma.data_ptr(),
+                                       beta.data_ptr(), 0, None, None, None, None, None, 1, a_ref.data_ptr(), s), "ev")
+    else:
+        L.check(lib.tspm_bn_apply(m, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+                                  beta.data_ptr(), 0, None, None, None, None, None, 1, a_ref.data_ptr(), None, 0, s), "ap")
+    pr = torch.empty(p2 * q2 * n, c, device=gpu)
+    ir = torch.empty(p2 * q2 * n, c, dtype=torch.uint8, device=gpu)
+    L.check(lib.tspm_maxpool_fwd(n, h, w, c, 3, 2, 1, p2, q2, a_ref.data_ptr(), pr.data_ptr(), ir.data_ptr(), None, 0,
+                                 s), "mp")
+    a = torch.full((m, c), 7.0, device=gpu)
+    pg = torch.full_like(pr, 7.0)
+    ig = torch.full_like(ir, 99)
+    L.check(lib.tspm_bn_apply_maxpool(n, h, w, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+                                      beta.data_ptr(), ev, 1e-5, a.data_ptr(), pg.data_ptr(), ig.data_ptr(), p2, q2, s),
+            "fused")
+    torch.cuda.synchronize()
+    for got, ref in ((a, a_ref), (pg, pr)):
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(ig, ir)
+    assert lib.tspm_bn_apply_maxpool(n, h, w, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+                                     beta.data_ptr(), ev, 1e-5, a.data_ptr(), pg.data_ptr(), ig.data_ptr(), p2 + 1, q2,
+                                     s) == 1
