@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--replays", type=int, default=10)
+    ap.add_argument("--dump", default="", help="write one step's kernels (stream, start, duration, name) here")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -81,6 +82,12 @@ def main():
                     "fwd_end_main_us": round(main_fwd_end, 1), "fwd_end_side_us": round(side_end_fwd, 1) if side else None,
                     "adam_start_us": round(adam[-1]["ts"] - t0, 1) if adam else None,
                     "bwd_end_side_us": round(max(e for _, e in by[side]) - t0, 1) if side else None})
+    if a.dump and len(steps) > 2:
+        st = steps[len(steps) // 2]
+        t0 = min(k["ts"] for k in st)
+        with open(a.dump, "w") as f:
+            for k in sorted(st, key=lambda k: k["ts"]):
+                f.write(f"{k['stream']:>3} {k['ts'] - t0:9.1f} {k['dur']:7.1f} {k['name'][:110]}\n")
     med = lambda key: (lambda v: v[len(v) // 2] if v else None)(sorted(r[key] for r in res if r[key] is not None))  # noqa: E731
     out = {"batch": a.batch, "steps": len(res), "median": {k: med(k) for k in
                                                           ("span_us", "union_busy_us", "both_streams_busy_us", "idle_us",

@@ -318,9 +318,20 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
       constexpr int RS = reg_stages<NI>();
       f32x4 R[RS][NI];
       auto load = [&](int st, f32x4 (&Rb)[NI]) {
+#if defined(TSPM_EXP_SAMEADDR)  // diagnostic ablation (A/B builds only): every stage re-reads stage st0's operands
+        const Off off = prep(st0 + 0 * st);
+#else
         const Off off = prep(st);
+#endif
 #pragma unroll
-        for (int i = 0; i < NI; ++i) Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+        for (int i = 0; i < NI; ++i) {
+#if defined(TSPM_EXP_NOLOAD)  // diagnostic ablation (A/B builds only): no operand traffic, address-dependent values
+          const float v = (float)(reinterpret_cast<uintptr_t>(src_i(off, i)) & 7);
+          Rb[i] = f32x4{v, v, v, v};
+#else
+          Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+#endif
+        }
       };
       auto store = [&](int it, f32x4 (&Rb)[NI]) {
 #pragma unroll

@@ -146,3 +146,30 @@ def test_bn_apply_maxpool_equals_apply_then_maxpool(gpu, n, h, w, c, ev):
     assert lib.tspm_bn_apply_maxpool(n, h, w, c, y.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
                                      beta.data_ptr(), ev, 1e-5, a.data_ptr(), pg.data_ptr(), ig.data_ptr(), p2 + 1, q2,
                                      s) == 1
+
+
+def test_pool_fusions_leave_the_step_bitwise_unchanged(gpu, monkeypatch):
+    """Four graph-replayed AVMNIST steps with the pooling fusions (TSPM_BN_POOL_SRC / TSPM_STEM_FUSE, the
+    defaults) give bitwise the parameters, BN buffers and Adam moments of the step with the separate pooling
+    launches."""
+    import tspm_amd
+    from oracle import avmnist_ref as orc
+    results = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("TSPM_BN_POOL_SRC", on)
+        monkeypatch.setenv("TSPM_STEM_FUSE", on)
+        torch.manual_seed(11)
+        ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
+        st = tspm_amd.FusedTrainStep(ours, opt, None, 32)
+        for i in range(4):
+            audio, image, labels, _ = orc.synthetic_batch(32, seed=90 + i)
+            st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+        torch.cuda.synchronize()
+        assert all(e.pool_src == (on == "1") and e.stem_fuse == (on == "1") for e in (st.eng_a, st.eng_i))
+        bufs = [t.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)
+                for t in (m.running_mean, m.running_var)]
+        mom = [t for fg in opt.flat_groups() for t in (fg.exp_avg, fg.exp_avg_sq)]
+        results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs + mom).cpu())
+        st.close()
+    assert torch.equal(results[0], results[1])
