@@ -211,6 +211,12 @@ int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const
                        const float* res_mean, const float* res_inv, const float* res_gamma, const float* res_beta,
                        int32_t relu, int32_t eval, float eps, float* out, float* pooled, tspm_stream_t stream);
 
+/* ABI 19: minimum dynamic LDS (bytes, <= 160 KiB; 0 = none) of the LDS-staged conv launches issued after this call
+ * (variants 1 and 2): a floor caps how many of one launch's workgroups share a CU, so a concurrent stream keeps CU
+ * room.  Process-wide host state read at launch time; a captured launch keeps the value it was captured with.
+ * Set by the step for the encoder with slack (step.py, TSPM_SLACK_LDS_FLOOR). */
+int tspm_set_conv_lds_floor(size_t bytes);
+
 /* ABI 19: the stem's BN apply + ReLU with the following MaxPool2d(3, 2, 1) in the same launch (resnet.py:138-140):
  * pooled [p][q][n][c] and its argmax taps idx exactly as tspm_maxpool_fwd over tspm_bn_apply's output, and that
  * output out [h][w][n][c] (nullable; the BN backward's ReLU mask) — bitwise the two launches.  eval != 0: inv is

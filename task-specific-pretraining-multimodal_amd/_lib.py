@@ -128,6 +128,7 @@ _SIGS = {
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
     # ABI 19: the stem's apply + ReLU + max pool in one launch; the BN backward reading a pooling layer's gradient
+    "tspm_set_conv_lds_floor": (c_int32, [c_size_t]),
     "tspm_bn_apply_maxpool": (c_int32, [c_int32] * 4 + [_P] * 5 + [c_int32, c_float, _P, _P, _P, c_int32, c_int32, _P]),
     "tspm_bn_bwd_src": (c_int32, [c_int64, c_int32, POINTER(BnGSrc)] + [_P] * 17 + [c_size_t, _P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),

@@ -683,6 +683,15 @@ extern "C" int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* s, con
   return 3LL * tspm_conv_fwd_tiles(s, user) * s->k;
 }
 
+namespace tspm_detail {
+size_t g_lds_floor = 0;
+}
+extern "C" int tspm_set_conv_lds_floor(size_t bytes) {
+  if (bytes > 160 * 1024) return TSPM_ERR_INVALID;
+  tspm_detail::g_lds_floor = bytes;
+  return TSPM_OK;
+}
+
 extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
                              const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn, void* ws,
                              size_t ws_bytes, tspm_stream_t stream) {

@@ -248,6 +248,11 @@ struct LdsImpl {
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();
+// Minimum dynamic LDS of the LDS-staged launches (tspm_set_conv_lds_floor): a caller-chosen floor caps how many
+// of a launch's workgroups share a CU, leaving room for a concurrent stream's kernels.  Host state read at
+// launch time (a captured launch keeps the value it was captured with).
+extern size_t g_lds_floor;
+inline size_t lds_with_floor(size_t lds) { return std::max(lds, std::min(g_lds_floor, (size_t)160 * 1024)); }
 // The 1-channel 7x7/2 stems, tspm_conv_algo.variant 3 (stem.hip)
 bool stem_supported(const tspm_conv_shape* s);
 int stem_pb(const tspm_conv_shape* s);

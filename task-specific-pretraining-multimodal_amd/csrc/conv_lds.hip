@@ -374,7 +374,11 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
       if (it == 0) TSPM_STAMP(tspm_g_stamps_lds, 1);
       frags(lds + (it % D) * SF, A, B);
       TSPM_LOOP_LAP(lds);
+#if defined(TSPM_EXP_NOMFMA)  // diagnostic ablation (A/B builds only): fragments read, no matrix work
+      acc.v[0][0][0] += A[0][0][0] + B[0][0][0];
+#else
       mma_plain<C>(acc, A, B);
+#endif
       TSPM_LOOP_LAP(mma);
       TSPM_LOOP_STAGE();
     }
@@ -958,7 +962,7 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
     if (!room) bf.counters = nullptr;
   }
   const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
-  const size_t lds = lds_bytes(a, bf.counters != nullptr);
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, bf.counters != nullptr));
 #define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
@@ -985,7 +989,7 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
   }
   const dim3 grid(g.m / bm_of(a), cdiv(s->c, bn_of(a)), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
-  const size_t lds = lds_bytes(a, false);
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false));
 #define TSPM_DG(CFG) hipLaunchKernelGGL(k_dgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, dy, w, dx, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_DG) }();
 #undef TSPM_DG
@@ -1009,7 +1013,7 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
   const int RSC = s->r * s->s * s->c;
   const dim3 grid(cdiv(s->k, bm_of(a)), RSC / bn_of(a), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
-  const size_t lds = lds_bytes(a, false);
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false));
 #define TSPM_WG(CFG) hipLaunchKernelGGL(k_wgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, dy, dw, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_WG) }();
 #undef TSPM_WG
@@ -1100,7 +1104,7 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
   if ((ad.splits > 1 && (size_t)L.dgx * L.dgy > cmax) || (aw.splits > 1 && (size_t)L.wgx * L.wgy > cmax))
     return TSPM_ERR_INVALID;
   L.dy = dy; L.w = w; L.x = x; L.dx = dx; L.dw = dw;
-  L.lds = std::max(lds_bytes(ad, false), lds_bytes(aw, false));
+  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)));
   L.st = st;
   bwd_dispatch(ad, aw, &L);
   TSPM_LAUNCH_CHECK();

@@ -139,7 +139,7 @@ class EncoderEngine:
         # at batch 128 (within the box-to-box spread), equal at 1024 (profiles/r4/r4n_ab_bn2.json,
         # r4o_ab_bn2_b1024.json), while the merge tails inflate the conv kernels' device time — the conv
         # roofline that tracks the conv kernels reads 0.193 instead of 0.205 (profiles/r4_v1_bench.json)
-        self.bn_two_level = False
+        self.bn_two_level = os.environ.get("TSPM_BN_TWO_LEVEL", "0") == "1"
         # the last block's BN apply also writes the average-pooled features (tspm_bn_apply_pool, ABI 17): one
         # launch less at the tail of each encoder's forward
         self.fuse_pool = True

@@ -16,6 +16,7 @@ zero_grad pass); with world_size > 1 the flat buffer is all-reduced between back
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 from typing import Dict, Optional
@@ -164,6 +165,11 @@ class FusedTrainStep:
         # shared by every step build: L.shared_streams)
         self.side, self.comm = L.shared_streams(dev, 2)
         self.serial = os.environ.get("TSPM_SERIAL", "0") == "1"  # True: one stream (per-kernel timing)
+        # the audio encoder's LDS-staged convs with an 82,000-byte LDS floor: one workgroup per CU, leaving room
+        # for the image chain, the replayed step's critical path (scripts/overlap_probe.py --dump: image forward +
+        # head + image backward + image Adam).  A/B, alternating processes: 2.5907 vs 2.6280 ms (56,000 bytes:
+        # 2.613 vs 2.630), profiles/r5/r5i_floor*.json.  TSPM_SLACK_LDS_FLOOR=0 restores the unconstrained launches
+        self.slack_lds_floor = int(os.environ.get("TSPM_SLACK_LDS_FLOOR", "82000"))
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         # single-GPU step (adam_split): each encoder's parameters updated by Adam on that encoder's stream right
@@ -220,7 +226,8 @@ class FusedTrainStep:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-        self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
+        with self._slack_floor():
+            self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
         main.wait_stream(side)
         sh = main.cuda_stream
         # (the head's weight-gradient launch on the image stream, beside the audio backward, was measured slower:
@@ -230,12 +237,14 @@ class FusedTrainStep:
         side.wait_stream(main)
         if marks is not None:
             mark_a, mark_i = marks
-            self.eng_a.backward(self.dfused, self.F, phase=1)
+            with self._slack_floor():
+                self.eng_a.backward(self.dfused, self.F, phase=1)
             mark_a.bump(main)
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F, phase=1)
                 mark_i.bump(side)
-            self.eng_a.backward(None, self.F, phase=2)
+            with self._slack_floor():
+                self.eng_a.backward(None, self.F, phase=2)
             with torch.cuda.stream(side):
                 self.eng_i.backward(None, self.F, phase=2)
         elif self._split_opt():
@@ -248,14 +257,30 @@ class FusedTrainStep:
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F)
                 self.opt.launch_ranges(side.cuda_stream, img)
-            self.eng_a.backward(self.dfused, self.F)
+            with self._slack_floor():
+                self.eng_a.backward(self.dfused, self.F)
             self.opt.launch_ranges(main.cuda_stream, rest)
         else:
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F)
-            self.eng_a.backward(self.dfused, self.F)
+            with self._slack_floor():
+                self.eng_a.backward(self.dfused, self.F)
         main.wait_stream(side)
         L.counters_add(self.nbt)
+
+    @contextlib.contextmanager
+    def _slack_floor(self):
+        """The audio encoder's LDS-staged conv launches with a minimum LDS allocation (tspm_set_conv_lds_floor,
+        TSPM_SLACK_LDS_FLOOR bytes), so fewer of its workgroups share a CU with the image chain
+        (the replayed step's critical path, scripts/overlap_probe.py --dump)."""
+        floor = self.slack_lds_floor
+        if floor and not self.serial:
+            L.check(L.lib().tspm_set_conv_lds_floor(floor), "set_conv_lds_floor")
+        try:
+            yield
+        finally:
+            if floor and not self.serial:
+                L.check(L.lib().tspm_set_conv_lds_floor(0), "set_conv_lds_floor")
 
     def _split_opt(self) -> bool:
         """Adam launched per encoder inside the fwd/bwd enqueue (single GPU, no gradient clipping: the

@@ -365,3 +365,26 @@ def test_pretrained_config_param_groups_run_fused_step(gpu, tmp_path):
         torch.cuda.synchronize()
         res.append(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu())
     assert torch.equal(res[0], res[1])
+
+
+def test_audio_lds_floor_leaves_the_step_bitwise_unchanged(gpu, monkeypatch):
+    """The audio encoder's LDS floor (TSPM_SLACK_LDS_FLOOR, the default 82,000 bytes vs 0) changes only how many
+    workgroups share a CU: four replayed steps' parameters, BN buffers and Adam moments are bitwise unchanged."""
+    results = []
+    for floor in ("0", "82000"):
+        monkeypatch.setenv("TSPM_SLACK_LDS_FLOOR", floor)
+        torch.manual_seed(17)
+        ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+        opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
+        st = tspm_amd.FusedTrainStep(ours, opt, None, 32)
+        assert st.slack_lds_floor == int(floor)
+        for i in range(4):
+            audio, image, labels, _ = orc.synthetic_batch(32, seed=40 + i)
+            st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+        torch.cuda.synchronize()
+        bufs = [t.detach().reshape(-1) for m in ours.modules() if isinstance(m, torch.nn.BatchNorm2d)
+                for t in (m.running_mean, m.running_var)]
+        mom = [t for fg in opt.flat_groups() for t in (fg.exp_avg, fg.exp_avg_sq)]
+        results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs + mom).cpu())
+        st.close()
+    assert torch.equal(results[0], results[1])
