@@ -40,8 +40,9 @@ enum {
  * tspm_conv_fwd_bnin, tspm_conv_wgrad_t, tspm_conv_dgrad_bnfuse / _bwd_bnfuse / _dgrad_bn_tiles,
  * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles;
  * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward, and
- * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch). */
-#define TSPM_ABI_VERSION 19
+ * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch, and tspm_set_conv_lds_floor;
+ * 20 = tspm_conv_bwd_adam, the fused backward launch carrying an Adam update over earlier-finished parameters). */
+#define TSPM_ABI_VERSION 20
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -433,6 +434,26 @@ int tspm_adam_step(int64_t count, float* param, const float* grad, float* exp_av
  * MML_Suite/models/msa/utt_fusion.py:188-190).  g' = (g * grad_scale) * clip_coef. */
 int tspm_adam_step_clip(int64_t count, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                         const tspm_adam_hyper* hyper, const float* clip_coef, tspm_stream_t stream);
+
+/* ABI 20: tspm_conv_bwd that also carries an Adam update: `blocks` extra workgroups of the same grid run
+ * tspm_adam_step's element loop over `count` elements starting at param / grad / exp_avg / exp_avg_sq (a range of
+ * the optimizer's flat buffers whose gradients an EARLIER launch on the stream finished and which no later launch
+ * reads), bitwise tspm_adam_step over that range (hyper->step must already be advanced by tspm_adam_begin).  The
+ * optimizer pass that follows the backward (MML_Suite train loop: loss.backward(); optimizer.step(),
+ * train_multimodal.py) is thereby spread over the backward's latency-bound launches instead of following them.
+ * count = 0: plain tspm_conv_bwd. */
+typedef struct tspm_adam_job {
+  float* param;
+  const float* grad;
+  float *exp_avg, *exp_avg_sq;
+  int64_t count;
+  const tspm_adam_hyper* hyper;
+  int32_t blocks, pad_;
+} tspm_adam_job;
+int tspm_conv_bwd_adam(const tspm_conv_shape* s, const tspm_conv_algo* dgrad_algo, const tspm_conv_algo* wgrad_algo,
+                       const float* x, const tspm_strides4* x_strides, const float* dy, const float* w, float* dx,
+                       int32_t beta, float* dw, const tspm_adam_job* job, void* ws_d, size_t ws_d_bytes, void* ws_w,
+                       size_t ws_w_bytes, tspm_stream_t stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Layout / data-stage helpers (collate → device, MML_Suite/data/avmnist.py:186-191,248-277)

@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -48,6 +48,14 @@ class BnFuse(Structure):
                 ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float), ("save_mean", c_void_p),
                 ("save_invstd", c_void_p), ("counters_len", c_int32), ("reserved_", c_int32),
                 ("partial_floats", c_int64)]
+
+
+class AdamJob(ctypes.Structure):
+    """tspm_adam_job (ABI 20): an Adam update over `count` elements of FusedAdam's flat buffers (pointers at the
+    range start) carried by `blocks` extra workgroups of a tspm_conv_bwd_adam launch."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("count", ctypes.c_int64), ("hyper", ctypes.c_void_p),
+                ("blocks", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 class BnGSrc(Structure):
@@ -129,6 +137,8 @@ _SIGS = {
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
     # ABI 19: the stem's apply + ReLU + max pool in one launch; the BN backward reading a pooling layer's gradient
     "tspm_set_conv_lds_floor": (c_int32, [c_size_t]),
+    # ABI 20: the fused backward launch carrying an Adam update over earlier-finished parameters
+    "tspm_conv_bwd_adam": (c_int32, [_P] * 8 + [c_int32, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_apply_maxpool": (c_int32, [c_int32] * 4 + [_P] * 5 + [c_int32, c_float, _P, _P, _P, c_int32, c_int32, _P]),
     "tspm_bn_bwd_src": (c_int32, [c_int64, c_int32, POINTER(BnGSrc)] + [_P] * 17 + [c_size_t, _P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),

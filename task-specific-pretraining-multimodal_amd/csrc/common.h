@@ -40,6 +40,49 @@ TSPM_DEV bool tspm_dropout_keep(uint64_t base, long long i, float p) {
 }
 
 // nn.ReLU / F.relu: clamp_min(x, 0), which propagates NaN (fmaxf would return 0 for a NaN input)
+// Adam (torch.optim.Adam, L2 weight decay folded into the gradient): the per-launch constants and the element
+// update, shared by k_adam (misc.hip) and the weight-gradient epilogues that apply it (conv_lds.hip), so both
+// forms give bitwise the same parameters and moments.  1-beta2 and the bias corrections are formed in double and
+// rounded to fp32 once, as ATen does.
+struct AdamConsts {
+  float step_size, bc2s, w1, b2, omb2, eps, wd, gs;
+};
+TSPM_DEV AdamConsts adam_consts(const tspm_adam_hyper* hp) {
+  const tspm_adam_hyper h = *hp;
+  const double bc1 = 1.0 - pow(h.beta1, (double)h.step);
+  const double bc2 = 1.0 - pow(h.beta2, (double)h.step);
+  AdamConsts c;
+  c.step_size = (float)(h.lr / bc1);
+  c.bc2s = (float)sqrt(bc2);
+  c.w1 = (float)(1.0 - h.beta1);
+  c.b2 = (float)h.beta2;
+  c.omb2 = (float)(1.0 - h.beta2);
+  c.eps = (float)h.eps;
+  c.wd = (float)h.weight_decay;
+  c.gs = (float)h.grad_scale;
+  return c;
+}
+// adam_consts held in scalar registers (every lane computes the same values)
+TSPM_DEV AdamConsts adam_consts_uniform(const tspm_adam_hyper* hp) {
+  AdamConsts c = adam_consts(hp);
+  auto u = [](float f) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(f))); };
+  c.step_size = u(c.step_size); c.bc2s = u(c.bc2s); c.w1 = u(c.w1); c.b2 = u(c.b2);
+  c.omb2 = u(c.omb2); c.eps = u(c.eps); c.wd = u(c.wd); c.gs = u(c.gs);
+  return c;
+}
+// g' = g * grad_scale [* clip]; g' += wd * p; m = lerp(m, g', 1-beta1); v = beta2 v + (1-beta2) g'^2;
+// p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps)
+TSPM_DEV void adam_update(float& pp, float gg, float& mm, float& vv, const AdamConsts& c, bool clip, float cc) {
+  gg = gg * c.gs;
+  if (clip) gg = gg * cc;
+  if (c.wd != 0.f) gg = gg + c.wd * pp;
+  mm = mm + c.w1 * (gg - mm);
+  vv = vv * c.b2;
+  vv = vv + c.omb2 * gg * gg;
+  const float denom = sqrtf(vv) / c.bc2s + c.eps;
+  pp = pp + (-c.step_size) * (mm / denom);
+}
+
 TSPM_DEV float relu_f(float v) { return v > 0.f ? v : (v != v ? v : 0.f); }
 TSPM_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 TSPM_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }

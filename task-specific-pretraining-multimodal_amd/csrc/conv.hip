@@ -594,7 +594,7 @@ bool algo_supported(const Algo& a) {
   } while (0)
 
 ConvArgs make_args(const tspm_conv_shape* s) {
-  ConvArgs g;
+  ConvArgs g{};
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = (long long)s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
@@ -835,8 +835,21 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
                              tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
-  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, ws_d, ws_d_bytes, ws_w, ws_w_bytes,
-                        static_cast<hipStream_t>(stream));
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, nullptr, ws_d, ws_d_bytes, ws_w,
+                        ws_w_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int tspm_conv_bwd_adam(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                                  const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
+                                  int32_t beta, float* dw, const tspm_adam_job* job, void* ws_d, size_t ws_d_bytes,
+                                  void* ws_w, size_t ws_w_bytes, tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !job) return TSPM_ERR_INVALID;
+  if (job->count < 0 || job->blocks < 0 || (job->count > 0 && (!job->param || !job->grad || !job->exp_avg ||
+                                                               !job->exp_avg_sq || !job->hyper || job->blocks < 1)))
+    return TSPM_ERR_INVALID;
+  if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, job->count > 0 ? job : nullptr, ws_d,
+                        ws_d_bytes, ws_w, ws_w_bytes, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs,

@@ -243,8 +243,8 @@ struct LdsImpl {
                size_t ws_bytes, hipStream_t st);
   bool (*bwd_built)(const LdsAlgo& ad, const LdsAlgo& aw);
   int (*bwd)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
-             const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-             hipStream_t st);
+             const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, void* wsd, size_t wsd_bytes,
+             void* wsw, size_t wsw_bytes, hipStream_t st);
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();

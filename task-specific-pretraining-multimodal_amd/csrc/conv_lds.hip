@@ -774,14 +774,56 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_wgrad_lds(ConvArgs g
 // wgx x wgy x splits), the rest the data-gradient tiles.  The branch is workgroup-uniform; each
 // body is the standalone kernel's, so results are bitwise those of the two separate launches.
 // =============================================================================================
+// An Adam update carried by a backward launch (tspm_conv_bwd_adam, ABI 20): `blocks` extra workgroups of the grid
+// run k_adam's element loop (adam_consts / adam_update: bitwise tspm_adam_step) over `count` elements of the flat
+// buffers — parameters an earlier backward launch finished — beside the launch's latency-bound GEMM tiles.
+struct AdamJobArgs {
+  float* p;
+  const float* g;
+  float *m, *v;
+  long long count;
+  const tspm_adam_hyper* h;
+};
+TSPM_DEV void adam_job_body(const AdamJobArgs& a, int blk, int blocks) {
+  const AdamConsts c = adam_consts_uniform(a.h);
+  const long long n4 = a.count >> 2;
+  for (long long i = (long long)blk * kBlock + threadIdx.x; i < n4; i += (long long)blocks * kBlock) {
+    f32x4 pp = ld4(a.p + 4 * i), gg = ld4(a.g + 4 * i), mm = ld4(a.m + 4 * i), vv = ld4(a.v + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // element copies, as k_adam
+      float a = pp[j], b = mm[j], cc = vv[j];
+      adam_update(a, gg[j], b, cc, c, false, 1.f);
+      pp[j] = a; mm[j] = b; vv[j] = cc;
+    }
+    st4(a.p + 4 * i, pp);
+    st4(a.m + 4 * i, mm);
+    st4(a.v + 4 * i, vv);
+  }
+  if (blk == 0 && threadIdx.x < (a.count & 3)) {
+    const long long i = (n4 << 2) + threadIdx.x;
+    float pp = a.p[i], mm = a.m[i], vv = a.v[i];
+    adam_update(pp, a.g[i], mm, vv, c, false, 1.f);
+    a.p[i] = pp;
+    a.m[i] = mm;
+    a.v[i] = vv;
+  }
+}
+
 template <class CD, class CW>
 __global__ __launch_bounds__(kBlock, (min_waves2<CD, CW>())) void k_bwd_lds(ConvArgs gd, const float* __restrict__ dy,
                                                      const float* __restrict__ w, float* __restrict__ dx,
                                                      float* __restrict__ slabs_d, int dgx, int dgy, ConvArgs gw,
                                                      const float* __restrict__ x, float* __restrict__ dw,
-                                                     float* __restrict__ slabs_w, int wgx, int wgy) {
+                                                     float* __restrict__ slabs_w, int wgx, int wgy, AdamJobArgs aj,
+                                                     int naj) {
   extern __shared__ float lds[];
-  int b = gd.xcd == 1 ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int nconv = (int)gridDim.x - naj;
+  if ((int)blockIdx.x < naj) {  // the carried Adam update: the first naj workgroups, dispatched ahead of the tiles
+    adam_job_body(aj, (int)blockIdx.x, naj);
+    return;
+  }
+  const int b0 = (int)blockIdx.x - naj;
+  int b = gd.xcd == 1 ? xcd_swizzle(b0, nconv) : b0;
   const int nw = wgx * wgy * gw.splits;
   if (b < nw) {
     const int z = b / (wgx * wgy);
@@ -842,7 +884,7 @@ int acquire_enabled() {
 }
 
 ConvArgs args_of(const tspm_conv_shape* s) {
-  ConvArgs g;
+  ConvArgs g{};
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
@@ -1031,12 +1073,14 @@ struct BwdLaunch {
   int dgx, dgy, wgx, wgy;
   size_t lds;
   hipStream_t st;
+  AdamJobArgs aj;
+  int naj;
 };
 template <class CD, class CW>
 void bwd_go(const BwdLaunch& L) {
-  const int nblk = L.wgx * L.wgy * L.gw.splits + L.dgx * L.dgy * L.gd.splits;
+  const int nblk = L.wgx * L.wgy * L.gw.splits + L.dgx * L.dgy * L.gd.splits + L.naj;
   hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kBlock), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
-                     L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy);
+                     L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy, L.aj, L.naj);
 }
 bool is_cfg(const LdsAlgo& a, int tm, int wm, int wn, int wk) {
   return a.tm == tm && a.tn == 1 && a.wm == wm && a.wn == wn && a.wk == wk;
@@ -1071,8 +1115,8 @@ bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
 bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(ad, aw, nullptr); }
 
 int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
-            const float* w, float* dx, int beta, float* dw, void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes,
-            hipStream_t st) {
+            const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, void* wsd, size_t wsd_bytes,
+            void* wsw, size_t wsw_bytes, hipStream_t st) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
   if (!slab_fits(ad.splits, (long long)s->h * s->w * s->n, s->c) ||
       !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
@@ -1104,6 +1148,10 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
   if ((ad.splits > 1 && (size_t)L.dgx * L.dgy > cmax) || (aw.splits > 1 && (size_t)L.wgx * L.wgy > cmax))
     return TSPM_ERR_INVALID;
   L.dy = dy; L.w = w; L.x = x; L.dx = dx; L.dw = dw;
+  if (adam) {
+    L.aj = AdamJobArgs{adam->param, adam->grad, adam->exp_avg, adam->exp_avg_sq, (long long)adam->count, adam->hyper};
+    L.naj = adam->blocks;
+  }
   L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)));
   L.st = st;
   bwd_dispatch(ad, aw, &L);

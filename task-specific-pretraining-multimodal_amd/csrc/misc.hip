@@ -372,34 +372,12 @@ __global__ __launch_bounds__(256) void k_adam(long long count, float* __restrict
                                               float* __restrict__ m, float* __restrict__ v,
                                               const tspm_adam_hyper* __restrict__ hp,
                                               const float* __restrict__ clip) {
-  __shared__ float sh[8];
-  if (threadIdx.x == 0) {
-    const tspm_adam_hyper h = *hp;
-    const double bc1 = 1.0 - pow(h.beta1, (double)h.step);
-    const double bc2 = 1.0 - pow(h.beta2, (double)h.step);
-    sh[0] = (float)(h.lr / bc1);          // step_size
-    sh[1] = (float)sqrt(bc2);             // bias_correction2_sqrt
-    sh[2] = (float)(1.0 - h.beta1);       // lerp weight
-    sh[3] = (float)h.beta2;
-    sh[4] = (float)(1.0 - h.beta2);
-    sh[5] = (float)h.eps;
-    sh[6] = (float)h.weight_decay;
-    sh[7] = (float)h.grad_scale;
-  }
+  __shared__ AdamConsts sh;
+  if (threadIdx.x == 0) sh = adam_consts(hp);
   __syncthreads();
-  const float step_size = sh[0], bc2s = sh[1], w1 = sh[2], b2 = sh[3], omb2 = sh[4], eps = sh[5], wd = sh[6],
-              gs = sh[7];
+  const AdamConsts c = sh;
   const float cc = clip ? clip[0] : 1.f;
-  auto upd = [&](float& pp, float gg, float& mm, float& vv) {
-    gg = gg * gs;
-    if (clip) gg = gg * cc;
-    if (wd != 0.f) gg = gg + wd * pp;
-    mm = mm + w1 * (gg - mm);
-    vv = vv * b2;
-    vv = vv + omb2 * gg * gg;
-    const float denom = sqrtf(vv) / bc2s + eps;
-    pp = pp + (-step_size) * (mm / denom);
-  };
+  auto upd = [&](float& pp, float gg, float& mm, float& vv) { adam_update(pp, gg, mm, vv, c, clip != nullptr, cc); };
   const long long n4 = count >> 2;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     f32x4 pp = ld4(p + 4 * i), gg = ld4(g + 4 * i), mm = ld4(m + 4 * i), vv = ld4(v + 4 * i);

@@ -144,6 +144,9 @@ class EncoderEngine:
         # launch less at the tail of each encoder's forward
         self.fuse_pool = True
         self.debug_hook = None  # optional: fn(name, tensor) called with backward intermediates (diagnostics)
+        # optional step.AdamCarry: the single-GPU train step's Adam updates of finished blocks carried by later
+        # backward launches (tspm_conv_bwd_adam, ABI 20); None = every update by the optimizer's own launches
+        self.adam_carry = None
         # the pooling backwards folded into the adjacent BN backward (tspm_bn_bwd_src, round 5); TSPM_BN_POOL_SRC=0
         # restores the separate tspm_avgpool_bwd / tspm_maxpool_bwd launches for A/B
         self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
@@ -470,7 +473,7 @@ class EncoderEngine:
             self.conv_timer.end()
 
     def _bwd_pair(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, dx: torch.Tensor, beta: int,
-                  sh: int) -> bool:
+                  sh: int, carry_share: float = 0.0) -> bool:
         """Input and weight gradient of ``op`` in one launch (tspm_conv_bwd: the two GEMMs read the same
         dy and are independent, so their workgroups share the grid).  False (nothing launched) when the
         pair is not built in or the tuner found the two separate launches faster; the caller then launches
@@ -486,10 +489,18 @@ class EncoderEngine:
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
         if self.conv_timer:
             self.conv_timer.begin(op, "bwd")
-        L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
-                                  x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
-                                  beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
-                                  self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
+        job = self.adam_carry.take(carry_share) if self.adam_carry is not None else None
+        if job is not None:  # an Adam update over earlier-finished parameters rides on this launch (ABI 20)
+            L.check(lib.tspm_conv_bwd_adam(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
+                                           ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides), dy.data_ptr(),
+                                           self._w(op).data_ptr(), dx.data_ptr(), beta, gw.data_ptr(), ctypes.byref(job),
+                                           self.ws_conv.data_ptr(), self.ws_conv_bytes, self.ws_conv2.data_ptr(),
+                                           self.ws_conv_bytes, sh), "conv_bwd_adam")
+        else:
+            L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
+                                      x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
+                                      beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
+                                      self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
         if self.conv_timer:
             self.conv_timer.end()
         return True
@@ -502,6 +513,12 @@ class EncoderEngine:
                                         self.ws_conv_bytes, sh), "conv_dgrad")
         if self.conv_timer:
             self.conv_timer.end()
+
+    def block_params(self, bp: "BlockPlan") -> List[torch.nn.Parameter]:
+        ms = [bp.conv1.module, bp.bn1.module, bp.conv2.module, bp.bn2.module]
+        if bp.ds_conv is not None:
+            ms += [bp.ds_conv.module, bp.ds_bn.module]
+        return [p for m in ms for p in m.parameters(recurse=False)]
 
     def phase_params(self, phase: int) -> List[torch.nn.Parameter]:
         """Parameters whose gradients backward phase `phase` (1 or 2) writes: phase 1 = fc and the
@@ -539,6 +556,8 @@ class EncoderEngine:
                        fc.weight.data_ptr(), self._grad(fc.weight).data_ptr(),
                        self._grad(fc.bias).data_ptr() if fc.bias is not None else None, self.g_pooled.data_ptr(),
                        self.final_c, sh)
+            if self.adam_carry is not None:
+                self.adam_carry.ready([p for p in fc.parameters()])
             h, w = self.final_hw
             G, Gn = self.gA, self.gB
             # the last BN reads the average pool's gradient directly (no broadcast tensor) unless a debug hook
@@ -579,7 +598,7 @@ class EncoderEngine:
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
-            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh):
+            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, carry_share=0.5):
                 self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh)
                 self._dgrad(bp.conv2, d2, da1, 0, sh)
             d1 = bp.g_y1
@@ -594,9 +613,11 @@ class EncoderEngine:
                 self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             # conv1's input gradient accumulates last onto the previous block's output gradient
-            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh):
+            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, carry_share=1.0):
                 self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
                 self._dgrad(bp.conv1, d1, Gnv, 1, sh)
+            if self.adam_carry is not None:  # this block's parameters are final and read by no later launch
+                self.adam_carry.ready(self.block_params(bp))
             G, Gn = Gn, G
         if phase == 1:
             self._bw_state = (G, Gn)

@@ -19,7 +19,7 @@ from __future__ import annotations
 import contextlib
 import os
 import time
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -109,6 +109,77 @@ def fused_step_supported(model, optimizer, loss_functions, A: torch.Tensor, I: t
     return A.shape[0] == I.shape[0]
 
 
+class AdamCarry:
+    """Adam updates carried by an encoder's later backward launches (tspm_conv_bwd_adam, ABI 20).
+
+    The backward visits the blocks from the last to the first.  When a block is done its parameters (and, first,
+    the fc's) are final and no later launch reads them (``ready``); the next fused dgrad + wgrad launches then carry
+    their Adam update as extra workgroups of the same grid (``take``: conv2's launch half of what is pending,
+    conv1's the rest), overlapping the latency-bound GEMM tiles instead of following the backward.  Parameters
+    are visited in descending flat-buffer order, so what is pending is one contiguous element range of the
+    (single) flat group; ``carried`` lists the issued ranges — the caller updates the rest with launch_ranges.
+    Bitwise the one-launch update (Adam is element-wise; the carried loop is tspm_adam_step's)."""
+
+    def __init__(self, opt, max_blocks: int = 512, elems_per_block: int = 8192):
+        fgs = opt.flat_groups()
+        self.fg = fgs[0] if len(fgs) == 1 else None
+        self.where = {}
+        if self.fg is not None:
+            from .optim import _ALIGN
+            for p, o in zip(self.fg.params, self.fg.offsets):
+                self.where[id(p)] = (o, o + (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN)
+        self.lo = self.hi = None  # pending [lo, hi)
+        self.carried: List[Tuple[int, int]] = []
+        self.max_blocks = max_blocks
+        self.elems_per_block = elems_per_block
+
+    def ready(self, params) -> None:
+        spans = [self.where.get(id(p)) for p in params]
+        if not spans or any(sp is None for sp in spans):
+            return
+        a, b = min(sp[0] for sp in spans), max(sp[1] for sp in spans)
+        if self.lo is None:
+            self.lo, self.hi = a, b
+        elif b == self.lo:
+            self.lo = a
+        # anything else (not adjacent) stays with the caller's own launches
+
+    def take(self, share: float):
+        if self.lo is None or share <= 0:
+            return None
+        n = self.hi - self.lo
+        k = n if share >= 1 else min(n, (int(n * share) + 3) // 4 * 4)
+        if k <= 0:
+            return None
+        a, b = self.hi - k, self.hi
+        self.hi = a
+        if self.hi <= self.lo:
+            self.lo = self.hi = None
+        self.carried.append((a, b))
+        fg = self.fg
+        blocks = max(1, min(self.max_blocks, -(-k // self.elems_per_block)))
+        return L.AdamJob(fg.param[a:].data_ptr(), fg.grad[a:].data_ptr(), fg.exp_avg[a:].data_ptr(),
+                         fg.exp_avg_sq[a:].data_ptr(), k, fg.hyper.data_ptr(), blocks, 0)
+
+    def rest_of(self, ranges):
+        """``ranges`` (per group, list of [a, b)) minus the carried ranges."""
+        if self.fg is None or not self.carried:
+            return ranges
+        out = []
+        cut = sorted(self.carried)
+        for a, b in ranges[0]:
+            cur = a
+            for c, d in cut:
+                if d <= cur or c >= b:
+                    continue
+                if c > cur:
+                    out.append((cur, c))
+                cur = max(cur, d)
+            if cur < b:
+                out.append((cur, b))
+        return [out] + list(ranges[1:])
+
+
 class FusedTrainStep:
     def __init__(self, model, optimizer: FusedAdam, loss_functions, batch: int, audio_hw=(32, 94), image_hw=(28, 28),
                  use_graph: bool = True, allreduce=None, adam_split=True):
@@ -170,6 +241,11 @@ class FusedTrainStep:
         # head + image backward + image Adam).  A/B, alternating processes: 2.5907 vs 2.6280 ms (56,000 bytes:
         # 2.613 vs 2.630), profiles/r5/r5i_floor*.json.  TSPM_SLACK_LDS_FLOOR=0 restores the unconstrained launches
         self.slack_lds_floor = int(os.environ.get("TSPM_SLACK_LDS_FLOOR", "82000"))
+        # Adam updates of finished blocks carried by the later backward launches of "image" / "audio" / "both"
+        # encoders (AdamCarry; single-GPU split schedule only); "none" = the optimizer's own launches.  A/B,
+        # alternating processes (profiles/r5/r5n-r5p): both 2.5526 vs 2.5931 ms with 512 carrying workgroups of
+        # 8,192 elements (256 x 16,384: 2.5571 vs 2.5933; image only: 2.5692 vs 2.5965)
+        self.adam_carry = os.environ.get("TSPM_ADAM_CARRY", "both")
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         # single-GPU step (adam_split): each encoder's parameters updated by Adam on that encoder's stream right
@@ -254,12 +330,24 @@ class FusedTrainStep:
             # each encoder's parameters on its own stream at its chain's end, the head's with the audio encoder's
             # (the increment on the image stream and main joining it before the audio + head ranges, with
             # num_batches_tracked moved to the image stream's start: 2.614 vs 2.595 ms, profiles/r4/r4q_ab_lean.json)
+            kw = dict(max_blocks=int(os.environ.get("TSPM_ADAM_CARRY_BLOCKS", "512")),
+                      elems_per_block=int(os.environ.get("TSPM_ADAM_CARRY_ELEMS", "8192")))
+            ci = AdamCarry(self.opt, **kw) if self.adam_carry in ("image", "both") else None
+            ca = AdamCarry(self.opt, **kw) if self.adam_carry in ("audio", "both") else None
             with torch.cuda.stream(side):
-                self.eng_i.backward(self.dfused[:, ea:], self.F)
-                self.opt.launch_ranges(side.cuda_stream, img)
+                self.eng_i.adam_carry = ci
+                try:
+                    self.eng_i.backward(self.dfused[:, ea:], self.F)
+                finally:
+                    self.eng_i.adam_carry = None
+                self.opt.launch_ranges(side.cuda_stream, ci.rest_of(img) if ci else img)
             with self._slack_floor():
-                self.eng_a.backward(self.dfused, self.F)
-            self.opt.launch_ranges(main.cuda_stream, rest)
+                self.eng_a.adam_carry = ca
+                try:
+                    self.eng_a.backward(self.dfused, self.F)
+                finally:
+                    self.eng_a.adam_carry = None
+            self.opt.launch_ranges(main.cuda_stream, ca.rest_of(rest) if ca else rest)
         else:
             with torch.cuda.stream(side):
                 self.eng_i.backward(self.dfused[:, ea:], self.F)

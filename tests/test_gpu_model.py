@@ -367,17 +367,21 @@ def test_pretrained_config_param_groups_run_fused_step(gpu, tmp_path):
     assert torch.equal(res[0], res[1])
 
 
-def test_audio_lds_floor_leaves_the_step_bitwise_unchanged(gpu, monkeypatch):
-    """The audio encoder's LDS floor (TSPM_SLACK_LDS_FLOOR, the default 82,000 bytes vs 0) changes only how many
-    workgroups share a CU: four replayed steps' parameters, BN buffers and Adam moments are bitwise unchanged."""
+@pytest.mark.parametrize("knob,values", [("TSPM_SLACK_LDS_FLOOR", ("0", "82000")),
+                                         ("TSPM_ADAM_CARRY", ("none", "image")),
+                                         ("TSPM_ADAM_CARRY", ("none", "both"))])
+def test_step_schedules_leave_the_step_bitwise_unchanged(gpu, monkeypatch, knob, values):
+    """Scheduling switches of the single-GPU step change no arithmetic: the audio encoder's LDS floor (only how
+    many workgroups share a CU) and the Adam updates carried by later backward launches (tspm_conv_bwd_adam:
+    tspm_adam_step's element loop over the finished blocks' ranges) — four replayed steps' parameters, BN buffers
+    and Adam moments are bitwise those of the plain schedule."""
     results = []
-    for floor in ("0", "82000"):
-        monkeypatch.setenv("TSPM_SLACK_LDS_FLOOR", floor)
+    for val in values:
+        monkeypatch.setenv(knob, val)
         torch.manual_seed(17)
         ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
         opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
         st = tspm_amd.FusedTrainStep(ours, opt, None, 32)
-        assert st.slack_lds_floor == int(floor)
         for i in range(4):
             audio, image, labels, _ = orc.synthetic_batch(32, seed=40 + i)
             st.step(audio.to(gpu), image.to(gpu), labels.to(gpu))
