@@ -41,7 +41,8 @@ enum {
  * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles;
  * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward, and
  * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch, and tspm_set_conv_lds_floor;
- * 20 = tspm_conv_bwd_adam, the fused backward launch carrying an Adam update over earlier-finished parameters). */
+ * 20 = tspm_conv_bwd_adam, the fused backward launch carrying an Adam update over earlier-finished parameters,
+ * and tspm_head_desc.adam_step). */
 #define TSPM_ABI_VERSION 20
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
@@ -394,6 +395,9 @@ typedef struct tspm_head_desc {
   float *h1, *hh, *logits, *dlogits, *dz3, *dz0, *dx, *row_ws;
   float *gw0, *gb0, *gw3, *gb3, *gw5, *gb5;
   float *loss, *stats;             /* stats nullable */
+  int64_t* adam_step;              /* nullable (ABI 20): the optimizer's tspm_adam_hyper.step, incremented once by
+                                    * launch 2 after launch 1 read `counter` (tspm_adam_begin's job, one launch fewer
+                                    * between the forward and the backward) */
 } tspm_head_desc;
 int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t stream);
 

@@ -82,12 +82,12 @@ class LinearBwdDesc(Structure):
 
 
 class HeadDesc(Structure):
-    """tspm_head_desc (ABI 16): the AVMNIST fusion head's train step in two launches."""
+    """tspm_head_desc (ABI 16; adam_step ABI 20): the AVMNIST fusion head's train step in two launches."""
     _fields_ = [(n, c_int32) for n in ("n", "in_", "hidden", "hidden2", "classes", "ldx", "lddx", "gen_keep")] + \
         [(n, c_void_p) for n in ("x", "w0", "b0", "w3", "b3", "w5", "b5")] + \
         [("p", c_float), ("loss_weight", c_float), ("seed", c_uint64)] + \
         [(n, c_void_p) for n in ("counter", "keep", "labels", "h1", "hh", "logits", "dlogits", "dz3", "dz0", "dx",
-                                 "row_ws", "gw0", "gb0", "gw3", "gb3", "gw5", "gb5", "loss", "stats")]
+                                 "row_ws", "gw0", "gb0", "gw3", "gb3", "gw5", "gb5", "loss", "stats", "adam_step")]
 
 
 # name -> (restype, argtypes)

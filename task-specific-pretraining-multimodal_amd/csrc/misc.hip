@@ -1095,6 +1095,7 @@ __global__ __launch_bounds__(64 * WK) void k_head_wgrad(GemmMulti mp, int total,
   if (threadIdx.x == 0) {
     const float l = (float)(red[0] / (double)d.n);
     d.loss[0] = l * d.loss_weight;
+    if (d.adam_step) d.adam_step[0] += 1;  // after launch 1 read the step counter (dropout), before any Adam launch
     if (d.stats) {
       d.stats[0] += (float)red[0];
       d.stats[1] += (float)red[T];

@@ -259,6 +259,7 @@ class FusedTrainStep:
         self.exchange_probe: Optional[list] = None
         self._split_ranges = None
         self._graph_gen_keep = True
+        self._head_bumps_step = False
         self.calls = 0
         self._sig = (id(optimizer), id(loss_functions), batch)
         # dropout RNG counter = FusedAdam's device step counter (distinct per step, graph-safe)
@@ -288,7 +289,8 @@ class FusedTrainStep:
                        dlogits=g(self.dlogits), dz3=g(self.dh), dz0=g(self.dh1), dx=g(self.dfused), row_ws=g(self.row_ws),
                        gw0=g(net[0].weight.grad), gb0=g(net[0].bias.grad), gw3=g(net[3].weight.grad),
                        gb3=g(net[3].bias.grad), gw5=g(net[5].weight.grad), gb5=g(net[5].bias.grad),
-                       loss=g(self.loss), stats=g(self.stats))
+                       loss=g(self.loss), stats=g(self.stats),
+                       adam_step=self._rng_ctr_ptr if self._head_bumps_step else None)
         L.check(L.lib().tspm_head_train_step(d, sh), "head_train_step")
 
     def _fwd_bwd(self, marks=None) -> None:
@@ -306,6 +308,10 @@ class FusedTrainStep:
             self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
         main.wait_stream(side)
         sh = main.cuda_stream
+        # the single-GPU split schedule with one flat group: the head's second launch advances the Adam step
+        # counter (tspm_head_desc.adam_step) instead of a tspm_adam_begin launch before the fork
+        self._head_bumps_step = (marks is None and self._split_opt() and len(self.opt.flat_groups()) == 1
+                                 and os.environ.get("TSPM_HEAD_BUMPS_STEP", "1") != "0")
         # (the head's weight-gradient launch on the image stream, beside the audio backward, was measured slower:
         # 2.604 vs 2.589 ms, profiles/r4/r4m2_ab_head.json)
         self._head(sh)
@@ -325,7 +331,8 @@ class FusedTrainStep:
                 self.eng_i.backward(None, self.F, phase=2)
         elif self._split_opt():
             img, rest = self._adam_ranges()
-            self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before every range
+            if not self._head_bumps_step:
+                self.opt.launch_begin(main.cuda_stream)  # one step-count increment, before every range
             side.wait_stream(main)
             # each encoder's parameters on its own stream at its chain's end, the head's with the audio encoder's
             # (the increment on the image stream and main joining it before the audio + head ranges, with
