@@ -240,11 +240,15 @@ class FusedTrainStep:
         # for the image chain, the replayed step's critical path (scripts/overlap_probe.py --dump: image forward +
         # head + image backward + image Adam).  A/B, alternating processes: 2.5907 vs 2.6280 ms (56,000 bytes:
         # 2.613 vs 2.630), profiles/r5/r5i_floor*.json.  TSPM_SLACK_LDS_FLOOR=0 restores the unconstrained launches
-        self.slack_lds_floor = int(os.environ.get("TSPM_SLACK_LDS_FLOOR", "82000"))
+        # At batch 1024 the floor costs 1.05 ms per step (10.84 vs 9.79 ms, profiles/r5/r5t_floor_b1024.json: the
+        # audio chain's large convs need their occupancy there) and at batch 32 it is neutral (2.6497 vs 2.6459 ms,
+        # r5u_floor_b32.json), so the default applies at batches 64-128 only
+        self.slack_lds_floor = int(os.environ.get("TSPM_SLACK_LDS_FLOOR", "82000" if 64 <= batch <= 128 else "0"))
         # Adam updates of finished blocks carried by the later backward launches of "image" / "audio" / "both"
         # encoders (AdamCarry; single-GPU split schedule only); "none" = the optimizer's own launches.  A/B,
         # alternating processes (profiles/r5/r5n-r5p): both 2.5526 vs 2.5931 ms with 512 carrying workgroups of
-        # 8,192 elements (256 x 16,384: 2.5571 vs 2.5933; image only: 2.5692 vs 2.5965)
+        # 8,192 elements (256 x 16,384: 2.5571 vs 2.5933; image only: 2.5692 vs 2.5965); batch 1024: 9.807 vs
+        # 9.866 ms (r5u_carry_b1024.json)
         self.adam_carry = os.environ.get("TSPM_ADAM_CARRY", "both")
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
