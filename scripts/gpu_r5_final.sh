@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round-5 evidence set on the committed tree, in two calls (each under gpurun's 20-minute limit):
-#   bash scripts/gpu_r4_final.sh suite TAG   smoke + the whole GPU suite
-#   bash scripts/gpu_r4_final.sh prof  TAG   the headline line + rocprofv3 stats / trace + PMC FETCH / WRITE passes
+#   bash scripts/gpu_r5_final.sh suite TAG   smoke + the whole GPU suite
+#   bash scripts/gpu_r5_final.sh prof  TAG   the headline line + rocprofv3 stats / trace + PMC FETCH / WRITE passes
 #                                            (scripts/prof_bench.sh), the MFMA-busy passes at batch 128 and 1024
-#                                            (scripts/pmc_mfma.sh), the other BASELINE configs' lines, --phased
+#                                            (scripts/pmc_mfma.sh)
+#   bash scripts/gpu_r5_final.sh lines TAG   the other BASELINE configs' lines, --phased
 # Each step has its own time limit; the script stops at the first failure.
 set -e
 cd $GRAFT_REPO_ROOT
@@ -15,10 +16,12 @@ if [ "$MODE" = "suite" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gpu_suite.log 2>&1
   exit 0
 fi
-bash scripts/prof_bench.sh $T
-bash scripts/pmc_mfma.sh ${T}_b128
-bash scripts/pmc_mfma.sh ${T}_b1024 --batch-per-rank 1024
-cd $GRAFT_REPO_ROOT
+if [ "$MODE" = "prof" ]; then
+  bash scripts/prof_bench.sh $T
+  bash scripts/pmc_mfma.sh ${T}_b128
+  bash scripts/pmc_mfma.sh ${T}_b1024 --batch-per-rank 1024
+  exit 0
+fi
 timeout -k 10 200 python -u bench.py --no-cpu-baseline --pcie-steps 0 --batch-per-rank 32 --steps 50 > gpurun_out/${T}_bench_b32.json 2> gpurun_out/${T}_b32.err
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --pcie-steps 0 --batch-per-rank 1024 --steps 20 --kernel-table gpurun_out/${T}_kernel_table_b1024.json > gpurun_out/${T}_bench_b1024.json 2> gpurun_out/${T}_b1024.err
 timeout -k 10 200 python -u bench.py --mono > gpurun_out/${T}_mono.json 2> gpurun_out/${T}_mono.err

@@ -2,8 +2,8 @@
 
     python scripts/roofline_from_trace.py gpurun_out/<tag>_prof/run_kernel_trace.csv [valid_tap_flop_per_step]
 
-A step = the dispatches between consecutive step-count increments (k_adam_begin, once per step: the Adam
-update runs as several range launches since round 4); traces without it split at k_adam.  Steps whose
+A step = the dispatches from one input gather (k_avmnist_gather, one per bench step) to the next; traces without
+gathers split at the step-count increment (k_adam_begin) or at k_adam.  Steps whose
 kernel count equals the modal count are the graph-replayed training steps; for those it prints the
 summed conv-kernel duration per step, the busy time (union of the conv kernels' intervals) and the
 resulting fractions of the fp32 MFMA peak, plus the per-family kernel time — the same quantities
@@ -51,13 +51,20 @@ def main(path, flops=FLOPS):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    mark = "k_adam_begin(" if any("k_adam_begin(" in n for _, _, n in rows) else "k_adam("
     steps, cur = [], []
-    for a, b, n in rows:
-        cur.append((a, b, n))
-        if mark in n:
-            steps.append(cur)
-            cur = []
+    if any("k_avmnist_gather" in n for _, _, n in rows):  # bench steps start at the input gather (round 5: the Adam
+        for a, b, n in rows:                               # step count is advanced inside the head's launch)
+            if "k_avmnist_gather" in n and cur:
+                steps.append(cur)
+                cur = []
+            cur.append((a, b, n))
+    else:
+        mark = "k_adam_begin(" if any("k_adam_begin(" in n for _, _, n in rows) else "k_adam("
+        for a, b, n in rows:
+            cur.append((a, b, n))
+            if mark in n:
+                steps.append(cur)
+                cur = []
     mode = Counter(len(s) for s in steps).most_common(1)[0][0]
     good = [s for s in steps if len(s) == mode]
     conv_sum = [sum(b - a for a, b, n in s if CONV.search(n)) / 1e6 for s in good]
