@@ -22,6 +22,7 @@ if [ "$MODE" = "prof" ]; then
   bash scripts/pmc_mfma.sh ${T}_b1024 --batch-per-rank 1024
   exit 0
 fi
+timeout -k 10 300 python -u bench.py --kernel-table gpurun_out/${T}_kernel_table.json > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err
 timeout -k 10 200 python -u bench.py --no-cpu-baseline --pcie-steps 0 --batch-per-rank 32 --steps 50 > gpurun_out/${T}_bench_b32.json 2> gpurun_out/${T}_b32.err
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --pcie-steps 0 --batch-per-rank 1024 --steps 20 --kernel-table gpurun_out/${T}_kernel_table_b1024.json > gpurun_out/${T}_bench_b1024.json 2> gpurun_out/${T}_b1024.err
 timeout -k 10 200 python -u bench.py --mono > gpurun_out/${T}_mono.json 2> gpurun_out/${T}_mono.err

@@ -36,7 +36,7 @@ from tspm_amd import engine as E  # noqa: E402
 from conv_bench import step_ops  # noqa: E402
 from tune_convs import Bufs, bwd_launcher, graph_time, launcher, lds_candidates  # noqa: E402
 
-B = 128
+B = int(os.environ.get("TUNE_BATCH", "128"))  # per-rank batch of the tuned step
 
 
 def build(table, dev):

@@ -244,6 +244,7 @@ class FusedTrainStep:
         # audio chain's large convs need their occupancy there) and at batch 32 it is neutral (2.6497 vs 2.6459 ms,
         # r5u_floor_b32.json), so the default applies at batches 64-128 only
         self.slack_lds_floor = int(os.environ.get("TSPM_SLACK_LDS_FLOOR", "82000" if 64 <= batch <= 128 else "0"))
+        self.slack_parts = os.environ.get("TSPM_SLACK_PARTS", "fb")  # the audio forward (f) and / or backward (b)
         # Adam updates of finished blocks carried by the later backward launches of "image" / "audio" / "both"
         # encoders (AdamCarry; single-GPU split schedule only); "none" = the optimizer's own launches.  A/B,
         # alternating processes (profiles/r5/r5n-r5p): both 2.5526 vs 2.5931 ms with 512 carrying workgroups of
@@ -308,7 +309,7 @@ class FusedTrainStep:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.eng_i.forward(self.I, self.fused[:, ea:], self.F, train=True, bump_batches_tracked=False)
-        with self._slack_floor():
+        with self._slack_floor("f"):
             self.eng_a.forward(self.A, self.fused, self.F, train=True, bump_batches_tracked=False)
         main.wait_stream(side)
         sh = main.cuda_stream
@@ -368,11 +369,11 @@ class FusedTrainStep:
         L.counters_add(self.nbt)
 
     @contextlib.contextmanager
-    def _slack_floor(self):
+    def _slack_floor(self, part: str = "b"):
         """The audio encoder's LDS-staged conv launches with a minimum LDS allocation (tspm_set_conv_lds_floor,
         TSPM_SLACK_LDS_FLOOR bytes), so fewer of its workgroups share a CU with the image chain
         (the replayed step's critical path, scripts/overlap_probe.py --dump)."""
-        floor = self.slack_lds_floor
+        floor = self.slack_lds_floor if part in self.slack_parts else 0
         if floor and not self.serial:
             L.check(L.lib().tspm_set_conv_lds_floor(floor), "set_conv_lds_floor")
         try:
