@@ -28,3 +28,56 @@ def test_fused_step_refuses_unsupported_head():
     a, i = torch.zeros(2, 32, 94), torch.zeros(2, 1, 28, 28)
     from tspm_amd.step import fused_step_supported
     assert not fused_step_supported(m, object.__new__(Opt), None, a, i)
+
+
+class _FakeGroup:
+    """A FusedAdam flat group's layout (offsets aligned to 4 floats) over CPU tensors: AdamCarry only reads
+    offsets, numels and data pointers."""
+    def __init__(self, params):
+        self.params, self.offsets, off = params, [], 0
+        for p in params:
+            self.offsets.append(off)
+            off += (p.numel() + 3) // 4 * 4
+        self.numel = off
+        self.param, self.grad, self.exp_avg, self.exp_avg_sq = (torch.zeros(off) for _ in range(4))
+        self.hyper = torch.zeros(8, dtype=torch.float64)
+
+
+class _FakeOpt:
+    def __init__(self, params):
+        self.g = _FakeGroup(params)
+
+    def flat_groups(self):
+        return [self.g]
+
+
+def test_adam_carry_ranges_partition_the_encoder():
+    """AdamCarry (step.py): blocks become ready in descending flat order; the carried jobs and rest_of() partition
+    the encoder's range exactly once, every job starts 16-byte aligned, and a non-adjacent ready set is left to
+    the optimizer's own launches."""
+    from tspm_amd.step import AdamCarry
+    torch.manual_seed(0)
+    params = [torch.zeros(int(n)) for n in torch.randint(1, 3000, (13,))]  # stem .. fc, in flat order
+    opt = _FakeOpt(params)
+    c = AdamCarry(opt, max_blocks=7, elems_per_block=1000)
+    blocks = [params[0:2], params[2:5], params[5:8], params[8:11], params[11:13]]  # last = "fc"
+    base = opt.g.param.data_ptr()
+    jobs = []
+    c.ready(blocks[-1])
+    for b in reversed(blocks[:-1]):
+        for share in (0.5, 1.0):
+            j = c.take(share)
+            if j is not None:
+                jobs.append(j)
+                assert (j.param - base) % 16 == 0 and 1 <= j.blocks <= 7 and j.count > 0
+        c.ready(b)
+    c.ready([params[12]])  # already carried: not adjacent to what is pending -> ignored
+    cover = torch.zeros(opt.g.numel, dtype=torch.int32)
+    for a, b in c.carried:
+        cover[a:b] += 1
+    for a, b in c.rest_of([[(0, opt.g.numel)]])[0]:
+        cover[a:b] += 1
+    assert bool((cover == 1).all())
+    assert sum(j.count for j in jobs) == sum(b - a for a, b in c.carried)
+    # the first block (stem side) is never carried: nothing runs after it
+    assert c.carried and min(a for a, _ in c.carried) >= opt.g.offsets[2]
