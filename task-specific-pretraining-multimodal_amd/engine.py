@@ -152,6 +152,10 @@ class EncoderEngine:
         self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
         # the stem's BN apply + ReLU + max pool forward in one launch (A/B switch TSPM_STEM_FUSE=0)
         self.stem_fuse = os.environ.get("TSPM_STEM_FUSE", "1") != "0"
+        # the encoder fc forward (K = 512, 8-16 output tiles) split 8 ways over K: 2.4399 vs 2.4474 ms per step
+        # (A/B, profiles/r5/r5fc_*); TSPM_FC_SPLITS=1 restores the one-launch product
+        self.fc_splits = int(os.environ.get("TSPM_FC_SPLITS", "8"))
+        self._fc_ws = None
         N = batch
         f32 = dict(device=device, dtype=torch.float32)
         c1 = encoder.conv1
@@ -420,9 +424,19 @@ class EncoderEngine:
             L.check(lib.tspm_avgpool_fwd(h * w, N, self.final_c, xin.data_ptr(), self.pooled.data_ptr(), sh),
                     "avgpool_fwd")
         fc = self.enc.fc
-        L.check(lib.tspm_linear_fwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
-                                    fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb, sh),
-                "linear_fwd(fc)")
+        ks = self.fc_splits
+        if ks > 1:  # split-K fc forward (partials + one reduce launch; A/B switch TSPM_FC_SPLITS)
+            need = lib.tspm_linear_fwd_splitk_workspace(N, self.final_c, self.hidden, ks)
+            if self._fc_ws is None or self._fc_ws.numel() < need:
+                self._fc_ws = torch.empty(max(need, 16), dtype=torch.uint8, device=self.device)
+            L.check(lib.tspm_linear_fwd_splitk(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
+                                               fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(),
+                                               ld_emb, ks, self._fc_ws.data_ptr(), self._fc_ws.numel(), sh),
+                    "linear_fwd_splitk(fc)")
+        else:
+            L.check(lib.tspm_linear_fwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c,
+                                        fc.weight.data_ptr(), L.ptr(fc.bias), 0, None, 1.0, emb.data_ptr(), ld_emb,
+                                        sh), "linear_fwd(fc)")
 
     # ---------------------------------------------------------------------------------------
     def _grad(self, p: torch.Tensor) -> torch.Tensor:
