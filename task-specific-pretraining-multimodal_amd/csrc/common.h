@@ -188,6 +188,27 @@ TSPM_DEV bool last_arriver(unsigned* cnt, unsigned total, int* flag, bool acquir
 //
 // bn_merge_range is the merge itself over tiles [g_lo, g_hi) of a partial array with G_all tiles:
 // returns (in the threads with t < CB) the range's mean and sum of squared deviations in double.
+// Fixed-order sum of v over the GG = T / CB threads that share channel slot t % CB (CB a power of two);
+// the result is valid in threads t < CB.  Within a wave the slots' copies are folded by xor butterflies
+// (CB < 64: lanes l and l ^ o, o = CB .. 32, hold the same slot), then the waves' (or, for CB >= 64, the
+// threads') partials are added in index order through `red` — one barrier instead of log2(GG).
+TSPM_DEV double bn_group_sum(double v, int t, int CB, int T, double* red) {
+  int parts;
+  if (CB < 64) {
+    for (int o = CB; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    if ((t & 63) < CB) red[(t >> 6) * CB + (t & 63)] = v;
+    parts = T >> 6;
+  } else {
+    red[t] = v;
+    parts = T / CB;
+  }
+  __syncthreads();
+  double r = 0.0;
+  if (t < CB)
+    for (int j = 0; j < parts; ++j) r += red[j * CB + t];
+  return r;
+}
+
 template <bool SC1 = false>  // SC1: the partials are an in-launch hand-off read with ld_sc1
 TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const float* part, int g_lo, int g_hi,
                              int c0, int CB, double* red, double* smu, double& mean_out, double& m2_out,
@@ -208,62 +229,48 @@ TSPM_DEV void bn_merge_range(long long M, int C, int G_all, long long rpt, const
   // they miss in cache, so issue them together).  The loads are unconditional — tiles past g_hi re-read
   // tile g_hi-1 and get weight 0 — because a load under `if (g < g_hi)` made the compiler wait for each
   // tile's loads before issuing the next (vmcnt(0)/(1) after every tile: 11.9 us for the audio stem's
-  // 3,008-tile merge)
+  // 3,008-tile merge).  When the whole range is one batch per thread (every layer but the audio stem's),
+  // the three planes are loaded once and the second pass runs from registers.
+  const bool one = g_hi - g_lo <= 8 * GG;
+  float k0[8], k1[8], k2[8];
+  auto load = [&](int g0, bool m2) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long o = (long long)min(g0 + u * GG, g_hi - 1) * C + c;
+      k0[u] = ld(part + o);
+      k1[u] = ld(part + plane + o);
+      if (m2) k2[u] = ld(part + 2 * plane + o);
+    }
+  };
+  auto nb_of = [&](int g) -> double { return g < g_hi ? (double)min(rpt, M - (long long)g * rpt) : 0.0; };
   double s = 0.0;
   if (cok)
     for (int g0 = g_lo + gg; g0 < g_hi; g0 += 8 * GG) {
-      float k0[8], k1[8];
+      load(g0, one);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const long long o = (long long)min(g0 + u * GG, g_hi - 1) * C + c;
-        k0[u] = ld(part + o);
-        k1[u] = ld(part + plane + o);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int g = g0 + u * GG;
-        const double nb = g < g_hi ? (double)min(rpt, M - (long long)g * rpt) : 0.0;
-        s += nb * ((double)k0[u] + (double)k1[u]);
-      }
+      for (int u = 0; u < 8; ++u) s += nb_of(g0 + u * GG) * ((double)k0[u] + (double)k1[u]);
     }
-  red[t] = s;
-  __syncthreads();
-  for (int w = GG >> 1; w > 0; w >>= 1) {
-    if (gg < w) red[t] += red[t + w * CB];
-    __syncthreads();
-  }
-  if (gg == 0) smu[cl] = red[cl] / (double)n_rows;
+  s = bn_group_sum(s, t, CB, T, red);
+  if (t < CB) smu[cl] = s / (double)n_rows;
   __syncthreads();
   const double mean = smu[cl];
   double q = 0.0;
   if (cok)
     for (int g0 = g_lo + gg; g0 < g_hi; g0 += 8 * GG) {
-      float k0[8], k1[8], k2[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const long long o = (long long)min(g0 + u * GG, g_hi - 1) * C + c;
-        k0[u] = ld(part + o);
-        k1[u] = ld(part + plane + o);
-        k2[u] = ld(part + 2 * plane + o);
-      }
+      if (!one) load(g0, true);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int g = g0 + u * GG;
         if (g < g_hi) {
-          const double nb = (double)min(rpt, M - (long long)g * rpt);
+          const double nb = nb_of(g);
           const double mb = (double)k0[u] + (double)k1[u];
           q += (double)k2[u] + nb * (mb - mean) * (mb - mean);
         }
       }
     }
-  red[t] = q;
-  __syncthreads();
-  for (int w = GG >> 1; w > 0; w >>= 1) {
-    if (gg < w) red[t] += red[t + w * CB];
-    __syncthreads();
-  }
+  q = bn_group_sum(q, t, CB, T, red);
   mean_out = mean;
-  m2_out = red[cl];
+  m2_out = q;  // valid in threads t < CB
   __syncthreads();  // red is reused by the caller's next merge
 }
 
