@@ -941,15 +941,31 @@ int bn_bwd_merged(int64_t m, int32_t c, const GS& gs, bool gather, const float* 
   // gathering source (GMax: 8 loads per row) keeps 4.  (1,024-thread workgroups for the C = 64 partial pass:
   // BN 1.020 -> 0.972 ms of device time but the step 2.778 -> 2.786 ms — the wide workgroups crowd the other
   // encoder's stream; not built)
-  const int pu = (!bn_wide() || gather) ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
+  //
+  // The stems' long tiles (more than 192 rows: 752 / 196 rows at batch 128) run 1,024-thread workgroups, 64 row
+  // groups, so the gathering max-pool source (4 rows per batch) needs a quarter of the serial load batches (round
+  // 5: step 2.4175 vs 2.4293 ms, BN family 0.98 -> 0.95 ms, profiles/r5/r5rg_ab_stem_bn_rg64.json; the audio stem's
+  // gathered partial pass was 56-65 us).  Chosen from (m, c) alone, so a shape's gathered and dense partial sums keep
+  // the same order (bitwise).  TSPM_BN_RG64_ROWS moves the threshold (rows per tile).
+  static const long long rg64_rows = [] {
+    const char* e = getenv("TSPM_BN_RG64_ROWS");
+    return e ? atoll(e) : 193LL;
+  }();
+  const bool rg64 = bn_wide() && c <= kChanPerBlock && rpb >= rg64_rows;
+  const int pu = (!bn_wide() || gather || rg64) ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
 #define BNB_P(HO, TW, U)                                                                                       \
   hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, U, kRowGroups, GS>), pgrid, dim3(256), 0, st, (long long)m, c, gs, \
                      out, y, mean, y2, mean2, rpb, part)
-#define BNB_PU(HO, TW) \
-  if (pu == 16) { BNB_P(HO, TW, 16); } else if (pu == 8) { BNB_P(HO, TW, 8); } else { BNB_P(HO, TW, 4); }
+#define BNB_P64(HO, TW)                                                                                          \
+  hipLaunchKernelGGL((k_bn_bwd_partial<HO, TW, 4, 4 * kRowGroups, GS>), pgrid, dim3(64 * kRowGroups), 0, st,     \
+                     (long long)m, c, gs, out, y, mean, y2, mean2, rpb, part)
+#define BNB_PU(HO, TW)                                                                                    \
+  if (rg64) { BNB_P64(HO, TW); } else if (pu == 16) { BNB_P(HO, TW, 16); } else if (pu == 8) { BNB_P(HO, TW, 8); } \
+  else { BNB_P(HO, TW, 4); }
   if (ho) { if (two) { BNB_PU(true, true) } else { BNB_PU(true, false) } }
   else { if (two) { BNB_PU(false, true) } else { BNB_PU(false, false) } }
 #undef BNB_PU
+#undef BNB_P64
 #undef BNB_P
   TSPM_LAUNCH_CHECK();
   const int cblk = cdiv(c, kChanPerBlock);
