@@ -12,7 +12,8 @@
  *   - Activations are "HWNC": rows ordered (h, w, n), C contiguous fp32 per row.
  *   - Conv weights are OHWI fp32 (the channels_last view of the reference's OIHW nn.Conv2d weight;
  *     the state_dict keeps shape [O, I, H, W]).
- *   - No entry point allocates, synchronises the host, or keeps mutable global state; workspace is
+ *   - No entry point allocates, synchronises the host, reads the environment or keeps mutable global state
+ *     (ABI 21; tspm_flag_create / _destroy below are the one documented allocating pair); workspace is
  *     caller-provided (size queries provided).  Every call is enqueued on `stream` (a hipStream_t),
  *     so calls are capturable into a hipGraph.
  *   - Return value: TSPM_OK (0) or a TSPM_ERR_* code; nothing is launched on error.
@@ -40,10 +41,12 @@ enum {
  * tspm_conv_fwd_bnin, tspm_conv_wgrad_t, tspm_conv_dgrad_bnfuse / _bwd_bnfuse / _dgrad_bn_tiles,
  * tspm_bn_bwd_apply / _max_tiles, tspm_debug_barrier_timeouts, tspm_bn1d_bwd_maxout — and the 2x2 LDS tiles;
  * 19 = tspm_bn_bwd_src, the BN backward reading its gradient through a pooling layer's backward, and
- * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch, and tspm_set_conv_lds_floor;
+ * tspm_bn_apply_maxpool, the stem's apply + ReLU + max pool in one launch, and tspm_set_conv_lds_floor (gone in 21);
  * 20 = tspm_conv_bwd_adam, the fused backward launch carrying an Adam update over earlier-finished parameters,
- * and tspm_head_desc.adam_step). */
-#define TSPM_ABI_VERSION 20
+ * and tspm_head_desc.adam_step; 21 = round 6: no mutable global state and no environment reads inside the library —
+ * tspm_set_conv_lds_floor removed, the floor and the hand-off mode are per-call tspm_conv_algo fields, and the
+ * head's row block is tspm_head_desc.rows_per_block). */
+#define TSPM_ABI_VERSION 21
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -83,10 +86,20 @@ typedef struct tspm_conv_shape {
  *   stages the band's input rows (and, for the weight gradient, its dy rows) in LDS and runs the band
  *   on MFMA.  The forward's BN partial statistics are per band (tspm_conv_fwd_tiles /
  *   _tile_rows report the band count and rows); the weight gradient reduces per-workgroup slabs in
- *   the workspace after its TSPM_COUNTER_BYTES header (tspm_conv_wgrad_workspace).  Round 4. */
+ *   the workspace after its TSPM_COUNTER_BYTES header (tspm_conv_wgrad_workspace).  Round 4.
+ * lds_floor (ABI 21; variants 1 and 2): minimum dynamic LDS in bytes (<= 160 KiB; 0 = none) of this launch — a
+ *   floor caps how many of the launch's workgroups share a CU, so a concurrent stream keeps CU room (the step sets
+ *   it on the encoder with slack).  Scheduling only: results are bitwise the same.  For tspm_conv_bwd[_adam] the
+ *   larger of the two algos' floors applies.  (Replaces ABI 19-20's process-wide tspm_set_conv_lds_floor.)
+ * flags (ABI 21): TSPM_ALGO_HANDOFF_ACQUIRE — the split-K / BN-merge last arrivers take an agent-scope acquire
+ *   before plain loads instead of reading the write-through payload with sc1 loads (bitwise the same; the
+ *   reference side of tests/test_gpu_handoff.py, not a performance option). */
+#define TSPM_ALGO_HANDOFF_ACQUIRE 1
 typedef struct tspm_conv_algo {
   int32_t tm, tn, wn, wk, splits;
   int32_t variant;
+  int32_t lds_floor;
+  int32_t flags;
 } tspm_conv_algo;
 
 /* Element strides (n, h, w, c) of a conv input tensor.  HWNC tensors: {c, w*n*c, n*c, 1}.
@@ -212,12 +225,6 @@ int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const
                        const float* gamma, const float* beta, int32_t res_mode, const float* res,
                        const float* res_mean, const float* res_inv, const float* res_gamma, const float* res_beta,
                        int32_t relu, int32_t eval, float eps, float* out, float* pooled, tspm_stream_t stream);
-
-/* ABI 19: minimum dynamic LDS (bytes, <= 160 KiB; 0 = none) of the LDS-staged conv launches issued after this call
- * (variants 1 and 2): a floor caps how many of one launch's workgroups share a CU, so a concurrent stream keeps CU
- * room.  Process-wide host state read at launch time; a captured launch keeps the value it was captured with.
- * Set by the step for the encoder with slack (step.py, TSPM_SLACK_LDS_FLOOR). */
-int tspm_set_conv_lds_floor(size_t bytes);
 
 /* ABI 19: the stem's BN apply + ReLU with the following MaxPool2d(3, 2, 1) in the same launch (resnet.py:138-140):
  * pooled [p][q][n][c] and its argmax taps idx exactly as tspm_maxpool_fwd over tspm_bn_apply's output, and that
@@ -366,7 +373,7 @@ int tspm_cross_entropy(int32_t n, int32_t classes, const float* logits, const in
  * Dropout(p) → Linear(hidden, hidden2) → ReLU → Linear(hidden2, classes) (models/avmnist.py:219-230,
  * forward :267), the LossFunctionGroup's weighted cross-entropy (experiment_utils/loss.py:98-148) and
  * the head's whole backward, in TWO launches instead of ten:
- *   (1) one sample per workgroup (512 threads; round 5 — TSPM_HEAD_RB=4 selects round 4's blocks of 4
+ *   (1) one sample per workgroup (512 threads; round 5 — rows_per_block = 4 selects round 4's blocks of 4
  *       samples on 256 threads), the three weight matrices staged in LDS: dropout keep
  *       mask (same counter-hash bits as
  *       tspm_dropout_mask, or read from `keep` when gen_keep == 0), h1, hh, logits, per-row CE,
@@ -398,6 +405,9 @@ typedef struct tspm_head_desc {
   int64_t* adam_step;              /* nullable (ABI 20): the optimizer's tspm_adam_hyper.step, incremented once by
                                     * launch 2 after launch 1 read `counter` (tspm_adam_begin's job, one launch fewer
                                     * between the forward and the backward) */
+  int32_t rows_per_block;          /* ABI 21: samples per workgroup of launch 1 — 0 = the default (1 up to 256
+                                    * rows, else 4), or 1 / 4 (A/B; was the TSPM_HEAD_RB environment read) */
+  int32_t reserved_;
 } tspm_head_desc;
 int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t stream);
 

@@ -17,7 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TSPM_LIB", os.path.join(_HERE, "libtspm.so"))
-ABI_VERSION = 20
+ABI_VERSION = 21
 COUNTER_BYTES = 65536     # TSPM_COUNTER_BYTES: arrival-counter header of a split wgrad workspace
 
 
@@ -33,9 +33,17 @@ class ConvShape(Structure):
     _fields_ = [(n, c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "p", "q")]
 
 
+ALGO_HANDOFF_ACQUIRE = 1  # tspm_conv_algo.flags (ABI 21)
+
+
 class ConvAlgo(Structure):
-    """tspm_conv_algo: (tm, tn, wn, wk, splits[, variant]); variant 1 = LDS-staged kernels."""
-    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits", "variant")]
+    """tspm_conv_algo: (tm, tn, wn, wk, splits[, variant[, lds_floor, flags]]); variant 1 = LDS-staged kernels.
+    lds_floor / flags (ABI 21) are per-call launch options: the LDS floor (scheduling only) and the hand-off mode."""
+    _fields_ = [(n, c_int32) for n in ("tm", "tn", "wn", "wk", "splits", "variant", "lds_floor", "flags")]
+
+    def with_options(self, lds_floor: int = 0, flags: int = 0) -> "ConvAlgo":
+        """A copy with the per-call launch options set (the tile configuration unchanged)."""
+        return ConvAlgo(self.tm, self.tn, self.wn, self.wk, self.splits, self.variant, int(lds_floor), int(flags))
 
 
 class Strides4(Structure):
@@ -82,12 +90,14 @@ class LinearBwdDesc(Structure):
 
 
 class HeadDesc(Structure):
-    """tspm_head_desc (ABI 16; adam_step ABI 20): the AVMNIST fusion head's train step in two launches."""
+    """tspm_head_desc (ABI 16; adam_step ABI 20; rows_per_block ABI 21): the AVMNIST fusion head's train step in
+    two launches."""
     _fields_ = [(n, c_int32) for n in ("n", "in_", "hidden", "hidden2", "classes", "ldx", "lddx", "gen_keep")] + \
         [(n, c_void_p) for n in ("x", "w0", "b0", "w3", "b3", "w5", "b5")] + \
         [("p", c_float), ("loss_weight", c_float), ("seed", c_uint64)] + \
         [(n, c_void_p) for n in ("counter", "keep", "labels", "h1", "hh", "logits", "dlogits", "dz3", "dz0", "dx",
-                                 "row_ws", "gw0", "gb0", "gw3", "gb3", "gw5", "gb5", "loss", "stats", "adam_step")]
+                                 "row_ws", "gw0", "gb0", "gw3", "gb3", "gw5", "gb5", "loss", "stats", "adam_step")] + \
+        [("rows_per_block", c_int32), ("reserved_", c_int32)]
 
 
 # name -> (restype, argtypes)
@@ -136,7 +146,6 @@ _SIGS = {
                               _P, _P, c_int64, _P, c_size_t, _P]),
     "tspm_bn_bwd_workspace": (c_size_t, [c_int64, c_int32]),
     # ABI 19: the stem's apply + ReLU + max pool in one launch; the BN backward reading a pooling layer's gradient
-    "tspm_set_conv_lds_floor": (c_int32, [c_size_t]),
     # ABI 20: the fused backward launch carrying an Adam update over earlier-finished parameters
     "tspm_conv_bwd_adam": (c_int32, [_P] * 8 + [c_int32, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_apply_maxpool": (c_int32, [c_int32] * 4 + [_P] * 5 + [c_int32, c_float, _P, _P, _P, c_int32, c_int32, _P]),

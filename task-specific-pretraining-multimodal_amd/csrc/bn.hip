@@ -946,11 +946,9 @@ int bn_bwd_merged(int64_t m, int32_t c, const GS& gs, bool gather, const float* 
   // groups, so the gathering max-pool source (4 rows per batch) needs a quarter of the serial load batches (round
   // 5: step 2.4175 vs 2.4293 ms, BN family 0.98 -> 0.95 ms, profiles/r5/r5rg_ab_stem_bn_rg64.json; the audio stem's
   // gathered partial pass was 56-65 us).  Chosen from (m, c) alone, so a shape's gathered and dense partial sums keep
-  // the same order (bitwise).  TSPM_BN_RG64_ROWS moves the threshold (rows per tile).
-  static const long long rg64_rows = [] {
-    const char* e = getenv("TSPM_BN_RG64_ROWS");
-    return e ? atoll(e) : 193LL;
-  }();
+  // the same order (bitwise).  (Round 6: a fixed threshold; the environment knob that moved it is gone — the
+  // library reads no environment and keeps no mutable global state.)
+  constexpr long long rg64_rows = 193;
   const bool rg64 = bn_wide() && c <= kChanPerBlock && rpb >= rg64_rows;
   const int pu = (!bn_wide() || gather || rg64) ? 4 : rpb >= 32LL * kRowGroups ? 16 : rpb >= 16LL * kRowGroups ? 8 : 4;
 #define BNB_P(HO, TW, U)                                                                                       \

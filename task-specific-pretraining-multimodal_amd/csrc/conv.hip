@@ -637,13 +637,18 @@ Algo wgrad_algo(const tspm_conv_shape* s, const tspm_conv_algo* user) {
 
 // variants 1 and 2 (LDS-staged, conv_lds.hip: register-staged loader waves / single-role LDS-DMA ring):
 // wm = 4 / (wn * wk)
+// the per-call launch options of ABI 21 (tspm_conv_algo.lds_floor / flags) are in range
+bool opts_ok(const tspm_conv_algo* u) {
+  return !u || (u->lds_floor >= 0 && u->lds_floor <= 160 * 1024 && (u->flags & ~TSPM_ALGO_HANDOFF_ACQUIRE) == 0);
+}
 bool is_lds(const tspm_conv_algo* user) { return user && (user->variant == 1 || user->variant == 2); }
 bool is_stem(const tspm_conv_algo* user) { return user && user->variant == 3; }
 const tspm_detail::LdsImpl& lds_of(const tspm_conv_algo* user) {
   return user->variant == 2 ? tspm_detail::lds_impl_dma() : tspm_detail::lds_impl_reg();
 }
 tspm_detail::LdsAlgo lds_algo(const tspm_conv_algo* u) {
-  tspm_detail::LdsAlgo a{u->tm, u->tn, 0, u->wn, u->wk, u->splits > 0 ? u->splits : 1};
+  tspm_detail::LdsAlgo a{u->tm, u->tn, 0, u->wn, u->wk, u->splits > 0 ? u->splits : 1,
+                         (size_t)std::max(0, u->lds_floor), (u->flags & TSPM_ALGO_HANDOFF_ACQUIRE) ? 1 : 0};
   const int wnk = a.wn * a.wk;
   a.wm = (wnk > 0 && 4 % wnk == 0) ? 4 / wnk : 0;
   return a;
@@ -683,19 +688,10 @@ extern "C" int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* s, con
   return 3LL * tspm_conv_fwd_tiles(s, user) * s->k;
 }
 
-namespace tspm_detail {
-size_t g_lds_floor = 0;
-}
-extern "C" int tspm_set_conv_lds_floor(size_t bytes) {
-  if (bytes > 160 * 1024) return TSPM_ERR_INVALID;
-  tspm_detail::g_lds_floor = bytes;
-  return TSPM_OK;
-}
-
 extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
                              const tspm_strides4* xs, const float* w, float* y, const tspm_bn_fuse* bn, void* ws,
                              size_t ws_bytes, tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !w || !y) return TSPM_ERR_INVALID;
+  if (!shape_ok(s) || !x || !w || !y || !opts_ok(user)) return TSPM_ERR_INVALID;
   tspm_bn_fuse bf{};
   if (bn) {
     bf = *bn;
@@ -748,7 +744,7 @@ extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm
 extern "C" int tspm_conv_dgrad(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* dy,
                                const float* w, float* dx, int32_t beta, void* ws, size_t ws_bytes,
                                tspm_stream_t stream) {
-  if (!shape_ok(s) || !dy || !w || !dx) return TSPM_ERR_INVALID;
+  if (!shape_ok(s) || !dy || !w || !dx || !opts_ok(user)) return TSPM_ERR_INVALID;
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).dgrad_supported(s, la)) return TSPM_ERR_INVALID;
@@ -781,7 +777,7 @@ extern "C" size_t tspm_conv_wgrad_workspace(const tspm_conv_shape* s, const tspm
 extern "C" int tspm_conv_wgrad(const tspm_conv_shape* s, const tspm_conv_algo* user, const float* x,
                                const tspm_strides4* xs, const float* dy, float* dw, void* ws, size_t ws_bytes,
                                tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !dy || !dw) return TSPM_ERR_INVALID;
+  if (!shape_ok(s) || !x || !dy || !dw || !opts_ok(user)) return TSPM_ERR_INVALID;
   if (is_lds(user)) {
     const tspm_detail::LdsAlgo la = lds_algo(user);
     if (!lds_of(user).wgrad_supported(s, xs, la)) return TSPM_ERR_INVALID;
@@ -833,7 +829,7 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
                              const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
                              int32_t beta, float* dw, void* ws_d, size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes,
                              tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw) return TSPM_ERR_INVALID;
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !opts_ok(dg) || !opts_ok(wg)) return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, nullptr, ws_d, ws_d_bytes, ws_w,
                         ws_w_bytes, static_cast<hipStream_t>(stream));
@@ -843,7 +839,7 @@ extern "C" int tspm_conv_bwd_adam(const tspm_conv_shape* s, const tspm_conv_algo
                                   const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
                                   int32_t beta, float* dw, const tspm_adam_job* job, void* ws_d, size_t ws_d_bytes,
                                   void* ws_w, size_t ws_w_bytes, tspm_stream_t stream) {
-  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !job) return TSPM_ERR_INVALID;
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !job || !opts_ok(dg) || !opts_ok(wg)) return TSPM_ERR_INVALID;
   if (job->count < 0 || job->blocks < 0 || (job->count > 0 && (!job->param || !job->grad || !job->exp_avg ||
                                                                !job->exp_avg_sq || !job->hyper || job->blocks < 1)))
     return TSPM_ERR_INVALID;

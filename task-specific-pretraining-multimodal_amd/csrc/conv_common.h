@@ -222,6 +222,8 @@ TSPM_DEV void fwd_bn_tail(const ConvArgs& g, const tspm_bn_fuse& bf, float* lds)
 namespace tspm_detail {
 struct LdsAlgo {
   int tm, tn, wm, wn, wk, splits;
+  size_t floor;  // tspm_conv_algo.lds_floor: minimum dynamic LDS of the launch (ABI 21; per call, no global state)
+  int acq;       // tspm_conv_algo.flags & TSPM_ALGO_HANDOFF_ACQUIRE
 };
 // The LDS-staged kernels (conv_lds.hip) are built twice, with different operand loaders, and reached through
 // these tables: variant 1 = register-staged loader waves (lds_impl_reg), variant 2 = single-role waves with
@@ -248,11 +250,9 @@ struct LdsImpl {
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();
-// Minimum dynamic LDS of the LDS-staged launches (tspm_set_conv_lds_floor): a caller-chosen floor caps how many
-// of a launch's workgroups share a CU, leaving room for a concurrent stream's kernels.  Host state read at
-// launch time (a captured launch keeps the value it was captured with).
-extern size_t g_lds_floor;
-inline size_t lds_with_floor(size_t lds) { return std::max(lds, std::min(g_lds_floor, (size_t)160 * 1024)); }
+// Minimum dynamic LDS of an LDS-staged launch (tspm_conv_algo.lds_floor, ABI 21): a caller-chosen floor caps how
+// many of the launch's workgroups share a CU, leaving room for a concurrent stream's kernels.  Passed per call.
+inline size_t lds_with_floor(size_t lds, const LdsAlgo& a) { return std::max(lds, std::min(a.floor, (size_t)160 * 1024)); }
 // The 1-channel 7x7/2 stems, tspm_conv_algo.variant 3 (stem.hip)
 bool stem_supported(const tspm_conv_shape* s);
 int stem_pb(const tspm_conv_shape* s);

@@ -875,22 +875,17 @@ bool hwnc(const tspm_conv_shape* s, const tspm_strides4* st) {
 constexpr int xcd_enabled() { return 0; }
 
 // The last arriver of a split-K tile / BN merge group reads the sc1 payload with sc1 loads and takes no
-// agent-scope acquire (conv 2.612 -> 2.595 ms without it; bitwise the same).  TSPM_HANDOFF_ACQUIRE=1
-// restores the acquire: the reference side of the hand-off validation (tests/test_gpu_handoff.py), not a
-// performance option.
-int acquire_enabled() {
-  const char* e = getenv("TSPM_HANDOFF_ACQUIRE");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-ConvArgs args_of(const tspm_conv_shape* s) {
+// agent-scope acquire (conv 2.612 -> 2.595 ms without it; bitwise the same).  The algo flag
+// TSPM_ALGO_HANDOFF_ACQUIRE restores the acquire: the reference side of the hand-off validation
+// (tests/test_gpu_handoff.py), not a performance option.
+ConvArgs args_of(const tspm_conv_shape* s, const LdsAlgo& a) {
   ConvArgs g{};
   g.n = s->n; g.h = s->h; g.w = s->w; g.c = s->c; g.k = s->k; g.r = s->r; g.s = s->s;
   g.st = s->stride; g.pad = s->pad; g.p = s->p; g.q = s->q;
   g.sn = s->c; g.sh = (long long)s->w * s->n * s->c; g.sw = (long long)s->n * s->c; g.sc = 1;
   g.m = 0; g.splits = 1; g.slab = 0; g.beta = 0; g.cnt = nullptr;
   g.xcd = xcd_enabled();
-  g.acq = acquire_enabled();
+  g.acq = a.acq;
   return g;
 }
 
@@ -978,7 +973,7 @@ size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
 
 int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
             const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
-  ConvArgs g = args_of(s);
+  ConvArgs g = args_of(s, a);
   g.m = s->p * s->q * s->n;
   g.splits = a.splits;
   if (!slab_fits(a.splits, g.m, s->k)) return TSPM_ERR_INVALID;
@@ -1004,7 +999,7 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
     if (!room) bf.counters = nullptr;
   }
   const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
-  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, bf.counters != nullptr));
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, bf.counters != nullptr), a);
 #define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
@@ -1018,7 +1013,7 @@ int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const fl
 
 int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
               void* ws, size_t ws_bytes, hipStream_t st) {
-  ConvArgs g = args_of(s);
+  ConvArgs g = args_of(s, a);
   g.m = s->h * s->w * s->n;
   g.splits = a.splits;
   g.beta = beta ? 1 : 0;
@@ -1031,7 +1026,7 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
   }
   const dim3 grid(g.m / bm_of(a), cdiv(s->c, bn_of(a)), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
-  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false));
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false), a);
 #define TSPM_DG(CFG) hipLaunchKernelGGL(k_dgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, dy, w, dx, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_DG) }();
 #undef TSPM_DG
@@ -1042,7 +1037,7 @@ int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const
 
 int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* dy, float* dw, void* ws,
               size_t ws_bytes, hipStream_t st) {
-  ConvArgs g = args_of(s);
+  ConvArgs g = args_of(s, a);
   g.m = s->k;
   g.splits = a.splits;
   if (!slab_fits(a.splits, s->k, (long long)s->r * s->s * s->c)) return TSPM_ERR_INVALID;
@@ -1055,7 +1050,7 @@ int lds_wgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const 
   const int RSC = s->r * s->s * s->c;
   const dim3 grid(cdiv(s->k, bm_of(a)), RSC / bn_of(a), a.splits);
   if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
-  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false));
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, false), a);
 #define TSPM_WG(CFG) hipLaunchKernelGGL(k_wgrad_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, dy, dw, slabs)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_WG) }();
 #undef TSPM_WG
@@ -1122,7 +1117,7 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
       !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
     return TSPM_ERR_INVALID;
   BwdLaunch L{};
-  L.gd = args_of(s);
+  L.gd = args_of(s, ad);
   L.gd.m = s->h * s->w * s->n;
   L.gd.splits = ad.splits;
   L.gd.beta = beta ? 1 : 0;
@@ -1131,7 +1126,7 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
     L.gd.cnt = static_cast<unsigned*>(wsd);
     L.slabs_d = reinterpret_cast<float*>(static_cast<char*>(wsd) + TSPM_COUNTER_BYTES);
   }
-  L.gw = args_of(s);
+  L.gw = args_of(s, aw);
   L.gw.m = s->k;
   L.gw.splits = aw.splits;
   if (aw.splits > 1) {
@@ -1152,7 +1147,9 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
     L.aj = AdamJobArgs{adam->param, adam->grad, adam->exp_avg, adam->exp_avg_sq, (long long)adam->count, adam->hyper};
     L.naj = adam->blocks;
   }
-  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)));
+  LdsAlgo af = ad;  // one launch: the larger of the two halves' floors
+  af.floor = std::max(ad.floor, aw.floor);
+  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)), af);
   L.st = st;
   bwd_dispatch(ad, aw, &L);
   TSPM_LAUNCH_CHECK();

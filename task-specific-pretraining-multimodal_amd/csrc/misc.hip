@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64 * WK) void k_gemm_pair(GemmArgs a, GemmArgs b, i
 // Quad tiles (64x64, one quadrant per wave) measured on the MMIMDb image-encoder products at batch 256 did
 // not pay — weight-grad 25.4 us (25.0 with 32x32 tiles), data-grad 36.8 us (25-31): the L1 sharing between
 // a workgroup's waves does not materialise for these strides.  Off (not reachable).
-constexpr bool getenv_flag_quad() { return false; }
+constexpr bool quad_tiles_enabled() { return false; }
 
 // Split-K combine: C = epi(sum over slices in order of slab[s]) with gemm_small's epilogue.
 __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs g, int splits) {
@@ -276,7 +276,7 @@ int gemm_small(const GemmArgs& g0, hipStream_t st, int splits) {
   // products, K = 512: step 2.584-2.590 vs 2.584-2.589 ms, no gain — profiles/r4/r4j_gemm_wk8_*.json)
   while (wk < 4 && kk / (wk * 2) >= 32) wk *= 2;
   // quad tiles where 32x32 tiles are plentiful (>= 1024) and K is short enough for one wave
-  g.quad = (splits <= 1 && tiles >= 1024 && g.K <= 1024 && getenv_flag_quad()) ? 1 : 0;
+  g.quad = (splits <= 1 && tiles >= 1024 && g.K <= 1024 && quad_tiles_enabled()) ? 1 : 0;
   if (g.quad) wk = 4;
   const size_t lds = g.quad ? 0 : (size_t)(wk - 1) * (16 * 64 + 32) * sizeof(float);
   const dim3 grid(g.quad ? cdiv(g.M, 64) * cdiv(g.N, 64) : tiles, splits > 1 ? splits : 1);
@@ -1109,6 +1109,7 @@ __global__ __launch_bounds__(64 * WK) void k_head_wgrad(GemmMulti mp, int total,
 extern "C" int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t stream) {
   if (!desc) return TSPM_ERR_INVALID;
   const tspm_head_desc& d = *desc;
+  if (d.rows_per_block != 0 && d.rows_per_block != 1 && d.rows_per_block != 4) return TSPM_ERR_INVALID;
   if (d.n <= 0 || d.in <= 0 || d.hidden <= 0 || d.hidden2 <= 0 || d.classes <= 0) return TSPM_ERR_INVALID;
   if (d.in > HEAD_MAXIN || d.hidden > HEAD_MAXH || d.hidden2 > HEAD_MAXH2 || d.classes > HEAD_MAXC)
     return TSPM_ERR_INVALID;
@@ -1123,12 +1124,8 @@ extern "C" int tspm_head_train_step(const tspm_head_desc* desc, tspm_stream_t st
   HeadArgs a{d, d.p > 0.f ? 1.0f / (1.0f - d.p) : 1.0f};
   // one sample per workgroup up to 256 rows (batch 128: 21.2 vs 26.7 us graph-timed, step -9 us); blocks of 4
   // beyond (batch 1024: 1,024 workgroups each staging the 134 KB of weights took 52.9 vs 21.1 us,
-  // gpurun_out/r5b_head*.txt); TSPM_HEAD_RB=1/4 forces one for A/B
-  static const int rb_env = [] {
-    const char* e = getenv("TSPM_HEAD_RB");
-    return (e && e[0] == '4') ? 4 : (e && e[0] == '1') ? 1 : 0;
-  }();
-  const int rb = rb_env ? rb_env : (d.n <= 256 ? 1 : 4);
+  // gpurun_out/r5b_head*.txt); tspm_head_desc.rows_per_block = 1 / 4 forces one (ABI 21; 0 = this default)
+  const int rb = d.rows_per_block ? d.rows_per_block : (d.n <= 256 ? 1 : 4);
   const size_t lds_rows = head_lds_floats(d.in, d.hidden, d.hidden2, d.classes, rb) * sizeof(float);
   if (lds_rows > 160 * 1024) return TSPM_ERR_INVALID;
   if (rb == 4) hipLaunchKernelGGL((k_head_rows<4, 256>), dim3(cdiv(d.n, 4)), dim3(256), lds_rows, st, a);

@@ -147,6 +147,9 @@ class EncoderEngine:
         # optional step.AdamCarry: the single-GPU train step's Adam updates of finished blocks carried by later
         # backward launches (tspm_conv_bwd_adam, ABI 20); None = every update by the optimizer's own launches
         self.adam_carry = None
+        # minimum dynamic LDS of this engine's LDS-staged conv launches (tspm_conv_algo.lds_floor, ABI 21 — a per-call
+        # launch option, no library state): set by the train step around the encoder with slack (step._slack_floor)
+        self.lds_floor = 0
         # the pooling backwards folded into the adjacent BN backward (tspm_bn_bwd_src, round 5); TSPM_BN_POOL_SRC=0
         # restores the separate tspm_avgpool_bwd / tspm_maxpool_bwd launches for A/B
         self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
@@ -218,7 +221,8 @@ class EncoderEngine:
         self.gA = torch.empty(max_blk, **f32)
         self.gB = torch.empty(max_blk, **f32)
         self.da1 = torch.empty(max_blk, **f32)
-        self.g_stem = torch.empty(self.a0.numel(), **f32)
+        # the materialised max-pool gradient: only when the stem BN does not read it through the argmax taps
+        self.g_stem = None if self.pool_src else torch.empty(self.a0.numel(), **f32)
         self.dy_stem = torch.empty(self.a0.numel(), **f32)
         self.g_pooled = torch.empty(N, c, **f32)
         self.g_final = torch.empty(h * w * N * c, **f32)
@@ -284,10 +288,14 @@ class EncoderEngine:
             raise L.TspmError("conv weight must be OHWI (channels_last); call prepare_encoder_layout() first")
         return w
 
+    def _a(self, algo: L.ConvAlgo) -> L.ConvAlgo:
+        """``algo`` with this engine's per-call launch options (the LDS floor)."""
+        return algo.with_options(self.lds_floor) if self.lds_floor else algo
+
     def _conv_fwd(self, op: ConvOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
                   bnf: Optional[L.BnFuse] = None) -> None:
         lib = L.lib()
-        s, a = op.shape, op.algo_fwd
+        s, a = op.shape, self._a(op.algo_fwd)
         ws = self.ws_conv
         if self.conv_timer:
             self.conv_timer.begin(op, "fwd")
@@ -480,7 +488,8 @@ class EncoderEngine:
             raise L.TspmError("conv weight grad must be OHWI (channels_last)")
         if self.conv_timer:
             self.conv_timer.begin(op, "wgrad")
-        L.check(L.lib().tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides),
+        aw = self._a(op.algo_wgrad)
+        L.check(L.lib().tspm_conv_wgrad(ctypes.byref(op.shape), ctypes.byref(aw), x_ptr, ctypes.byref(strides),
                                         dy.data_ptr(), gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes, sh),
                 "conv_wgrad")
         if self.conv_timer:
@@ -504,14 +513,14 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.begin(op, "bwd")
         job = self.adam_carry.take(carry_share) if self.adam_carry is not None else None
+        ad, aw = self._a(op.algo_dgrad), self._a(op.algo_wgrad)
         if job is not None:  # an Adam update over earlier-finished parameters rides on this launch (ABI 20)
-            L.check(lib.tspm_conv_bwd_adam(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad),
-                                           ctypes.byref(op.algo_wgrad), x_ptr, ctypes.byref(strides), dy.data_ptr(),
+            L.check(lib.tspm_conv_bwd_adam(ctypes.byref(op.shape), ctypes.byref(ad), ctypes.byref(aw), x_ptr, ctypes.byref(strides), dy.data_ptr(),
                                            self._w(op).data_ptr(), dx.data_ptr(), beta, gw.data_ptr(), ctypes.byref(job),
                                            self.ws_conv.data_ptr(), self.ws_conv_bytes, self.ws_conv2.data_ptr(),
                                            self.ws_conv_bytes, sh), "conv_bwd_adam")
         else:
-            L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), ctypes.byref(op.algo_wgrad),
+            L.check(lib.tspm_conv_bwd(ctypes.byref(op.shape), ctypes.byref(ad), ctypes.byref(aw),
                                       x_ptr, ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
                                       beta, gw.data_ptr(), self.ws_conv.data_ptr(), self.ws_conv_bytes,
                                       self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
@@ -522,7 +531,8 @@ class EncoderEngine:
     def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
         if self.conv_timer:
             self.conv_timer.begin(op, "dgrad")
-        L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(op.algo_dgrad), dy.data_ptr(),
+        ad = self._a(op.algo_dgrad)
+        L.check(L.lib().tspm_conv_dgrad(ctypes.byref(op.shape), ctypes.byref(ad), dy.data_ptr(),
                                         self._w(op).data_ptr(), dx.data_ptr(), beta, self.ws_conv.data_ptr(),
                                         self.ws_conv_bytes, sh), "conv_dgrad")
         if self.conv_timer:
@@ -644,6 +654,8 @@ class EncoderEngine:
                            idx=self.mp_idx.data_ptr())
             self._bn_bwd_src(self.stem_bn, src, self.a0, self.y0, self.dy_stem, sh=sh)
         else:
+            if self.g_stem is None:  # pool_src switched off after construction
+                self.g_stem = torch.empty(self.a0.numel(), device=self.device, dtype=torch.float32)
             L.check(lib.tspm_maxpool_bwd(N, p1, q1, C0, 3, 2, 1, p2, q2, G.data_ptr(), self.mp_idx.data_ptr(),
                                          self.g_stem.data_ptr(), sh), "maxpool_bwd")
             self._bn_bwd(self.stem_bn, self.g_stem, self.a0, self.y0, self.dy_stem, sh=sh)

@@ -89,7 +89,7 @@ def head_supported(model) -> bool:
         return False
     if F % 4 or H % 4 or H2 % 4:
         return False
-    rb = 4  # the larger of the kernel's row blocks (TSPM_HEAD_RB=4; the default is 1)
+    rb = 4  # the larger of the kernel's row blocks (tspm_head_desc.rows_per_block = 4; the default is 1 up to 256 rows)
     ldc = ((C + 3) & ~3) + 4
     floats = H * (F + 4) + H2 * (H + 4) + C * (H2 + 4) + rb * ((F + 4) + (H + 4) + (H2 + 4) + ldc) + (H + H2 + C + rb)
     return floats * 4 <= 160 * 1024
@@ -137,7 +137,13 @@ class AdamCarry:
         spans = [self.where.get(id(p)) for p in params]
         if not spans or any(sp is None for sp in spans):
             return
-        a, b = min(sp[0] for sp in spans), max(sp[1] for sp in spans)
+        # the block's spans must tile [a, b) exactly: with a parameter order that interleaves another block's (or
+        # the other encoder's) parameters into this range, [min, max) would cover elements whose gradients may
+        # still be in flight — such a block stays with the optimizer's own launches
+        spans = sorted(spans)
+        if any(spans[i][1] != spans[i + 1][0] for i in range(len(spans) - 1)):
+            return
+        a, b = spans[0][0], spans[-1][1]
         if self.lo is None:
             self.lo, self.hi = a, b
         elif b == self.lo:
@@ -251,6 +257,9 @@ class FusedTrainStep:
         # 8,192 elements (256 x 16,384: 2.5571 vs 2.5933; image only: 2.5692 vs 2.5965); batch 1024: 9.807 vs
         # 9.866 ms (r5u_carry_b1024.json)
         self.adam_carry = os.environ.get("TSPM_ADAM_CARRY", "both")
+        # the head's samples per workgroup (tspm_head_desc.rows_per_block, ABI 21): 0 = the library's default (1 up
+        # to 256 rows, else 4); TSPM_HEAD_RB=1 / 4 forces one for A/B (read here, not inside the library)
+        self.head_rows_per_block = int(os.environ.get("TSPM_HEAD_RB", "0"))
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         # single-GPU step (adam_split): each encoder's parameters updated by Adam on that encoder's stream right
@@ -295,7 +304,8 @@ class FusedTrainStep:
                        gw0=g(net[0].weight.grad), gb0=g(net[0].bias.grad), gw3=g(net[3].weight.grad),
                        gb3=g(net[3].bias.grad), gw5=g(net[5].weight.grad), gb5=g(net[5].bias.grad),
                        loss=g(self.loss), stats=g(self.stats),
-                       adam_step=self._rng_ctr_ptr if self._head_bumps_step else None)
+                       adam_step=self._rng_ctr_ptr if self._head_bumps_step else None,
+                       rows_per_block=self.head_rows_per_block)
         L.check(L.lib().tspm_head_train_step(d, sh), "head_train_step")
 
     def _fwd_bwd(self, marks=None) -> None:
@@ -370,17 +380,17 @@ class FusedTrainStep:
 
     @contextlib.contextmanager
     def _slack_floor(self, part: str = "b"):
-        """The audio encoder's LDS-staged conv launches with a minimum LDS allocation (tspm_set_conv_lds_floor,
-        TSPM_SLACK_LDS_FLOOR bytes), so fewer of its workgroups share a CU with the image chain
-        (the replayed step's critical path, scripts/overlap_probe.py --dump)."""
+        """The audio encoder's LDS-staged conv launches with a minimum LDS allocation (TSPM_SLACK_LDS_FLOOR bytes,
+        passed per launch as tspm_conv_algo.lds_floor — ABI 21, no library state), so fewer of its workgroups share
+        a CU with the image chain (the replayed step's critical path, scripts/overlap_probe.py --dump).  The floor
+        lives on this step's own audio engine and only while its launches are enqueued."""
         floor = self.slack_lds_floor if part in self.slack_parts else 0
         if floor and not self.serial:
-            L.check(L.lib().tspm_set_conv_lds_floor(floor), "set_conv_lds_floor")
+            self.eng_a.lds_floor = floor
         try:
             yield
         finally:
-            if floor and not self.serial:
-                L.check(L.lib().tspm_set_conv_lds_floor(0), "set_conv_lds_floor")
+            self.eng_a.lds_floor = 0
 
     def _split_opt(self) -> bool:
         """Adam launched per encoder inside the fwd/bwd enqueue (single GPU, no gradient clipping: the

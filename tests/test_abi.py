@@ -115,3 +115,42 @@ def test_abi_version_consistent_everywhere():
         doc = [int(v) for v in re.findall(r"tspm_abi_version\(\) == (\d+)", f.read())]
     assert doc and all(v == hdr for v in doc)
     assert L.ABI_VERSION == hdr
+
+
+def test_launch_options_are_per_call_and_validated():
+    """ABI 21: the LDS floor and the hand-off mode are tspm_conv_algo fields (no process-wide setter); values out of
+    range are refused before any launch."""
+    lib = L.load()
+    assert ctypes.sizeof(L.ConvAlgo) == 32
+    assert not hasattr(L, "tspm_set_conv_lds_floor") and "tspm_set_conv_lds_floor" not in L._SIGS
+    a = L.ConvAlgo(1, 1, 1, 4, 1, 1)
+    b = a.with_options(82000, L.ALGO_HANDOFF_ACQUIRE)
+    assert (b.tm, b.tn, b.wn, b.wk, b.splits, b.variant, b.lds_floor, b.flags) == (1, 1, 1, 4, 1, 1, 82000, 1)
+    assert (a.lds_floor, a.flags) == (0, 0)  # the tuned configuration itself is not modified
+    s = L.ConvShape(128, 7, 7, 64, 64, 3, 3, 1, 1, 7, 7)
+    st = L.hwnc_strides(128, 7, 7, 64)
+    for bad in (a.with_options(160 * 1024 + 1), a.with_options(-1), a.with_options(0, 2)):
+        B = ctypes.byref(bad)
+        assert lib.tspm_conv_fwd(ctypes.byref(s), B, 16, ctypes.byref(st), 16, 16, None, None, 0, None) == 1
+        assert lib.tspm_conv_dgrad(ctypes.byref(s), B, 16, 16, 16, 0, None, 0, None) == 1
+        assert lib.tspm_conv_wgrad(ctypes.byref(s), B, 16, ctypes.byref(st), 16, 16, None, 0, None) == 1
+        assert lib.tspm_conv_bwd(ctypes.byref(s), B, ctypes.byref(a), 16, ctypes.byref(st), 16, 16, 16, 0, 16,
+                                 None, 0, None, 0, None) == 1
+    hd = L.HeadDesc(n=8, in_=192, hidden=128, hidden2=64, classes=10, ldx=192, lddx=192, rows_per_block=2)
+    assert lib.tspm_head_train_step(ctypes.byref(hd), None) == 1
+
+
+def test_library_sources_read_no_environment_and_keep_no_mutable_globals():
+    """nothing under csrc/ reads the environment, and no product translation unit defines a
+    mutable file-scope variable (the stamp buffers exist only in the TSPM_STAMPS diagnostic build)."""
+    csrc = os.path.join(REPO, "task-specific-pretraining-multimodal_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".hip", ".h")):
+            continue
+        src = open(os.path.join(csrc, f)).read()
+        assert "getenv" not in src, f
+        product = re.sub(r"#if(def TSPM_STAMPS| defined\(TSPM_STAMPS\)).*?#endif", "", src, flags=re.S)
+        for line in product.splitlines():
+            if re.match(r"^(static\s+)?(__device__\s+)?(unsigned|int|long|size_t|float|double|bool|char)\b[\w\s\*]*\s\w+\s*(=|;|\[)",
+                        line) and "constexpr" not in line and "(" not in line:
+                raise AssertionError(f"{f}: file-scope variable: {line.strip()}")

@@ -2,14 +2,14 @@
 
 The last arriving workgroup of a split-K tile (and of a BatchNorm merge group) reads the other
 workgroups' slabs / partial statistics with L1-bypassing sc1 loads instead of taking an acquire
-(csrc/common.h ld_sc1, last_arriver(acquire=false); TSPM_HANDOFF_ACQUIRE=1 restores the acquire).
+(csrc/common.h ld_sc1, last_arriver(acquire=false); the per-call flag TSPM_ALGO_HANDOFF_ACQUIRE (ABI 21)
+restores the acquire).
 MI355X_MICROARCH.md asks every hand-off to be tested under UNEVEN load, with the consumer's L1 warm,
 checking every word: here the same workspace and output buffers are reused by 48 back-to-back
 launches on fresh inputs each (a stale slab line from the previous launch would change the result)
 while a second stream streams a 1 GiB buffer, and every output word is compared with the acquire
 path's result for the same input."""
 import ctypes
-import os
 
 import pytest
 import torch
@@ -70,9 +70,10 @@ class _Runner:
             if self.kind != "wgrad" else to_hwnc(torch.randn(n, k, p, q, generator=g))
         return a.to(self.dev), b.to(self.dev)
 
-    def run(self, a, b):
+    def run(self, a, b, acquire: bool):
         lib, sh = L.lib(), L.stream_handle()
-        S, A = ctypes.byref(self.shp), ctypes.byref(self.a)
+        algo = self.a.with_options(flags=L.ALGO_HANDOFF_ACQUIRE if acquire else 0)
+        S, A = ctypes.byref(self.shp), ctypes.byref(algo)
         if self.kind == "fwd":
             st = L.hwnc_strides(self.n, self.h, self.w, self.c)
             L.check(lib.tspm_conv_fwd(S, A, a.data_ptr(), ctypes.byref(st), b.data_ptr(), self.out.data_ptr(),
@@ -89,27 +90,24 @@ class _Runner:
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1:10]}-{c[10]}")
-def test_sc1_handoff_equals_acquire_under_load(gpu, case, monkeypatch):
+def test_sc1_handoff_equals_acquire_under_load(gpu, case):
     kind, *shp, algo = case
     run = _Runner(kind, *shp, algo, gpu)
     g = torch.Generator().manual_seed(77)
     ins = [run.inputs(g) for _ in range(REPS)]
     # reference: the acquire path, serial, no concurrent load
-    monkeypatch.setenv("TSPM_HANDOFF_ACQUIRE", "1")
-    ref = [run.run(a, b).clone() for a, b in ins]
+    ref = [run.run(a, b, True).clone() for a, b in ins]
     torch.cuda.synchronize()
     # the sc1 path, back to back on the same buffers, beside a streaming second stream
-    monkeypatch.setenv("TSPM_HANDOFF_ACQUIRE", "0")
     big = torch.empty(256 * 1024 * 1024, device=gpu)  # 1 GiB
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(6):
             big.mul_(1.0000001)
-    got = [run.run(a, b) for a, b in ins]
+    got = [run.run(a, b, False) for a, b in ins]
     torch.cuda.synchronize()
     del big
     for i, (x, y) in enumerate(zip(got, ref)):
         bad = (x != y) & ~(torch.isnan(x) & torch.isnan(y))
         assert not bool(bad.any()), f"{kind} {shp} {algo}: launch {i}: {int(bad.sum())} words differ from the acquire path"
-    assert os.environ.get("TSPM_HANDOFF_ACQUIRE") == "0"

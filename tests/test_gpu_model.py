@@ -133,8 +133,11 @@ def test_fused_step_vs_golden_reference(gpu, golden):
     print(tally)
 
 
-@pytest.mark.parametrize("batch", [32, 128])
+@pytest.mark.parametrize("batch", [32, 128, 1024])
 def test_fused_step_vs_oracle(gpu, batch):
+    """The benched fused step (two-stream graph, carried Adam, LDS floor at 64-128) against the forced-decision fp64
+    oracle; batch 1024 = configs[2]'s other per-rank reading (the batch-1024 tuned table: variant-2 kernels, no
+    floor) — flips counted and bounded as at 128 (parity.MAX_FLIP_FRAC)."""
     torch.manual_seed(3)
     ours = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
     opt = tspm_amd.FusedAdam(ours.parameters(), lr=5e-4, weight_decay=1e-4)
@@ -318,7 +321,8 @@ def test_fused_train_step_api_and_state_dict_roundtrip(gpu, tmp_path):
     assert list(loaded["model_state_dict"]) == list(ref.state_dict())
     for k, v in ref.state_dict().items():
         assert loaded["model_state_dict"][k].shape == v.shape
-    # every BatchNorm of both encoders counted 3 steps (advanced by the head's second launch since ABI 21)
+    # every BatchNorm of both encoders counted 3 steps (the shared nbt counter, bumped by L.counters_add at the end
+    # of each step)
     nbt = {k: int(v) for k, v in loaded["model_state_dict"].items() if k.endswith("num_batches_tracked")}
     assert len(nbt) == sum(isinstance(mm, torch.nn.BatchNorm2d) for mm in m.modules()) and set(nbt.values()) == {3}
     st = loaded["optimizer_state_dict"]["state"][0]
@@ -394,3 +398,36 @@ def test_step_schedules_leave_the_step_bitwise_unchanged(gpu, monkeypatch, knob,
         results.append(torch.cat([p.detach().reshape(-1) for p in ours.parameters()] + bufs + mom).cpu())
         st.close()
     assert torch.equal(results[0], results[1])
+
+
+def test_floored_and_unfloored_steps_interleaved_are_bitwise_the_plain_step(gpu, monkeypatch):
+    """ABI 21: the audio LDS floor is a per-launch tspm_conv_algo field on the step's own audio
+    engine, not library state.  Two floored steps and one unfloored step, built and run in interleaved order (each
+    builds and captures its graph between the others' replays), all end bitwise equal to the plain step — no floor
+    leaks into another step's launches and none is lost."""
+    cfg = [("82000", "fa"), ("0", "pl"), ("82000", "fb")]
+    steps, models, opts = {}, {}, {}
+    for floor, tag in cfg:
+        monkeypatch.setenv("TSPM_SLACK_LDS_FLOOR", floor)
+        torch.manual_seed(23)
+        models[tag] = tspm_amd.AVMNIST(tspm_amd.ResNet18(1, 64), tspm_amd.ResNet34(1, 128), 128, dropout=0.5).to(gpu)
+        opts[tag] = tspm_amd.FusedAdam(models[tag].parameters(), lr=5e-4, weight_decay=1e-4)
+        steps[tag] = tspm_amd.FusedTrainStep(models[tag], opts[tag], None, 64)
+        assert steps[tag].slack_lds_floor == int(floor)
+    monkeypatch.delenv("TSPM_SLACK_LDS_FLOOR")
+    batches = [orc.synthetic_batch(64, seed=70 + i) for i in range(4)]
+    for i, (audio, image, labels, _) in enumerate(batches):
+        order = ("fa", "pl", "fb") if i % 2 == 0 else ("fb", "pl", "fa")
+        for tag in order:
+            steps[tag].step(audio.to(gpu), image.to(gpu), labels.to(gpu))
+            assert steps[tag].eng_a.lds_floor == 0  # the floor is set only while the step enqueues its audio launches
+    torch.cuda.synchronize()
+    res = {}
+    for tag in steps:
+        m, opt = models[tag], opts[tag]
+        bufs = [t.detach().reshape(-1) for mm in m.modules() if isinstance(mm, torch.nn.BatchNorm2d)
+                for t in (mm.running_mean, mm.running_var)]
+        mom = [t for fg in opt.flat_groups() for t in (fg.exp_avg, fg.exp_avg_sq)]
+        res[tag] = torch.cat([p.detach().reshape(-1) for p in m.parameters()] + bufs + mom).cpu()
+        steps[tag].close()
+    assert torch.equal(res["fa"], res["pl"]) and torch.equal(res["fb"], res["pl"])

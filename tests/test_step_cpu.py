@@ -81,3 +81,29 @@ def test_adam_carry_ranges_partition_the_encoder():
     assert sum(j.count for j in jobs) == sum(b - a for a, b in c.carried)
     # the first block (stem side) is never carried: nothing runs after it
     assert c.carried and min(a for a, _ in c.carried) >= opt.g.offsets[2]
+
+
+def test_adam_carry_refuses_blocks_whose_spans_do_not_tile_their_range():
+    """with a parameter order that interleaves another block's parameters into a block's
+    [min, max) flat range, the block is not carried (the foreign elements' gradients may still be in flight); the
+    contiguous blocks still are, and carried + rest still cover every element exactly once."""
+    from tspm_amd.step import AdamCarry
+    params = [torch.zeros(n) for n in (40, 24, 36, 52, 8, 16)]
+    opt = _FakeOpt(params)
+    c = AdamCarry(opt, max_blocks=4, elems_per_block=16)
+    c.ready([params[0], params[2]])  # params[1] (another block's) sits between them
+    assert c.lo is None and c.take(1.0) is None
+    c.ready([params[4], params[5]])  # contiguous tail block
+    assert (c.lo, c.hi) == (opt.g.offsets[4], opt.g.numel)
+    c.ready([params[3], params[1]])  # not adjacent to each other: refused, pending range unchanged
+    assert (c.lo, c.hi) == (opt.g.offsets[4], opt.g.numel)
+    c.ready([params[3]])  # adjacent to the pending range: extends it
+    assert c.lo == opt.g.offsets[3]
+    j = c.take(1.0)
+    assert j.count == opt.g.numel - opt.g.offsets[3]
+    cover = torch.zeros(opt.g.numel, dtype=torch.int32)
+    for a, b in c.carried:
+        cover[a:b] += 1
+    for a, b in c.rest_of([[(0, opt.g.numel)]])[0]:
+        cover[a:b] += 1
+    assert bool((cover == 1).all())
