@@ -469,6 +469,41 @@ int tspm_conv_bwd_adam(const tspm_conv_shape* s, const tspm_conv_algo* dgrad_alg
                        int32_t beta, float* dw, const tspm_adam_job* job, void* ws_d, size_t ws_d_bytes, void* ws_w,
                        size_t ws_w_bytes, tspm_stream_t stream);
 
+/* Round 6 (ABI 21): the BatchNorm backward's partial sums formed by the dgrad epilogue that writes its incoming
+ * gradient.  In the ResNet backward (resnet.py:37-54 under autograd) the gradient of bn1's output is conv2's input
+ * gradient, and the gradient of bn2's output (through the block's ReLU) is the next block's conv1 input gradient
+ * accumulated onto the residual branch; the last-arriving workgroup of each dgrad tile holds those values in
+ * registers.  With bnp set, tspm_conv_bwd_ex's dgrad epilogue also writes, per 32-row tile t and channel c of dx
+ * (after the beta accumulate — dx itself bitwise as without bnp), with g' = dx * [out > 0]:
+ *   part[0][t][c] = sum g',  part[1][t][c] = sum g' (y - mean[c]),  part[2][t][c] = sum g' (y2 - mean2[c]) (y2 set)
+ * — exactly what tspm_bn_bwd's partial pass computes over its own row tiles, so tspm_bn_bwd_apply_part can run the
+ * BN backward's apply (merge + dy) without that pass: one launch fewer per BatchNorm backward.  Needs
+ * (h*w*n) % 32 == 0; out, y, y2 are [h*w*n][c] HWNC like dx. */
+typedef struct tspm_bn_bwd_part {
+  const float* out;    /* the ReLU output that gates the gradient */
+  const float* y;      /* the BN's input (its conv output) */
+  const float* mean;   /* its save_mean [c] */
+  const float* y2;     /* nullable: a second BN fed by the same gradient (the block's downsample branch) */
+  const float* mean2;  /* its save_mean [c] */
+  float* part;         /* [2 or 3][(h*w*n)/32][c] */
+} tspm_bn_bwd_part;
+/* tspm_conv_bwd with an optional carried Adam job (as tspm_conv_bwd_adam; nullable) and optional BN-backward
+ * partial sums of dx (bnp; nullable). */
+int tspm_conv_bwd_ex(const tspm_conv_shape* s, const tspm_conv_algo* dgrad_algo, const tspm_conv_algo* wgrad_algo,
+                     const float* x, const tspm_strides4* x_strides, const float* dy, const float* w, float* dx,
+                     int32_t beta, float* dw, const tspm_adam_job* job, const tspm_bn_bwd_part* bnp, void* ws_d,
+                     size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes, tspm_stream_t stream);
+/* The BN backward's second launch alone (tspm_bn_bwd's k_bn_bwd_apply_m) over partial sums `part` of `tiles` row
+ * tiles ([2 or 3][tiles][c], e.g. from tspm_conv_bwd_ex's bnp; tiles <= 128): every workgroup merges the tiles in
+ * double in a fixed order, writes dgamma / dbeta (first row block) and dy = gamma*invstd*(g' - mean(g') -
+ * xhat*mean(g' xhat)) [dy2 likewise for y2], dres = g' (nullable).  Arguments otherwise as tspm_bn_bwd with g dense
+ * (out required). */
+int tspm_bn_bwd_apply_part(int64_t m, int32_t c, int32_t tiles, const float* part, const float* g, const float* out,
+                           const float* y, const float* mean, const float* invstd, const float* gamma, float* dgamma,
+                           float* dbeta, float* dy, const float* y2, const float* mean2, const float* invstd2,
+                           const float* gamma2, float* dgamma2, float* dbeta2, float* dy2, float* dres,
+                           tspm_stream_t stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Layout / data-stage helpers (collate → device, MML_Suite/data/avmnist.py:186-191,248-277)
  * ----------------------------------------------------------------------------------------------*/

@@ -29,6 +29,8 @@ def build(batch, kw, dev):
     stemw = kw.pop("_stemw", None)  # stem weight-gradient algo override
     bn2 = kw.pop("_bn2", None)      # encoders ("a", "i") whose BN statistics merge in two levels in the conv
     pool = kw.pop("_pool", None)    # False: a separate tspm_avgpool_fwd launch after the last block's apply
+    bnp = kw.pop("_bnp", None)      # encoders ("a", "i") whose BN backward partial sums come from the dgrad epilogue
+    floor = kw.pop("_floor", None)  # the audio encoder's LDS floor (bytes) instead of the default
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
     if stem is not None or stemw is not None:
         from tspm_amd import _lib as L
@@ -40,6 +42,10 @@ def build(batch, kw, dev):
             e._alloc_workspace()
     if pool is not None:
         step.eng_a.fuse_pool = step.eng_i.fuse_pool = bool(pool)
+    if bnp is not None:
+        step.eng_a.bn_dgrad_part, step.eng_i.bn_dgrad_part = "a" in bnp, "i" in bnp
+    if floor is not None:
+        step.slack_lds_floor = int(floor)
     if bn2 is not None:
         step.eng_a.bn_two_level, step.eng_i.bn_two_level = "a" in bn2, "i" in bn2
     feed = bench.corpus_loader(step, batch, 1234, dev, 16384)

@@ -66,6 +66,12 @@ class AdamJob(ctypes.Structure):
                 ("blocks", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class BnBwdPart(Structure):
+    """tspm_bn_bwd_part (ABI 21, round 6): the BN backward's partial sums formed by the dgrad epilogue that writes its
+    incoming gradient (tspm_conv_bwd_ex), consumed by tspm_bn_bwd_apply_part."""
+    _fields_ = [(n, c_void_p) for n in ("out", "y", "mean", "y2", "mean2", "part")]
+
+
 class BnGSrc(Structure):
     """tspm_bn_gsrc (ABI 19): a pooling layer's output gradient as the BN backward's gradient source."""
     _fields_ = [(n, c_int32) for n in ("kind", "n", "h", "w", "p", "q", "npos", "ldg")] + \
@@ -150,6 +156,9 @@ _SIGS = {
     "tspm_conv_bwd_adam": (c_int32, [_P] * 8 + [c_int32, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_apply_maxpool": (c_int32, [c_int32] * 4 + [_P] * 5 + [c_int32, c_float, _P, _P, _P, c_int32, c_int32, _P]),
     "tspm_bn_bwd_src": (c_int32, [c_int64, c_int32, POINTER(BnGSrc)] + [_P] * 17 + [c_size_t, _P]),
+    # round 6: the BN backward's partial sums in the producing dgrad's epilogue, and the apply launch alone
+    "tspm_conv_bwd_ex": (c_int32, [_P] * 8 + [c_int32, _P, _P, POINTER(BnBwdPart), _P, c_size_t, _P, c_size_t, _P]),
+    "tspm_bn_bwd_apply_part": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 18 + [_P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),

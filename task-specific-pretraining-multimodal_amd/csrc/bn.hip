@@ -987,6 +987,34 @@ int bn_bwd_merged(int64_t m, int32_t c, const GS& gs, bool gather, const float* 
 }
 }  // namespace
 
+extern "C" int tspm_bn_bwd_apply_part(int64_t m, int32_t c, int32_t tiles, const float* part, const float* g,
+                                      const float* out, const float* y, const float* mean, const float* invstd,
+                                      const float* gamma, float* dgamma, float* dbeta, float* dy, const float* y2,
+                                      const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
+                                      float* dbeta2, float* dy2, float* dres, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > kMergeTiles || !part || !g || !out || !y || !mean || !invstd ||
+      !gamma || !dy)
+    return TSPM_ERR_INVALID;
+  const bool two = y2 != nullptr;
+  if (two && (!mean2 || !invstd2 || !gamma2 || !dy2)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const GDense gs{g, c};
+  // the apply launch shape of bn_bwd_merged (~512 workgroups, >= 64 rows each)
+  const int cblk = cdiv(c, kChanPerBlock);
+  long long rb = cdiv64(m, std::max(1, 512 / cblk));
+  if (rb < 64) rb = 64;
+  const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
+#define BNB_MP(TW, DR)                                                                                            \
+  hipLaunchKernelGGL((k_bn_bwd_apply_m<true, TW, DR, GDense>), agrid, dim3(256), 0, st, (long long)m, c, tiles, part, \
+                     invstd, gamma, invstd2, gamma2, dgamma, dbeta, dgamma2, dbeta2, gs, out, y, mean, y2, mean2, rb,  \
+                     dy, dy2, dres)
+  if (two) { if (dres) BNB_MP(true, true); else BNB_MP(true, false); }
+  else { if (dres) BNB_MP(false, true); else BNB_MP(false, false); }
+#undef BNB_MP
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
 extern "C" int tspm_bn_bwd_src(int64_t m, int32_t c, const tspm_bn_gsrc* src, const float* out, const float* y,
                                const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                                float* dy, const float* y2, const float* mean2, const float* invstd2,

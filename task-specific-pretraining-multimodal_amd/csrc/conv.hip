@@ -831,7 +831,7 @@ extern "C" int tspm_conv_bwd(const tspm_conv_shape* s, const tspm_conv_algo* dg,
                              tspm_stream_t stream) {
   if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !opts_ok(dg) || !opts_ok(wg)) return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
-  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, nullptr, ws_d, ws_d_bytes, ws_w,
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, nullptr, nullptr, ws_d, ws_d_bytes, ws_w,
                         ws_w_bytes, static_cast<hipStream_t>(stream));
 }
 
@@ -844,8 +844,25 @@ extern "C" int tspm_conv_bwd_adam(const tspm_conv_shape* s, const tspm_conv_algo
                                                                !job->exp_avg_sq || !job->hyper || job->blocks < 1)))
     return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
-  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, job->count > 0 ? job : nullptr, ws_d,
-                        ws_d_bytes, ws_w, ws_w_bytes, static_cast<hipStream_t>(stream));
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, job->count > 0 ? job : nullptr, nullptr,
+                        ws_d, ws_d_bytes, ws_w, ws_w_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int tspm_conv_bwd_ex(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                                const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
+                                int32_t beta, float* dw, const tspm_adam_job* job, const tspm_bn_bwd_part* bnp,
+                                void* ws_d, size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes, tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !opts_ok(dg) || !opts_ok(wg)) return TSPM_ERR_INVALID;
+  if (job && (job->count < 0 || job->blocks < 0 ||
+              (job->count > 0 && (!job->param || !job->grad || !job->exp_avg || !job->exp_avg_sq || !job->hyper ||
+                                  job->blocks < 1))))
+    return TSPM_ERR_INVALID;
+  if (bnp && (!bnp->out || !bnp->y || !bnp->mean || !bnp->part || (bnp->y2 && !bnp->mean2) ||
+              ((long long)s->h * s->w * s->n) % 32 != 0))
+    return TSPM_ERR_INVALID;
+  if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
+  return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, (job && job->count > 0) ? job : nullptr,
+                        bnp, ws_d, ws_d_bytes, ws_w, ws_w_bytes, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs,

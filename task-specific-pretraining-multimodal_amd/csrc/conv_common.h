@@ -17,7 +17,17 @@ struct ConvArgs {
   unsigned* cnt;             // wgrad: per-tile arrival counters (in-launch slab reduction), or null
   int xcd;                   // LDS-staged kernels: XCD-aware workgroup -> tile mapping (1) or identity (0)
   int acq;                   // LDS-staged kernels: agent acquire before reading split-K slabs / BN partials
-                             // (1), or sc1 loads only (0, default; TSPM_HANDOFF_ACQUIRE=1 for A/B)
+                             // (1), or sc1 loads only (0, default; TSPM_ALGO_HANDOFF_ACQUIRE for A/B)
+  // LDS-staged dgrad epilogue (round 6, tspm_conv_bwd_ex): the BatchNorm-backward partial sums of the gradient
+  // being written — g' = dx * [bnb_out > 0], per 32-row tile and channel sum(g'), sum(g' (bnb_y - mean)) [and
+  // sum(g' (bnb_y2 - mean2))] into bnb_part [3][tiles][C] — so the BN backward that consumes dx needs no partial
+  // pass of its own.  bnb_part == nullptr: off.
+  const float* bnb_out;
+  const float* bnb_y;
+  const float* bnb_mean;
+  const float* bnb_y2;
+  const float* bnb_mean2;
+  float* bnb_part;
 };
 
 template <int TM, int TN>
@@ -66,6 +76,59 @@ struct Acc {
           }
         }
       }
+  }
+  // store (or accumulate onto) rows x cols as store() does — bitwise the same dx — and emit the BatchNorm-backward
+  // partial sums of the stored values per 32-row tile and column (ConvArgs.bnb_*): the mask / y / y2 / old-dx
+  // loads of 8 rows are issued together, the two lane halves' 16 rows each combined with one xor shuffle.
+  TSPM_DEV void store_bnb(float* out, int row0, int col0, int rows, int cols, long long ld, int lane,
+                          bool accumulate, const ConvArgs& g) const {
+    const long long plane = (long long)(rows >> 5) * cols;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = col0 + b * 32 + (lane & 31);
+      const bool colok = col < cols;
+      const int c = colok ? col : cols - 1;
+      const float mu = g.bnb_mean[c];
+      const float mu2 = g.bnb_y2 ? g.bnb_mean2[c] : 0.f;
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        float sg = 0.f, sx = 0.f, sx2 = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float old[8], msk[8], yy[8], yy2[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int row = min(row0 + a * 32 + acc_row(h * 8 + j, lane), rows - 1);
+            const long long off = (long long)row * ld + c;
+            old[j] = accumulate ? out[off] : 0.f;
+            msk[j] = g.bnb_out[off];
+            yy[j] = g.bnb_y[off];
+            yy2[j] = g.bnb_y2 ? g.bnb_y2[off] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int row = row0 + a * 32 + acc_row(h * 8 + j, lane);
+            const float val = accumulate ? (old[j] + v[a][b][h * 8 + j]) : v[a][b][h * 8 + j];
+            if (row < rows && colok) {
+              out[(long long)row * ld + col] = val;
+              const float gm = msk[j] > 0.f ? val : 0.f;
+              sg += gm;
+              sx += gm * (yy[j] - mu);
+              sx2 += gm * (yy2[j] - mu2);
+            }
+          }
+        }
+        sg += __shfl_xor(sg, 32, 64);
+        sx += __shfl_xor(sx, 32, 64);
+        sx2 += __shfl_xor(sx2, 32, 64);
+        if (lane < 32 && colok) {
+          float* p = g.bnb_part + (long long)((row0 + a * 32) >> 5) * cols + col;
+          p[0] = sg;
+          p[plane] = sx;
+          if (g.bnb_y2) p[2 * plane] = sx2;
+        }
+      }
+    }
   }
   // split-K combine of the WK waves of one tile through LDS (wave wk > 0 writes, wave 0 sums in
   // order).  Every wave of the workgroup must call this (it contains barriers).
@@ -245,8 +308,8 @@ struct LdsImpl {
                size_t ws_bytes, hipStream_t st);
   bool (*bwd_built)(const LdsAlgo& ad, const LdsAlgo& aw);
   int (*bwd)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
-             const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, void* wsd, size_t wsd_bytes,
-             void* wsw, size_t wsw_bytes, hipStream_t st);
+             const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, const tspm_bn_bwd_part* bnp,
+             void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes, hipStream_t st);
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();

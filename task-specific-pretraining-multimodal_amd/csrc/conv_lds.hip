@@ -677,7 +677,10 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   if (!splitk_reduce<C>(acc, id, lane, slabs, (long long)g.m * Cc, g.splits, g.cnt, row0, col0, g.m, Cc, Cc, lds, bk, g.acq != 0))
     return;
   TSPM_STAMP(tspm_g_stamps_lds, 4);
-  if (id.wk == 0 && col0 < Cc) acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
+  if (id.wk == 0 && col0 < Cc) {
+    if (g.bnb_part) acc.store_bnb(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0, g);
+    else acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
+  }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
 }
 template <class C>
@@ -1110,8 +1113,8 @@ bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
 bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(ad, aw, nullptr); }
 
 int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
-            const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, void* wsd, size_t wsd_bytes,
-            void* wsw, size_t wsw_bytes, hipStream_t st) {
+            const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, const tspm_bn_bwd_part* bnp,
+            void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes, hipStream_t st) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
   if (!slab_fits(ad.splits, (long long)s->h * s->w * s->n, s->c) ||
       !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
@@ -1121,6 +1124,12 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
   L.gd.m = s->h * s->w * s->n;
   L.gd.splits = ad.splits;
   L.gd.beta = beta ? 1 : 0;
+  if (bnp) {  // the BN-backward partial sums of dx in the dgrad epilogue (round 6)
+    if (L.gd.m % 32 != 0 || !bnp->out || !bnp->y || !bnp->mean || !bnp->part || (bnp->y2 && !bnp->mean2))
+      return TSPM_ERR_INVALID;
+    L.gd.bnb_out = bnp->out; L.gd.bnb_y = bnp->y; L.gd.bnb_mean = bnp->mean;
+    L.gd.bnb_y2 = bnp->y2; L.gd.bnb_mean2 = bnp->mean2; L.gd.bnb_part = bnp->part;
+  }
   if (ad.splits > 1) {
     if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
     L.gd.cnt = static_cast<unsigned*>(wsd);

@@ -96,6 +96,9 @@ class BNOp:
     channels: int
     mean: Optional[torch.Tensor] = None      # save_mean  [C]
     invstd: Optional[torch.Tensor] = None    # save_invstd [C]
+    # round 6: the backward's partial sums written by the dgrad epilogue that produces this BN's incoming gradient
+    # (tspm_conv_bwd_ex), [3][rows/32][C]; None when the BN is not eligible (tiles > 128, pooled gradient source)
+    part: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -153,6 +156,12 @@ class EncoderEngine:
         # the pooling backwards folded into the adjacent BN backward (tspm_bn_bwd_src, round 5); TSPM_BN_POOL_SRC=0
         # restores the separate tspm_avgpool_bwd / tspm_maxpool_bwd launches for A/B
         self.pool_src = os.environ.get("TSPM_BN_POOL_SRC", "1") != "0"
+        # the BN backward's partial sums formed in the epilogue of the fused dgrad + wgrad launch that writes the BN's
+        # incoming gradient (tspm_conv_bwd_ex / tspm_bn_bwd_apply_part, round 6) for the BNs of at most 128 32-row
+        # tiles whose gradient a fused backward launch produces: one k_bn_bwd_partial launch fewer per such BN.
+        # TSPM_BN_DGRAD_PART=0 restores the partial pass (A/B)
+        self.bn_dgrad_part = os.environ.get("TSPM_BN_DGRAD_PART", "1") != "0"
+        self._bnp_ready = set()
         # the stem's BN apply + ReLU + max pool forward in one launch (A/B switch TSPM_STEM_FUSE=0)
         self.stem_fuse = os.environ.get("TSPM_STEM_FUSE", "1") != "0"
         # the encoder fc forward (K = 512, 8-16 output tiles) split 8 ways over K: 2.4399 vs 2.4474 ms per step
@@ -214,6 +223,12 @@ class EncoderEngine:
         for bn in self.all_bns():
             bn.mean = torch.empty(bn.channels, **f32)
             bn.invstd = torch.empty(bn.channels, **f32)
+        # dgrad-epilogue partial sums: bn1 of every block (conv2's input gradient) and bn2 of every block but the last
+        # (the next block's conv1 input gradient); 3 planes (the downsample BN shares bn2's gradient)
+        for i, bp in enumerate(self.blocks):
+            for bn, ok in ((bp.bn1, True), (bp.bn2, i + 1 < len(self.blocks))):
+                if ok and bn.rows % 32 == 0 and bn.rows // 32 <= 128:
+                    bn.part = torch.empty(3 * (bn.rows // 32) * bn.channels, **f32)
 
         # backward scratch: grads of block outputs (ping-pong), dy buffers
         max_blk = max(bp.out.numel() for bp in self.blocks)
@@ -464,6 +479,34 @@ class EncoderEngine:
                                 L.ptr(gb2) if bn2 else None, L.ptr(dy2), L.ptr(dres), None, None, 0,
                                 self.ws_bn.data_ptr(), self.ws_bn_bytes, sh), "bn_bwd")
 
+    def _bn_bwd_part(self, bn: BNOp, g, out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None, dres=None,
+                     sh=0):
+        """_bn_bwd whose partial sums the producing dgrad epilogue already wrote (bn.part, tspm_conv_bwd_ex): the
+        apply launch alone (tspm_bn_bwd_apply_part)."""
+        m = bn.module
+        gw, gb = self._grad(m.weight), self._grad(m.bias)
+        if bn2 is not None:
+            m2 = bn2.module
+            gw2, gb2 = self._grad(m2.weight), self._grad(m2.bias)
+        L.check(L.lib().tspm_bn_bwd_apply_part(
+            bn.rows, bn.channels, bn.rows // 32, bn.part.data_ptr(), g.data_ptr(), out_mask.data_ptr(), y.data_ptr(),
+            bn.mean.data_ptr(), bn.invstd.data_ptr(), m.weight.data_ptr(), gw.data_ptr(), gb.data_ptr(), dy.data_ptr(),
+            L.ptr(y2), L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
+            L.ptr(bn2.module.weight) if bn2 else None, L.ptr(gw2) if bn2 else None, L.ptr(gb2) if bn2 else None,
+            L.ptr(dy2), L.ptr(dres), sh), "bn_bwd_apply_part")
+
+    def _bnp_desc(self, bp: "BlockPlan", which: int) -> Optional["L.BnBwdPart"]:
+        """The partial-sum descriptor for bn1 (which=1) or bn2 (which=2) of block ``bp``, or None when that BN takes
+        the partial pass."""
+        bn = bp.bn1 if which == 1 else bp.bn2
+        if not self.bn_dgrad_part or bn.part is None or self.debug_hook is not None:
+            return None
+        if which == 1:
+            return L.BnBwdPart(bp.a1.data_ptr(), bp.y1.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr())
+        two = bp.ds_conv is not None
+        return L.BnBwdPart(bp.out.data_ptr(), bp.y2.data_ptr(), bn.mean.data_ptr(), bp.yd.data_ptr() if two else None,
+                           bp.ds_bn.mean.data_ptr() if two else None, bn.part.data_ptr())
+
     def _bn_bwd_src(self, bn: BNOp, src: "L.BnGSrc", out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None,
                     dres=None, sh=0):
         """_bn_bwd with the incoming gradient formed on the fly from a pooling layer's output gradient
@@ -496,7 +539,7 @@ class EncoderEngine:
             self.conv_timer.end()
 
     def _bwd_pair(self, op: ConvOp, x_ptr: int, strides: L.Strides4, dy: torch.Tensor, dx: torch.Tensor, beta: int,
-                  sh: int, carry_share: float = 0.0) -> bool:
+                  sh: int, carry_share: float = 0.0, bnp: Optional["L.BnBwdPart"] = None) -> bool:
         """Input and weight gradient of ``op`` in one launch (tspm_conv_bwd: the two GEMMs read the same
         dy and are independent, so their workgroups share the grid).  False (nothing launched) when the
         pair is not built in or the tuner found the two separate launches faster; the caller then launches
@@ -514,7 +557,13 @@ class EncoderEngine:
             self.conv_timer.begin(op, "bwd")
         job = self.adam_carry.take(carry_share) if self.adam_carry is not None else None
         ad, aw = self._a(op.algo_dgrad), self._a(op.algo_wgrad)
-        if job is not None:  # an Adam update over earlier-finished parameters rides on this launch (ABI 20)
+        if bnp is not None:  # the consuming BN's partial sums in the dgrad epilogue (+ the carried Adam job, if any)
+            L.check(lib.tspm_conv_bwd_ex(ctypes.byref(op.shape), ctypes.byref(ad), ctypes.byref(aw), x_ptr,
+                                         ctypes.byref(strides), dy.data_ptr(), self._w(op).data_ptr(), dx.data_ptr(),
+                                         beta, gw.data_ptr(), ctypes.byref(job) if job is not None else None,
+                                         ctypes.byref(bnp), self.ws_conv.data_ptr(), self.ws_conv_bytes,
+                                         self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd_ex")
+        elif job is not None:  # an Adam update over earlier-finished parameters rides on this launch (ABI 20)
             L.check(lib.tspm_conv_bwd_adam(ctypes.byref(op.shape), ctypes.byref(ad), ctypes.byref(aw), x_ptr, ctypes.byref(strides), dy.data_ptr(),
                                            self._w(op).data_ptr(), dx.data_ptr(), beta, gw.data_ptr(), ctypes.byref(job),
                                            self.ws_conv.data_ptr(), self.ws_conv_bytes, self.ws_conv2.data_ptr(),
@@ -575,6 +624,7 @@ class EncoderEngine:
         lib = L.lib()
         N = self.N
         if phase in (0, 1):
+            self._bnp_ready = set()
             fc = self.enc.fc
             linear_bwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c, g_emb.data_ptr(), ld_g,
                        fc.weight.data_ptr(), self._grad(fc.weight).data_ptr(),
@@ -608,25 +658,35 @@ class EncoderEngine:
             Gnv = Gn[:n_in]
             d2 = bp.g_y2
             src = pool_src if (phase in (0, 1) and i == len(self.blocks) - 1) else None
+            # bn2's partial sums came with the gradient when the next block's conv1 backward wrote them (round 6)
+            bn2_fn = self._bn_bwd_part if (src is None and id(bp.bn2) in self._bnp_ready) else self._bn_bwd
+            self._bnp_ready.discard(id(bp.bn2))
             if bp.ds_conv is not None:
                 dd = bp.g_yd
                 if src is not None:
                     self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
                 else:
-                    self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+                    bn2_fn(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
             elif src is not None:
                 self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
             else:
                 # identity residual: g' goes straight to the block-input gradient buffer
-                self._bn_bwd(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
+                bn2_fn(bp.bn2, Gv, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
-            if not self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, carry_share=0.5):
+            bnp1 = self._bnp_desc(bp, 1)
+            if self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, carry_share=0.5, bnp=bnp1):
+                bnp1_done = bnp1 is not None
+            else:
                 self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh)
                 self._dgrad(bp.conv2, d2, da1, 0, sh)
+                bnp1_done = False
             d1 = bp.g_y1
-            self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
+            if bnp1_done:
+                self._bn_bwd_part(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
+            else:
+                self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
             if self.debug_hook is not None:
                 self.debug_hook(f"block{i}.g_out", Gv)
                 self.debug_hook(f"block{i}.d_y2", d2)
@@ -636,8 +696,13 @@ class EncoderEngine:
             if bp.ds_conv is not None and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
                 self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
-            # conv1's input gradient accumulates last onto the previous block's output gradient
-            if not self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, carry_share=1.0):
+            # conv1's input gradient accumulates last onto the previous block's output gradient (whose bn2 partial sums
+            # its epilogue forms, round 6)
+            bnp2 = self._bnp_desc(self.blocks[i - 1], 2) if i > 0 else None
+            if self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, carry_share=1.0, bnp=bnp2):
+                if bnp2 is not None:
+                    self._bnp_ready.add(id(self.blocks[i - 1].bn2))
+            else:
                 self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
                 self._dgrad(bp.conv1, d1, Gnv, 1, sh)
             if self.adam_carry is not None:  # this block's parameters are final and read by no later launch
