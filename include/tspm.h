@@ -148,6 +148,20 @@ int32_t tspm_conv_fwd_bn_counters(const tspm_conv_shape* shape, const tspm_conv_
 int64_t tspm_conv_fwd_bn_partial_floats(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 size_t tspm_conv_fwd_workspace(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
 
+/* Round 6 (ABI 21): two independent LDS-staged forwards in ONE launch — the first 3x3 conv of a downsampling
+ * BasicBlock and its 1x1 downsample, which read the same block input (resnet.py:41,50-51).  Each half is exactly
+ * tspm_conv_fwd with its own shape, algo, operands, BN fuse and workspace (outputs, BN statistics and running stats
+ * bitwise those of the two separate calls); the algos must share (tm, tn, wn, wk, variant) — splits and lds_floor
+ * may differ (the launch takes the larger floor).  The two BN fuses need distinct partial / counter buffers and two
+ * split-K halves distinct workspaces.  TSPM_ERR_INVALID (nothing launched) when the pair is not supported. */
+int32_t tspm_conv_fwd_pair_supported(const tspm_conv_shape* s1, const tspm_conv_algo* a1, const tspm_strides4* xs1,
+                                     const tspm_conv_shape* s2, const tspm_conv_algo* a2, const tspm_strides4* xs2);
+int tspm_conv_fwd_pair(const tspm_conv_shape* s1, const tspm_conv_algo* a1, const float* x1,
+                       const tspm_strides4* xs1, const float* w1, float* y1, const tspm_bn_fuse* bn1, void* ws1,
+                       size_t ws1_bytes, const tspm_conv_shape* s2, const tspm_conv_algo* a2, const float* x2,
+                       const tspm_strides4* xs2, const float* w2, float* y2, const tspm_bn_fuse* bn2, void* ws2,
+                       size_t ws2_bytes, tspm_stream_t stream);
+
 /* dx[H,W,N,C] (HWNC) = beta * dx + conv_input_grad(dy[P,Q,N,K], w), beta in {0, 1}.  Workspace
  * (tspm_conv_dgrad_workspace) only for variant-1 split-K, laid out as for the forward. */
 int tspm_conv_dgrad(const tspm_conv_shape* shape, const tspm_conv_algo* algo, const float* dy,
@@ -493,6 +507,21 @@ int tspm_conv_bwd_ex(const tspm_conv_shape* s, const tspm_conv_algo* dgrad_algo,
                      const float* x, const tspm_strides4* x_strides, const float* dy, const float* w, float* dx,
                      int32_t beta, float* dw, const tspm_adam_job* job, const tspm_bn_bwd_part* bnp, void* ws_d,
                      size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes, tspm_stream_t stream);
+/* Round 6: the backward of a downsampling block's second conv (s, dg, wg: its dgrad + wgrad exactly as
+ * tspm_conv_bwd_ex, with the optional bnp) and of the block's 1x1 downsample (s2, dg2, wg2: dgrad with beta 0 into
+ * dx2 + wgrad into dw2) in ONE launch — both read gradients the block's bn2 backward has just written and write
+ * disjoint tensors (resnet.py:41-51 under autograd).  dg2 / wg2 must have dg / wg's (tm, tn, wn, wk, variant);
+ * splits may differ; split-K halves need pairwise distinct workspaces.  job (nullable) as tspm_conv_bwd_adam. */
+int32_t tspm_conv_bwd_quad_supported(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                                     const tspm_strides4* xs, const tspm_conv_shape* s2, const tspm_conv_algo* dg2,
+                                     const tspm_conv_algo* wg2, const tspm_strides4* xs2);
+int tspm_conv_bwd_quad(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg, const float* x,
+                       const tspm_strides4* xs, const float* dy, const float* w, float* dx, int32_t beta, float* dw,
+                       const tspm_bn_bwd_part* bnp, void* ws_d, size_t ws_d_bytes, void* ws_w, size_t ws_w_bytes,
+                       const tspm_conv_shape* s2, const tspm_conv_algo* dg2, const tspm_conv_algo* wg2,
+                       const float* x2, const tspm_strides4* xs2, const float* dy2, const float* w2, float* dx2,
+                       float* dw2, void* ws_d2, size_t ws_d2_bytes, void* ws_w2, size_t ws_w2_bytes,
+                       const tspm_adam_job* job, tspm_stream_t stream);
 /* The BN backward's second launch alone (tspm_bn_bwd's k_bn_bwd_apply_m) over partial sums `part` of `tiles` row
  * tiles ([2 or 3][tiles][c], e.g. from tspm_conv_bwd_ex's bnp; tiles <= 128): every workgroup merges the tiles in
  * double in a fixed order, writes dgamma / dbeta (first row block) and dy = gamma*invstd*(g' - mean(g') -

@@ -159,6 +159,13 @@ _SIGS = {
     # round 6: the BN backward's partial sums in the producing dgrad's epilogue, and the apply launch alone
     "tspm_conv_bwd_ex": (c_int32, [_P] * 8 + [c_int32, _P, _P, POINTER(BnBwdPart), _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_bwd_apply_part": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 18 + [_P]),
+    # round 6: a downsampling block's first conv and its 1x1 downsample in one launch
+    "tspm_conv_fwd_pair_supported": (c_int32, [_P] * 6),
+    "tspm_conv_fwd_pair": (c_int32, [_P] * 7 + [_P, c_size_t] + [_P] * 7 + [_P, c_size_t, _P]),
+    # round 6: a downsampling block's conv2 backward and its downsample's backward in one launch
+    "tspm_conv_bwd_quad_supported": (c_int32, [_P] * 8),
+    "tspm_conv_bwd_quad": (c_int32, [_P] * 8 + [c_int32, _P, _P, _P, c_size_t, _P, c_size_t] + [_P] * 9 +
+                           [_P, c_size_t, _P, c_size_t, _P, _P]),
     "tspm_maxpool_fwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P, c_int64, _P]),
     "tspm_maxpool_bwd": (c_int32, [c_int32] * 9 + [_P, _P, _P, _P]),
     "tspm_avgpool_fwd": (c_int32, [c_int32, c_int32, c_int32, _P, _P, _P]),

@@ -580,11 +580,13 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_m(long long M, int C, int 
   const long long plane = (long long)G * C;
   {
     double a[3][4] = {};
-    if (cok) {
+    // G <= kMergeTiles: one batch of loads; more tiles (tspm_bn_bwd_apply_part, round 6) in further batches of
+    // kMergeTiles — thread (lane, rg) still sums tiles rg, rg + 16, ... in order
+    for (int base = 0; cok && base < G; base += kMergeTiles) {
       f32x4 v[kMergeTiles / 16][3];
 #pragma unroll
       for (int u = 0; u < kMergeTiles / 16; ++u) {  // unconditional loads (tile clamped), then masked
-        const int gt = rg + 16 * u;
+        const int gt = base + rg + 16 * u;
         const bool ok = gt < G;
         const long long off = (long long)min(gt, G - 1) * C + 4 * c4;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -992,7 +994,7 @@ extern "C" int tspm_bn_bwd_apply_part(int64_t m, int32_t c, int32_t tiles, const
                                       const float* gamma, float* dgamma, float* dbeta, float* dy, const float* y2,
                                       const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
                                       float* dbeta2, float* dy2, float* dres, tspm_stream_t stream) {
-  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > kMergeTiles || !part || !g || !out || !y || !mean || !invstd ||
+  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > 8 * kMergeTiles || !part || !g || !out || !y || !mean || !invstd ||
       !gamma || !dy)
     return TSPM_ERR_INVALID;
   const bool two = y2 != nullptr;

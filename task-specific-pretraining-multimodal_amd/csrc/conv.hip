@@ -736,6 +736,36 @@ extern "C" int tspm_conv_fwd(const tspm_conv_shape* s, const tspm_conv_algo* use
   return TSPM_OK;
 }
 
+namespace {
+int bnf_ok(const tspm_bn_fuse* bn) {
+  if (!bn) return 1;
+  if (!bn->partial && bn->counters) return 0;
+  if (bn->counters && (!bn->save_mean || !bn->save_invstd)) return 0;
+  return 1;
+}
+}  // namespace
+
+extern "C" int32_t tspm_conv_fwd_pair_supported(const tspm_conv_shape* s1, const tspm_conv_algo* a1,
+                                                const tspm_strides4* xs1, const tspm_conv_shape* s2,
+                                                const tspm_conv_algo* a2, const tspm_strides4* xs2) {
+  if (!shape_ok(s1) || !shape_ok(s2) || !is_lds(a1) || !is_lds(a2) || a1->variant != a2->variant) return 0;
+  if (a1->tm != a2->tm || a1->tn != a2->tn || a1->wn != a2->wn || a1->wk != a2->wk) return 0;
+  const tspm_detail::LdsImpl& v = lds_of(a1);
+  return (v.fwd_supported(s1, xs1, lds_algo(a1)) && v.fwd_supported(s2, xs2, lds_algo(a2))) ? 1 : 0;
+}
+
+extern "C" int tspm_conv_fwd_pair(const tspm_conv_shape* s1, const tspm_conv_algo* a1, const float* x1,
+                                  const tspm_strides4* xs1, const float* w1, float* y1, const tspm_bn_fuse* bn1,
+                                  void* ws1, size_t ws1_bytes, const tspm_conv_shape* s2, const tspm_conv_algo* a2,
+                                  const float* x2, const tspm_strides4* xs2, const float* w2, float* y2,
+                                  const tspm_bn_fuse* bn2, void* ws2, size_t ws2_bytes, tspm_stream_t stream) {
+  if (!x1 || !w1 || !y1 || !x2 || !w2 || !y2 || !opts_ok(a1) || !opts_ok(a2) || !bnf_ok(bn1) || !bnf_ok(bn2))
+    return TSPM_ERR_INVALID;
+  if (!tspm_conv_fwd_pair_supported(s1, a1, xs1, s2, a2, xs2)) return TSPM_ERR_INVALID;
+  return lds_of(a1).fwd_pair(s1, lds_algo(a1), x1, w1, y1, bn1, ws1, ws1_bytes, s2, lds_algo(a2), x2, w2, y2, bn2, ws2,
+                             ws2_bytes, static_cast<hipStream_t>(stream));
+}
+
 extern "C" size_t tspm_conv_dgrad_workspace(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s) || !is_lds(user)) return 0;
   return lds_of(user).dgrad_workspace(s, lds_algo(user));
@@ -863,6 +893,39 @@ extern "C" int tspm_conv_bwd_ex(const tspm_conv_shape* s, const tspm_conv_algo* 
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, (job && job->count > 0) ? job : nullptr,
                         bnp, ws_d, ws_d_bytes, ws_w, ws_w_bytes, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int32_t tspm_conv_bwd_quad_supported(const tspm_conv_shape* s, const tspm_conv_algo* dg,
+                                                const tspm_conv_algo* wg, const tspm_strides4* xs,
+                                                const tspm_conv_shape* s2, const tspm_conv_algo* dg2,
+                                                const tspm_conv_algo* wg2, const tspm_strides4* xs2) {
+  if (!tspm_conv_bwd_supported(s, dg, wg, xs) || !tspm_conv_bwd_supported(s2, dg2, wg2, xs2)) return 0;
+  if (dg->variant != dg2->variant) return 0;
+  auto same = [](const tspm_conv_algo* a, const tspm_conv_algo* b) {
+    return a->tm == b->tm && a->tn == b->tn && a->wn == b->wn && a->wk == b->wk;
+  };
+  return (same(dg, dg2) && same(wg, wg2)) ? 1 : 0;
+}
+
+extern "C" int tspm_conv_bwd_quad(const tspm_conv_shape* s, const tspm_conv_algo* dg, const tspm_conv_algo* wg,
+                                  const float* x, const tspm_strides4* xs, const float* dy, const float* w, float* dx,
+                                  int32_t beta, float* dw, const tspm_bn_bwd_part* bnp, void* ws_d, size_t ws_d_bytes,
+                                  void* ws_w, size_t ws_w_bytes, const tspm_conv_shape* s2, const tspm_conv_algo* dg2,
+                                  const tspm_conv_algo* wg2, const float* x2, const tspm_strides4* xs2,
+                                  const float* dy2, const float* w2, float* dx2, float* dw2, void* ws_d2,
+                                  size_t ws_d2_bytes, void* ws_w2, size_t ws_w2_bytes, const tspm_adam_job* job,
+                                  tspm_stream_t stream) {
+  if (!shape_ok(s) || !x || !dy || !w || !dx || !dw || !opts_ok(dg) || !opts_ok(wg)) return TSPM_ERR_INVALID;
+  if (!shape_ok(s2) || !x2 || !dy2 || !w2 || !dx2 || !dw2 || !opts_ok(dg2) || !opts_ok(wg2)) return TSPM_ERR_INVALID;
+  if (job && (job->count < 0 || job->blocks < 0 ||
+              (job->count > 0 && (!job->param || !job->grad || !job->exp_avg || !job->exp_avg_sq || !job->hyper ||
+                                  job->blocks < 1))))
+    return TSPM_ERR_INVALID;
+  if (!tspm_conv_bwd_quad_supported(s, dg, wg, xs, s2, dg2, wg2, xs2)) return TSPM_ERR_INVALID;
+  return lds_of(dg).bwd_quad(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, bnp, ws_d, ws_d_bytes, ws_w,
+                             ws_w_bytes, s2, lds_algo(dg2), lds_algo(wg2), x2, dy2, w2, dx2, dw2, ws_d2, ws_d2_bytes,
+                             ws_w2, ws_w2_bytes, (job && job->count > 0) ? job : nullptr,
+                             static_cast<hipStream_t>(stream));
 }
 
 extern "C" int tspm_reduce_slabs(int64_t count, int32_t nslab, int64_t slab_stride, const float* slabs,

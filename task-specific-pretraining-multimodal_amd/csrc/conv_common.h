@@ -310,6 +310,16 @@ struct LdsImpl {
   int (*bwd)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
              const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, const tspm_bn_bwd_part* bnp,
              void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes, hipStream_t st);
+  int (*fwd_pair)(const tspm_conv_shape* s1, const LdsAlgo& a1, const float* x1, const float* w1, float* y1,
+                  const tspm_bn_fuse* bn1, void* ws1, size_t ws1_bytes, const tspm_conv_shape* s2, const LdsAlgo& a2,
+                  const float* x2, const float* w2, float* y2, const tspm_bn_fuse* bn2, void* ws2, size_t ws2_bytes,
+                  hipStream_t st);
+  int (*bwd_quad)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+                  const float* w, float* dx, int beta, float* dw, const tspm_bn_bwd_part* bnp, void* wsd,
+                  size_t wsd_bytes, void* wsw, size_t wsw_bytes, const tspm_conv_shape* s2, const LdsAlgo& ad2,
+                  const LdsAlgo& aw2, const float* x2, const float* dy2, const float* w2, float* dx2, float* dw2,
+                  void* wsd2, size_t wsd2_bytes, void* wsw2, size_t wsw2_bytes, const tspm_adam_job* adam,
+                  hipStream_t st);
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();

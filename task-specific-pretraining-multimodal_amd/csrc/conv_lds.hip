@@ -490,16 +490,16 @@ TSPM_DEV bool splitk_reduce(Acc<C::TM, C::TN>& acc, const WaveId<C>& id, int lan
 // Forward: y[(p,q,n), k] = sum_{valid (r,s), c} x[(p*st-pad+r, q*st-pad+s, n), c] w[k, r, s, c]
 // A image: BM rows (n) x 32 channels (swizzled); B image: BN rows (output channel) x 32 channels.
 // =============================================================================================
+// bk: the tile's coordinates and the row-block count (gx) of this GEMM; gy its column-block count (the launch's own
+// grid for k_fwd_lds, virtual ones when two forwards share a launch — k_fwd_pair_lds)
 template <class C>
-__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
-                                                     const float* __restrict__ w, float* __restrict__ y,
-                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
-  extern __shared__ float lds[];
+TSPM_DEV void fwd_body(const ConvArgs& g, const float* __restrict__ x, const float* __restrict__ w,
+                       float* __restrict__ y, const tspm_bn_fuse& bf, float* __restrict__ slabs, int gw, int ng,
+                       float* lds, const Blk& bk, int gy) {
   TSPM_STAMP(tspm_g_stamps_lds, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const WaveId<C> id;
   const int N = g.n, Cc = g.c, K = g.k, RSC = g.r * g.s * Cc;
-  const Blk bk = grid_blk(g.xcd);
   const int m0 = bk.x * C::BM, n0col = bk.y * C::BN;
   const int pos = m0 / N, nb0 = m0 - pos * N;
   const int pp = pos / g.q, qq = pos - pp * g.q;
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
   if (active) {
     acc.store(y, row0, col0, g.m, K, K, lane, false);
     if (bf.partial)
-      acc.bn_partials(bf.partial, (long long)gridDim.x * C::WM * K, bk.x * C::WM + id.wm, row0, col0, g.m, K,
+      acc.bn_partials(bf.partial, (long long)bk.gx * C::WM * K, bk.x * C::WM + id.wm, row0, col0, g.m, K,
                       lane, bf.counters != nullptr);
   }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
     int* flag = reinterpret_cast<int*>(lds);
     double* red = reinterpret_cast<double*>(lds) + 2;
     double* smu = red + kThreads;
-    const int T = gridDim.x * C::WM;
+    const int T = bk.gx * C::WM;
     const float* part = bf.partial;
     int G = T;
     long long rpt = C::TM * 32;
@@ -578,8 +578,8 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
       // two levels: the last workgroup of each group of gw row blocks merges the group's tiles into
       // one tile of the second array; the last group merges those
       const int grp = bk.x / gw;
-      const int x0 = grp * gw, x1 = min((int)gridDim.x, x0 + gw);
-      if (!last_arriver(bf.counters + gridDim.y + bk.y * ng + grp, (unsigned)(x1 - x0), flag, g.acq != 0)) return;
+      const int x0 = grp * gw, x1 = min(bk.gx, x0 + gw);
+      if (!last_arriver(bf.counters + gy + bk.y * ng + grp, (unsigned)(x1 - x0), flag, g.acq != 0)) return;
       float* part1 = bf.partial + 3LL * T * K;
       bn_merge_level1<true>(g.m, K, T, rpt, bf.partial, x0 * C::WM, x1 * C::WM, n0col, C::BN, part1, ng, grp, red, smu,
                             kThreads);
@@ -587,12 +587,45 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, 
       part = part1;
       G = ng;
       rpt = (long long)gw * C::WM * C::TM * 32;
-    } else if (!last_arriver(bf.counters + bk.y, gridDim.x, flag, g.acq != 0)) {
+    } else if (!last_arriver(bf.counters + bk.y, (unsigned)bk.gx, flag, g.acq != 0)) {
       return;
     }
     bn_merge_block<true>(g.m, K, G, rpt, part, n0col, C::BN, bf.running_mean, bf.running_var, bf.momentum, bf.eps,
                    bf.save_mean, bf.save_invstd, red, smu, kThreads);
   }
+}
+template <class C>
+__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_lds(ConvArgs g, const float* __restrict__ x,
+                                                     const float* __restrict__ w, float* __restrict__ y,
+                                                     tspm_bn_fuse bf, float* __restrict__ slabs, int gw, int ng) {
+  extern __shared__ float lds[];
+  fwd_body<C>(g, x, w, y, bf, slabs, gw, ng, lds, grid_blk(g.xcd), (int)gridDim.y);
+}
+
+// Two independent forwards in ONE launch (round 6): the first conv of a downsampling BasicBlock and its 1x1
+// downsample read the same block input and are independent (resnet.py:41,50-51), so their tiles share a grid —
+// workgroups [0, n1) run the first GEMM's tiles, the rest the second's; each body is k_fwd_lds's, so every output,
+// BN partial and in-launch merge is bitwise that of the separate launch.  Same tile configuration, own splits.
+struct FwdJob {
+  ConvArgs g;
+  const float* x;
+  const float* w;
+  float* y;
+  tspm_bn_fuse bf;
+  float* slabs;
+  int gw, ng, gx, gy;
+};
+template <class C>
+__global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_pair_lds(FwdJob j1, FwdJob j2) {
+  extern __shared__ float lds[];
+  int b = (int)blockIdx.x;
+  const int n1 = j1.gx * j1.gy * j1.g.splits;
+  const FwdJob& j = b < n1 ? j1 : j2;
+  if (b >= n1) b -= n1;
+  const int z = b / (j.gx * j.gy);
+  b -= z * j.gx * j.gy;
+  const int yb = b / j.gx;
+  fwd_body<C>(j.g, j.x, j.w, j.y, j.bf, j.slabs, j.gw, j.ng, lds, Blk{b - yb * j.gx, yb, z, j.gx}, j.gy);
 }
 
 // =============================================================================================
@@ -842,6 +875,46 @@ __global__ __launch_bounds__(kBlock, (min_waves2<CD, CW>())) void k_bwd_lds(Conv
   }
 }
 
+// The backward of a downsampling block's second conv and of its 1x1 downsample in ONE launch (round 6): both read
+// gradients the block's bn2 backward has just written (d_y2 and d_yd) and write disjoint tensors (conv2's input
+// gradient and the block-input gradient that conv1's data gradient later accumulates onto), so their four GEMMs —
+// the two weight gradients, then the two data gradients — share a grid, each body k_bwd_lds's (same tile
+// configurations, own split counts); carried-Adam workgroups first, as k_bwd_lds.
+struct BwdHalf {
+  ConvArgs gd, gw;
+  const float *dy, *w, *x;
+  float *dx, *dw, *slabs_d, *slabs_w;
+  int dgx, dgy, wgx, wgy;
+};
+template <class CD, class CW>
+__global__ __launch_bounds__(kBlock, (min_waves2<CD, CW>())) void k_bwd_quad_lds(BwdHalf h1, BwdHalf h2,
+                                                                                AdamJobArgs aj, int naj) {
+  extern __shared__ float lds[];
+  if ((int)blockIdx.x < naj) {
+    adam_job_body(aj, (int)blockIdx.x, naj);
+    return;
+  }
+  int b = (int)blockIdx.x - naj;
+  const int nw1 = h1.wgx * h1.wgy * h1.gw.splits, nw2 = h2.wgx * h2.wgy * h2.gw.splits;
+  const int nd1 = h1.dgx * h1.dgy * h1.gd.splits;
+  if (b < nw1 + nw2) {
+    const BwdHalf& h = b < nw1 ? h1 : h2;
+    if (b >= nw1) b -= nw1;
+    const int z = b / (h.wgx * h.wgy);
+    b -= z * h.wgx * h.wgy;
+    const int y = b / h.wgx;
+    wgrad_body<CW>(h.gw, h.x, h.dy, h.dw, h.slabs_w, lds, Blk{b - y * h.wgx, y, z, h.wgx});
+  } else {
+    b -= nw1 + nw2;
+    const BwdHalf& h = b < nd1 ? h1 : h2;
+    if (b >= nd1) b -= nd1;
+    const int z = b / (h.dgx * h.dgy);
+    b -= z * h.dgx * h.dgy;
+    const int y = b / h.dgx;
+    dgrad_body<CD>(h.gd, h.dy, h.w, h.dx, h.slabs_d, lds, Blk{b - y * h.dgx, y, z, h.dgx});
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -974,44 +1047,96 @@ size_t lds_wgrad_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, s->k, (long long)s->r * s->s * s->c);
 }
 
-int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
-            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
-  ConvArgs g = args_of(s, a);
+// A forward launch's arguments (split-K workspace, BN merge plan); `want` keeps the caller's BN request when the
+// merge cannot run in-launch (then tspm_bn_finalize follows the launch)
+int fwd_job(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, FwdJob& j, tspm_bn_fuse& want) {
+  j = FwdJob{};
+  j.g = args_of(s, a);
+  ConvArgs& g = j.g;
   g.m = s->p * s->q * s->n;
   g.splits = a.splits;
   if (!slab_fits(a.splits, g.m, s->k)) return TSPM_ERR_INVALID;
-  float* slabs = nullptr;
   if (a.splits > 1) {
     if (!ws || ws_bytes < lds_fwd_workspace(s, a)) return TSPM_ERR_WORKSPACE;
     g.cnt = static_cast<unsigned*>(ws);
-    slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
+    j.slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + TSPM_COUNTER_BYTES);
   }
   tspm_bn_fuse bf{};
   if (bn) bf = *bn;
-  const int bm = bm_of(a), bnn = bn_of(a);
-  const dim3 grid(g.m / bm, cdiv(s->k, bnn), a.splits);
-  if ((size_t)grid.x * grid.y > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
+  j.gx = g.m / bm_of(a);
+  j.gy = cdiv(s->k, bn_of(a));
+  if ((size_t)j.gx * j.gy > TSPM_COUNTER_BYTES / sizeof(unsigned) && a.splits > 1) return TSPM_ERR_INVALID;
   // in-launch BN merge: one level when each merging thread reads few tiles, two levels when the
   // caller's buffers allow it (tspm_bn_fuse.counters_len / partial_floats), else tspm_bn_finalize
-  const int tiles = (int)grid.x * a.wm;
+  const int tiles = j.gx * a.wm;
   const BnLevels lv = bn_levels(s, a);
-  const tspm_bn_fuse want = bf;
+  want = bf;
   if (bf.counters && lv.ng != 0) {
-    const bool room = lv.ng > 0 && bf.counters_len >= (long long)grid.y * (1 + lv.ng) &&
+    const bool room = lv.ng > 0 && bf.counters_len >= (long long)j.gy * (1 + lv.ng) &&
                       bf.partial_floats >= 3LL * (tiles + lv.ng) * s->k;
     if (!room) bf.counters = nullptr;
   }
-  const int gw = bf.counters ? lv.gw : 0, ng = bf.counters ? lv.ng : 0;
-  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, bf.counters != nullptr), a);
-#define TSPM_FWD(CFG) hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, g, x, w, y, bf, slabs, gw, ng)
+  j.gw = bf.counters ? lv.gw : 0;
+  j.ng = bf.counters ? lv.ng : 0;
+  j.bf = bf;
+  j.x = x; j.w = w; j.y = y;
+  return TSPM_OK;
+}
+int fwd_finalize(const tspm_conv_shape* s, const LdsAlgo& a, const FwdJob& j, const tspm_bn_fuse& want,
+                 hipStream_t st) {
+  if (want.counters && !j.bf.counters)
+    return tspm_bn_finalize(j.g.m, s->k, j.gx * a.wm, a.tm * 32, want.partial, want.running_mean, want.running_var,
+                            want.momentum, want.eps, want.save_mean, want.save_invstd, st);
+  return TSPM_OK;
+}
+
+int lds_fwd(const tspm_conv_shape* s, const LdsAlgo& a, const float* x, const float* w, float* y,
+            const tspm_bn_fuse* bn, void* ws, size_t ws_bytes, hipStream_t st) {
+  FwdJob j;
+  tspm_bn_fuse want;
+  const int e = fwd_job(s, a, x, w, y, bn, ws, ws_bytes, j, want);
+  if (e != TSPM_OK) return e;
+  const dim3 grid(j.gx, j.gy, a.splits);
+  const size_t lds = tspm_detail::lds_with_floor(lds_bytes(a, j.bf.counters != nullptr), a);
+#define TSPM_FWD(CFG) \
+  hipLaunchKernelGGL(k_fwd_lds<CFG>, grid, dim3(kBlock), lds, st, j.g, x, w, y, j.bf, j.slabs, j.gw, j.ng)
   const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD) }();
 #undef TSPM_FWD
   if (rc != TSPM_OK) return rc;
   TSPM_LAUNCH_CHECK();
-  if (want.counters && !bf.counters)
-    return tspm_bn_finalize(g.m, s->k, tiles, a.tm * 32, want.partial, want.running_mean, want.running_var,
-                            want.momentum, want.eps, want.save_mean, want.save_invstd, st);
-  return TSPM_OK;
+  return fwd_finalize(s, a, j, want, st);
+}
+
+// two forwards of the same tile configuration in one launch (k_fwd_pair_lds); the caller checked support
+int lds_fwd_pair(const tspm_conv_shape* s1, const LdsAlgo& a1, const float* x1, const float* w1, float* y1,
+                 const tspm_bn_fuse* bn1, void* ws1, size_t ws1_bytes, const tspm_conv_shape* s2, const LdsAlgo& a2,
+                 const float* x2, const float* w2, float* y2, const tspm_bn_fuse* bn2, void* ws2, size_t ws2_bytes,
+                 hipStream_t st) {
+  if (a1.tm != a2.tm || a1.tn != a2.tn || a1.wm != a2.wm || a1.wn != a2.wn || a1.wk != a2.wk) return TSPM_ERR_INVALID;
+  if (a1.splits > 1 && a2.splits > 1 && ws1 == ws2) return TSPM_ERR_INVALID;  // counters / slabs would collide
+  FwdJob j1, j2;
+  tspm_bn_fuse want1, want2;
+  int e = fwd_job(s1, a1, x1, w1, y1, bn1, ws1, ws1_bytes, j1, want1);
+  if (e != TSPM_OK) return e;
+  e = fwd_job(s2, a2, x2, w2, y2, bn2, ws2, ws2_bytes, j2, want2);
+  if (e != TSPM_OK) return e;
+  if (j1.bf.counters && j2.bf.counters && j1.bf.counters == j2.bf.counters) return TSPM_ERR_INVALID;
+  if (j1.bf.partial && j1.bf.partial == j2.bf.partial) return TSPM_ERR_INVALID;
+  const long long nblk = (long long)j1.gx * j1.gy * a1.splits + (long long)j2.gx * j2.gy * a2.splits;
+  LdsAlgo af = a1;
+  af.floor = std::max(a1.floor, a2.floor);
+  const size_t lds = tspm_detail::lds_with_floor(
+      std::max(lds_bytes(a1, j1.bf.counters != nullptr), lds_bytes(a2, j2.bf.counters != nullptr)), af);
+  const LdsAlgo& a = a1;
+#define TSPM_FWD2(CFG) hipLaunchKernelGGL(k_fwd_pair_lds<CFG>, dim3((unsigned)nblk), dim3(kBlock), lds, st, j1, j2)
+  const int rc = [&]() -> int { TSPM_LDS_DISPATCH(TSPM_FWD2) }();
+#undef TSPM_FWD2
+  if (rc != TSPM_OK) return rc;
+  TSPM_LAUNCH_CHECK();
+  e = fwd_finalize(s1, a1, j1, want1, st);
+  if (e != TSPM_OK) return e;
+  return fwd_finalize(s2, a2, j2, want2, st);
 }
 
 int lds_dgrad(const tspm_conv_shape* s, const LdsAlgo& a, const float* dy, const float* w, float* dx, int beta,
@@ -1073,9 +1198,18 @@ struct BwdLaunch {
   hipStream_t st;
   AdamJobArgs aj;
   int naj;
+  const BwdHalf* second;  // k_bwd_quad_lds: the downsample's backward in the same launch (nullptr: k_bwd_lds)
 };
 template <class CD, class CW>
 void bwd_go(const BwdLaunch& L) {
+  if (L.second) {
+    const BwdHalf h1{L.gd, L.gw, L.dy, L.w, L.x, L.dx, L.dw, L.slabs_d, L.slabs_w, L.dgx, L.dgy, L.wgx, L.wgy};
+    const BwdHalf& h2 = *L.second;
+    const int nblk = h1.wgx * h1.wgy * h1.gw.splits + h2.wgx * h2.wgy * h2.gw.splits + h1.dgx * h1.dgy * h1.gd.splits +
+                     h2.dgx * h2.dgy * h2.gd.splits + L.naj;
+    hipLaunchKernelGGL((k_bwd_quad_lds<CD, CW>), dim3(nblk), dim3(kBlock), L.lds, L.st, h1, h2, L.aj, L.naj);
+    return;
+  }
   const int nblk = L.wgx * L.wgy * L.gw.splits + L.dgx * L.dgy * L.gd.splits + L.naj;
   hipLaunchKernelGGL((k_bwd_lds<CD, CW>), dim3(nblk), dim3(kBlock), L.lds, L.st, L.gd, L.dy, L.w, L.dx, L.slabs_d,
                      L.dgx, L.dgy, L.gw, L.x, L.dw, L.slabs_w, L.wgx, L.wgy, L.aj, L.naj);
@@ -1112,52 +1246,105 @@ bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
 
 bool lds_bwd_built(const LdsAlgo& ad, const LdsAlgo& aw) { return bwd_dispatch(ad, aw, nullptr); }
 
+// one conv's dgrad + wgrad arguments (split-K workspaces, grid) for k_bwd_lds / k_bwd_quad_lds
+int bwd_half(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+             const float* w, float* dx, int beta, float* dw, const tspm_bn_bwd_part* bnp, void* wsd, size_t wsd_bytes,
+             void* wsw, size_t wsw_bytes, BwdHalf& h) {
+  if (!slab_fits(ad.splits, (long long)s->h * s->w * s->n, s->c) ||
+      !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
+    return TSPM_ERR_INVALID;
+  h = BwdHalf{};
+  h.gd = args_of(s, ad);
+  h.gd.m = s->h * s->w * s->n;
+  h.gd.splits = ad.splits;
+  h.gd.beta = beta ? 1 : 0;
+  if (bnp) {  // the BN-backward partial sums of dx in the dgrad epilogue (round 6)
+    if (h.gd.m % 32 != 0 || !bnp->out || !bnp->y || !bnp->mean || !bnp->part || (bnp->y2 && !bnp->mean2))
+      return TSPM_ERR_INVALID;
+    h.gd.bnb_out = bnp->out; h.gd.bnb_y = bnp->y; h.gd.bnb_mean = bnp->mean;
+    h.gd.bnb_y2 = bnp->y2; h.gd.bnb_mean2 = bnp->mean2; h.gd.bnb_part = bnp->part;
+  }
+  if (ad.splits > 1) {
+    if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
+    h.gd.cnt = static_cast<unsigned*>(wsd);
+    h.slabs_d = reinterpret_cast<float*>(static_cast<char*>(wsd) + TSPM_COUNTER_BYTES);
+  }
+  h.gw = args_of(s, aw);
+  h.gw.m = s->k;
+  h.gw.splits = aw.splits;
+  if (aw.splits > 1) {
+    if (!wsw || wsw_bytes < lds_wgrad_workspace(s, aw)) return TSPM_ERR_WORKSPACE;
+    h.gw.cnt = static_cast<unsigned*>(wsw);
+    h.slabs_w = reinterpret_cast<float*>(static_cast<char*>(wsw) + TSPM_COUNTER_BYTES);
+  }
+  if (ad.splits > 1 && aw.splits > 1 && wsd == wsw) return TSPM_ERR_INVALID;  // counters / slabs would collide
+  h.dgx = h.gd.m / bm_of(ad);
+  h.dgy = cdiv(s->c, bn_of(ad));
+  h.wgx = cdiv(s->k, bm_of(aw));
+  h.wgy = s->r * s->s * s->c / bn_of(aw);
+  const size_t cmax = TSPM_COUNTER_BYTES / sizeof(unsigned);
+  if ((ad.splits > 1 && (size_t)h.dgx * h.dgy > cmax) || (aw.splits > 1 && (size_t)h.wgx * h.wgy > cmax))
+    return TSPM_ERR_INVALID;
+  h.dy = dy; h.w = w; h.x = x; h.dx = dx; h.dw = dw;
+  return TSPM_OK;
+}
+
 int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
             const float* w, float* dx, int beta, float* dw, const tspm_adam_job* adam, const tspm_bn_bwd_part* bnp,
             void* wsd, size_t wsd_bytes, void* wsw, size_t wsw_bytes, hipStream_t st) {
   if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
-  if (!slab_fits(ad.splits, (long long)s->h * s->w * s->n, s->c) ||
-      !slab_fits(aw.splits, s->k, (long long)s->r * s->s * s->c))
-    return TSPM_ERR_INVALID;
+  BwdHalf h;
+  const int e = bwd_half(s, ad, aw, x, dy, w, dx, beta, dw, bnp, wsd, wsd_bytes, wsw, wsw_bytes, h);
+  if (e != TSPM_OK) return e;
   BwdLaunch L{};
-  L.gd = args_of(s, ad);
-  L.gd.m = s->h * s->w * s->n;
-  L.gd.splits = ad.splits;
-  L.gd.beta = beta ? 1 : 0;
-  if (bnp) {  // the BN-backward partial sums of dx in the dgrad epilogue (round 6)
-    if (L.gd.m % 32 != 0 || !bnp->out || !bnp->y || !bnp->mean || !bnp->part || (bnp->y2 && !bnp->mean2))
-      return TSPM_ERR_INVALID;
-    L.gd.bnb_out = bnp->out; L.gd.bnb_y = bnp->y; L.gd.bnb_mean = bnp->mean;
-    L.gd.bnb_y2 = bnp->y2; L.gd.bnb_mean2 = bnp->mean2; L.gd.bnb_part = bnp->part;
-  }
-  if (ad.splits > 1) {
-    if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
-    L.gd.cnt = static_cast<unsigned*>(wsd);
-    L.slabs_d = reinterpret_cast<float*>(static_cast<char*>(wsd) + TSPM_COUNTER_BYTES);
-  }
-  L.gw = args_of(s, aw);
-  L.gw.m = s->k;
-  L.gw.splits = aw.splits;
-  if (aw.splits > 1) {
-    if (!wsw || wsw_bytes < lds_wgrad_workspace(s, aw)) return TSPM_ERR_WORKSPACE;
-    L.gw.cnt = static_cast<unsigned*>(wsw);
-    L.slabs_w = reinterpret_cast<float*>(static_cast<char*>(wsw) + TSPM_COUNTER_BYTES);
-  }
-  if (ad.splits > 1 && aw.splits > 1 && wsd == wsw) return TSPM_ERR_INVALID;  // counters / slabs would collide
-  L.dgx = L.gd.m / bm_of(ad);
-  L.dgy = cdiv(s->c, bn_of(ad));
-  L.wgx = cdiv(s->k, bm_of(aw));
-  L.wgy = s->r * s->s * s->c / bn_of(aw);
-  const size_t cmax = TSPM_COUNTER_BYTES / sizeof(unsigned);
-  if ((ad.splits > 1 && (size_t)L.dgx * L.dgy > cmax) || (aw.splits > 1 && (size_t)L.wgx * L.wgy > cmax))
-    return TSPM_ERR_INVALID;
-  L.dy = dy; L.w = w; L.x = x; L.dx = dx; L.dw = dw;
+  L.gd = h.gd; L.gw = h.gw; L.dy = h.dy; L.w = h.w; L.x = h.x; L.dx = h.dx; L.dw = h.dw;
+  L.slabs_d = h.slabs_d; L.slabs_w = h.slabs_w; L.dgx = h.dgx; L.dgy = h.dgy; L.wgx = h.wgx; L.wgy = h.wgy;
   if (adam) {
     L.aj = AdamJobArgs{adam->param, adam->grad, adam->exp_avg, adam->exp_avg_sq, (long long)adam->count, adam->hyper};
     L.naj = adam->blocks;
   }
   LdsAlgo af = ad;  // one launch: the larger of the two halves' floors
   af.floor = std::max(ad.floor, aw.floor);
+  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)), af);
+  L.st = st;
+  bwd_dispatch(ad, aw, &L);
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
+// conv2's backward and the downsample's in one launch (k_bwd_quad_lds): the downsample's algos take conv2's tile
+// configurations (ad2 / aw2 must match ad / aw except splits and floor); workspaces pairwise distinct when split
+int lds_bwd_quad(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
+                 const float* w, float* dx, int beta, float* dw, const tspm_bn_bwd_part* bnp, void* wsd,
+                 size_t wsd_bytes, void* wsw, size_t wsw_bytes, const tspm_conv_shape* s2, const LdsAlgo& ad2,
+                 const LdsAlgo& aw2, const float* x2, const float* dy2, const float* w2, float* dx2, float* dw2,
+                 void* wsd2, size_t wsd2_bytes, void* wsw2, size_t wsw2_bytes, const tspm_adam_job* adam,
+                 hipStream_t st) {
+  if (!bwd_dispatch(ad, aw, nullptr)) return TSPM_ERR_INVALID;
+  auto same = [](const LdsAlgo& a, const LdsAlgo& b) {
+    return a.tm == b.tm && a.tn == b.tn && a.wm == b.wm && a.wn == b.wn && a.wk == b.wk;
+  };
+  if (!same(ad, ad2) || !same(aw, aw2)) return TSPM_ERR_INVALID;
+  const void* wss[4] = {ad.splits > 1 ? wsd : nullptr, aw.splits > 1 ? wsw : nullptr,
+                        ad2.splits > 1 ? wsd2 : nullptr, aw2.splits > 1 ? wsw2 : nullptr};
+  for (int i = 0; i < 4; ++i)
+    for (int j = i + 1; j < 4; ++j)
+      if (wss[i] && wss[i] == wss[j]) return TSPM_ERR_INVALID;
+  BwdHalf h1, h2;
+  int e = bwd_half(s, ad, aw, x, dy, w, dx, beta, dw, bnp, wsd, wsd_bytes, wsw, wsw_bytes, h1);
+  if (e != TSPM_OK) return e;
+  e = bwd_half(s2, ad2, aw2, x2, dy2, w2, dx2, 0, dw2, nullptr, wsd2, wsd2_bytes, wsw2, wsw2_bytes, h2);
+  if (e != TSPM_OK) return e;
+  BwdLaunch L{};
+  L.gd = h1.gd; L.gw = h1.gw; L.dy = h1.dy; L.w = h1.w; L.x = h1.x; L.dx = h1.dx; L.dw = h1.dw;
+  L.slabs_d = h1.slabs_d; L.slabs_w = h1.slabs_w; L.dgx = h1.dgx; L.dgy = h1.dgy; L.wgx = h1.wgx; L.wgy = h1.wgy;
+  L.second = &h2;
+  if (adam) {
+    L.aj = AdamJobArgs{adam->param, adam->grad, adam->exp_avg, adam->exp_avg_sq, (long long)adam->count, adam->hyper};
+    L.naj = adam->blocks;
+  }
+  LdsAlgo af = ad;
+  af.floor = std::max(std::max(ad.floor, aw.floor), std::max(ad2.floor, aw2.floor));
   L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)), af);
   L.st = st;
   bwd_dispatch(ad, aw, &L);
@@ -1173,7 +1360,8 @@ const LdsImpl& TSPM_LDS_IMPL() {
   static const LdsImpl t{&v::lds_fwd_supported, &v::lds_dgrad_supported, &v::lds_wgrad_supported,
                          &v::lds_fwd_workspace, &v::lds_fwd_bn_counters, &v::lds_fwd_bn_partial_floats,
                          &v::lds_dgrad_workspace, &v::lds_wgrad_workspace, &v::lds_fwd,
-                         &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd};
+                         &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd, &v::lds_fwd_pair,
+                         &v::lds_bwd_quad};
   return t;
 }
 }  // namespace tspm_detail

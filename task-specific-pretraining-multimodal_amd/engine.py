@@ -161,7 +161,15 @@ class EncoderEngine:
         # tiles whose gradient a fused backward launch produces: one k_bn_bwd_partial launch fewer per such BN.
         # TSPM_BN_DGRAD_PART=0 restores the partial pass (A/B)
         self.bn_dgrad_part = os.environ.get("TSPM_BN_DGRAD_PART", "1") != "0"
+        # ... for BNs of at most this many 32-row tiles (each apply workgroup merges them all in its prologue)
+        self.bnp_max_tiles = int(os.environ.get("TSPM_BN_DGRAD_PART_TILES", "1024"))
         self._bnp_ready = set()
+        # a downsampling block's first conv and its 1x1 downsample (same input, independent) in ONE forward launch
+        # (tspm_conv_fwd_pair, round 6; the downsample takes the first conv's tile shape); TSPM_FWD_PAIR=0: two launches
+        self.fwd_pair = os.environ.get("TSPM_FWD_PAIR", "1") != "0"
+        # ... and the backward of its second conv together with the downsample's (tspm_conv_bwd_quad, round 6; the
+        # downsample takes conv2's tile shapes); TSPM_BWD_QUAD=0: separate launches
+        self.bwd_quad = os.environ.get("TSPM_BWD_QUAD", "1") != "0"
         # the stem's BN apply + ReLU + max pool forward in one launch (A/B switch TSPM_STEM_FUSE=0)
         self.stem_fuse = os.environ.get("TSPM_STEM_FUSE", "1") != "0"
         # the encoder fc forward (K = 512, 8-16 output tiles) split 8 ways over K: 2.4399 vs 2.4474 ms per step
@@ -227,7 +235,7 @@ class EncoderEngine:
         # (the next block's conv1 input gradient); 3 planes (the downsample BN shares bn2's gradient)
         for i, bp in enumerate(self.blocks):
             for bn, ok in ((bp.bn1, True), (bp.bn2, i + 1 < len(self.blocks))):
-                if ok and bn.rows % 32 == 0 and bn.rows // 32 <= 128:
+                if ok and bn.rows % 32 == 0 and bn.rows // 32 <= 1024:
                     bn.part = torch.empty(3 * (bn.rows // 32) * bn.channels, **f32)
 
         # backward scratch: grads of block outputs (ping-pong), dy buffers
@@ -269,12 +277,24 @@ class EncoderEngine:
         # backward (tspm_conv_bwd) takes a second one for its weight-gradient half
         self.ws_conv = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_conv2 = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        # the downsample half of a quad backward launch (its split-K data / weight gradients)
+        self.ws_conv3 = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
+        self.ws_conv4 = torch.zeros(self.ws_conv_bytes, device=self.device, dtype=torch.uint8)
         self.ws_bn = torch.zeros(self.ws_bn_bytes, device=self.device, dtype=torch.uint8)
         # BN statistics merged in-launch (tspm_conv_fwd_bn_counters / _partial_floats)
         ncnt = max(op.bn_counters() for op in self.all_convs())
         self.bn_cnt = torch.zeros(ncnt, device=self.device, dtype=torch.int32)
         part = max(op.bn_partial_floats() for op in self.all_convs())
         self.bn_part = torch.empty(part, device=self.device, dtype=torch.float32)
+        # the downsample half of a paired forward launch merges its BN statistics in buffers of its own
+        ds = [bp.ds_conv for bp in self.blocks if bp.ds_conv is not None]
+        for bp in self.blocks:
+            if bp.ds_conv is not None:
+                bp.ds_pair_algo = self._pair_algo(bp)
+        ncnt2 = max([self._ds_fwd_algo_op(bp).bn_counters() for bp in self.blocks if bp.ds_conv is not None] + [1])
+        part2 = max([self._ds_fwd_algo_op(bp).bn_partial_floats() for bp in self.blocks if bp.ds_conv is not None] + [1])
+        self.bn_cnt2 = torch.zeros(ncnt2, device=self.device, dtype=torch.int32)
+        self.bn_part2 = torch.empty(part2, device=self.device, dtype=torch.float32)
 
     def set_algos(self, table: Dict[Tuple, Tuple[int, int, int, int, int]]) -> None:
         """Override tile configs: key (kind, n,h,w,c,k,r,s,stride) -> (tm, tn, wm, wn, splits)."""
@@ -320,12 +340,43 @@ class EncoderEngine:
         if self.conv_timer:
             self.conv_timer.end()
 
-    def _bnf(self, bn: BNOp) -> L.BnFuse:
+    def _bnf(self, bn: BNOp, second: bool = False) -> L.BnFuse:
         m = bn.module
-        return L.BnFuse(self.bn_part.data_ptr(), self.bn_cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
+        part, cnt = (self.bn_part2, self.bn_cnt2) if second else (self.bn_part, self.bn_cnt)
+        return L.BnFuse(part.data_ptr(), cnt.data_ptr(), L.ptr(m.running_mean), L.ptr(m.running_var),
                         BN_MOMENTUM if m.momentum is None else m.momentum, m.eps, bn.mean.data_ptr(),
-                        bn.invstd.data_ptr(), self.bn_cnt.numel() if self.bn_two_level else 0, 0,
-                        self.bn_part.numel() if self.bn_two_level else 0)
+                        bn.invstd.data_ptr(), cnt.numel() if self.bn_two_level else 0, 0,
+                        part.numel() if self.bn_two_level else 0)
+
+    def _pair_algo(self, bp: "BlockPlan") -> L.ConvAlgo:
+        """The downsample's algo inside the paired launch: the first conv's tile shape, the downsample's own tuned
+        split count when its tuned tile is the same, else no split."""
+        a1, ad = bp.conv1.algo_fwd, bp.ds_conv.algo_fwd
+        same = (a1.tm, a1.tn, a1.wn, a1.wk, a1.variant) == (ad.tm, ad.tn, ad.wn, ad.wk, ad.variant)
+        return L.ConvAlgo(a1.tm, a1.tn, a1.wn, a1.wk, ad.splits if same else 1, a1.variant)
+
+    def _ds_fwd_algo_op(self, bp: "BlockPlan") -> ConvOp:
+        return ConvOp(bp.ds_conv.module, bp.ds_conv.shape, algo_fwd=bp.ds_pair_algo)
+
+    def _fwd_pair(self, bp: "BlockPlan", x_ptr: int, strides: L.Strides4, train: bool, sh: int) -> bool:
+        """conv1 and the downsample of block ``bp`` in one launch (tspm_conv_fwd_pair); False = not supported for
+        these algos (nothing launched)."""
+        lib = L.lib()
+        c1, cd = bp.conv1, bp.ds_conv
+        a1, ad = self._a(c1.algo_fwd), self._a(bp.ds_pair_algo)
+        if not self.fwd_pair or self.conv_timer or not lib.tspm_conv_fwd_pair_supported(
+                ctypes.byref(c1.shape), ctypes.byref(a1), ctypes.byref(strides), ctypes.byref(cd.shape),
+                ctypes.byref(ad), ctypes.byref(strides)):
+            return False
+        b1 = self._bnf(bp.bn1) if train else None
+        b2 = self._bnf(bp.ds_bn, second=True) if train else None
+        L.check(lib.tspm_conv_fwd_pair(
+            ctypes.byref(c1.shape), ctypes.byref(a1), x_ptr, ctypes.byref(strides), self._w(c1).data_ptr(),
+            bp.y1.data_ptr(), ctypes.byref(b1) if b1 is not None else None, self.ws_conv.data_ptr(), self.ws_conv_bytes,
+            ctypes.byref(cd.shape), ctypes.byref(ad), x_ptr, ctypes.byref(strides), self._w(cd).data_ptr(),
+            bp.yd.data_ptr(), ctypes.byref(b2) if b2 is not None else None, self.ws_conv2.data_ptr(),
+            self.ws_conv_bytes, sh), "conv_fwd_pair")
+        return True
 
     def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
         """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
@@ -421,7 +472,10 @@ class EncoderEngine:
             pool = self.pooled if (bp is self.blocks[-1] and self.fuse_pool) else None
             s1 = bp.conv1.shape
             xs_in = L.hwnc_strides(N, s1.h, s1.w, s1.c)
-            if train:
+            paired = bp.ds_conv is not None and self._fwd_pair(bp, xin.data_ptr(), xs_in, train, sh)
+            if paired:
+                pass
+            elif train:
                 self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
             else:
                 self._conv_fwd(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
@@ -433,7 +487,9 @@ class EncoderEngine:
             else:
                 self._conv_fwd(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             if bp.ds_conv is not None:
-                if train:
+                if paired:
+                    pass
+                elif train:
                     self._conv_bn(bp.ds_conv, bp.ds_bn, xin.data_ptr(), xs_in, bp.yd, sh)
                 else:
                     self._conv_fwd(bp.ds_conv, xin.data_ptr(), xs_in, bp.yd, sh)
@@ -499,7 +555,7 @@ class EncoderEngine:
         """The partial-sum descriptor for bn1 (which=1) or bn2 (which=2) of block ``bp``, or None when that BN takes
         the partial pass."""
         bn = bp.bn1 if which == 1 else bp.bn2
-        if not self.bn_dgrad_part or bn.part is None or self.debug_hook is not None:
+        if not self.bn_dgrad_part or bn.part is None or self.debug_hook is not None or bn.rows // 32 > self.bnp_max_tiles:
             return None
         if which == 1:
             return L.BnBwdPart(bp.a1.data_ptr(), bp.y1.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr())
@@ -575,6 +631,44 @@ class EncoderEngine:
                                       self.ws_conv2.data_ptr(), self.ws_conv_bytes, sh), "conv_bwd")
         if self.conv_timer:
             self.conv_timer.end()
+        return True
+
+    def _quad_algos(self, bp: "BlockPlan") -> Tuple[L.ConvAlgo, L.ConvAlgo]:
+        """The downsample's (dgrad, wgrad) algos inside a quad launch: conv2's tile shapes, no dgrad split (one 1x1
+        tap), conv2's weight-gradient split (the same reduction over the output rows)."""
+        d, w = bp.conv2.algo_dgrad, bp.conv2.algo_wgrad
+        return (L.ConvAlgo(d.tm, d.tn, d.wn, d.wk, 1, d.variant), L.ConvAlgo(w.tm, w.tn, w.wn, w.wk, w.splits, w.variant))
+
+    def _bwd_quad(self, bp: "BlockPlan", xin: torch.Tensor, xs_in: L.Strides4, d2, da1, dd, Gnv, sh: int,
+                  bnp: Optional["L.BnBwdPart"]) -> bool:
+        """conv2's input + weight gradient (with bn1's partial sums when bnp) and the downsample's input gradient (into
+        the block-input gradient, beta 0) + weight gradient in ONE launch (tspm_conv_bwd_quad); False = not supported
+        (nothing launched)."""
+        lib = L.lib()
+        c2, cd = bp.conv2, bp.ds_conv
+        s2 = c2.shape
+        xs_a1 = L.hwnc_strides(self.N, s2.h, s2.w, s2.c)
+        ad, aw = self._a(c2.algo_dgrad), self._a(c2.algo_wgrad)
+        qd, qw = self._quad_algos(bp)
+        qd, qw = self._a(qd), self._a(qw)
+        if c2.bwd_fused is None:  # decided once, as _bwd_pair does: the eager and the captured steps agree
+            c2.bwd_fused = bool(lib.tspm_conv_bwd_supported(ctypes.byref(s2), ctypes.byref(c2.algo_dgrad),
+                                                            ctypes.byref(c2.algo_wgrad), ctypes.byref(xs_a1)))
+        if (not self.bwd_quad or self.conv_timer or not c2.bwd_fused or
+                not lib.tspm_conv_bwd_quad_supported(ctypes.byref(s2), ctypes.byref(ad), ctypes.byref(aw),
+                                                     ctypes.byref(xs_a1), ctypes.byref(cd.shape), ctypes.byref(qd),
+                                                     ctypes.byref(qw), ctypes.byref(xs_in))):
+            return False
+        g2, gd = self._grad(c2.module.weight), self._grad(cd.module.weight)
+        job = self.adam_carry.take(0.5) if self.adam_carry is not None else None
+        b = self.ws_conv_bytes
+        L.check(lib.tspm_conv_bwd_quad(
+            ctypes.byref(s2), ctypes.byref(ad), ctypes.byref(aw), bp.a1.data_ptr(), ctypes.byref(xs_a1), d2.data_ptr(),
+            self._w(c2).data_ptr(), da1.data_ptr(), 0, g2.data_ptr(), ctypes.byref(bnp) if bnp is not None else None,
+            self.ws_conv.data_ptr(), b, self.ws_conv2.data_ptr(), b, ctypes.byref(cd.shape), ctypes.byref(qd),
+            ctypes.byref(qw), xin.data_ptr(), ctypes.byref(xs_in), dd.data_ptr(), self._w(cd).data_ptr(), Gnv.data_ptr(),
+            gd.data_ptr(), self.ws_conv3.data_ptr(), b, self.ws_conv4.data_ptr(), b,
+            ctypes.byref(job) if job is not None else None, sh), "conv_bwd_quad")
         return True
 
     def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:
@@ -676,7 +770,11 @@ class EncoderEngine:
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             da1 = self.da1[:n_out]
             bnp1 = self._bnp_desc(bp, 1)
-            if self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, carry_share=0.5, bnp=bnp1):
+            # downsampling block: conv2's backward and the downsample's in one launch when supported (round 6)
+            quad = bp.ds_conv is not None and self._bwd_quad(bp, xin, xs_in, d2, da1, dd, Gnv, sh, bnp1)
+            if quad:
+                bnp1_done = bnp1 is not None
+            elif self._bwd_pair(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, da1, 0, sh, carry_share=0.5, bnp=bnp1):
                 bnp1_done = bnp1 is not None
             else:
                 self._wgrad(bp.conv2, bp.a1.data_ptr(), xs_a1, d2, sh)
@@ -693,7 +791,7 @@ class EncoderEngine:
                 self.debug_hook(f"block{i}.d_a1", da1)
                 self.debug_hook(f"block{i}.d_y1", d1)
             # the downsample's input gradient overwrites Gnv before conv1's accumulates onto it
-            if bp.ds_conv is not None and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
+            if bp.ds_conv is not None and not quad and not self._bwd_pair(bp.ds_conv, xin.data_ptr(), xs_in, dd, Gnv, 0, sh):
                 self._wgrad(bp.ds_conv, xin.data_ptr(), xs_in, dd, sh)
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             # conv1's input gradient accumulates last onto the previous block's output gradient (whose bn2 partial sums

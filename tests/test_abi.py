@@ -154,3 +154,32 @@ def test_library_sources_read_no_environment_and_keep_no_mutable_globals():
             if re.match(r"^(static\s+)?(__device__\s+)?(unsigned|int|long|size_t|float|double|bool|char)\b[\w\s\*]*\s\w+\s*(=|;|\[)",
                         line) and "constexpr" not in line and "(" not in line:
                 raise AssertionError(f"{f}: file-scope variable: {line.strip()}")
+
+
+def test_round6_entry_points_validate_before_launch():
+    """The round-6 entry points refuse bad arguments before any launch (no GPU here: an accepted call would fail with
+    TSPM_ERR_LAUNCH = 2, a refused one returns TSPM_ERR_INVALID = 1)."""
+    lib = L.load()
+    # tspm_bn_bwd_apply_part: more tiles than the merge prologue takes, a missing ReLU output
+    assert lib.tspm_bn_bwd_apply_part(512, 256, 1025, *([16] * 10), *([None] * 7), None, None) == 1
+    assert lib.tspm_bn_bwd_apply_part(512, 256, 16, 16, 16, None, *([16] * 7), *([None] * 7), None, None) == 1
+    # tspm_conv_fwd_pair: tile shapes differ; both halves split-K on one workspace
+    s1, s2 = L.ConvShape(128, 4, 4, 128, 256, 3, 3, 2, 1, 2, 2), L.ConvShape(128, 4, 4, 128, 256, 1, 1, 2, 0, 2, 2)
+    xs = L.hwnc_strides(128, 4, 4, 128)
+    a1, a2, a3 = L.ConvAlgo(1, 1, 2, 2, 1, 1), L.ConvAlgo(1, 1, 1, 4, 1, 1), L.ConvAlgo(1, 1, 2, 2, 2, 1)
+    B = ctypes.byref
+    assert not lib.tspm_conv_fwd_pair_supported(B(s1), B(a1), B(xs), B(s2), B(a2), B(xs))
+    assert lib.tspm_conv_fwd_pair_supported(B(s1), B(a1), B(xs), B(s2), B(a3), B(xs))
+    assert lib.tspm_conv_fwd_pair(B(s1), B(a1), 16, B(xs), 16, 16, None, 16, 1 << 30, B(s2), B(a2), 16, B(xs), 16, 16,
+                                  None, 32, 1 << 30, None) == 1
+    assert lib.tspm_conv_fwd_pair(B(s1), B(a3), 16, B(xs), 16, 16, None, 16, 1 << 30, B(s2), B(a3), 16, B(xs), 16, 16,
+                                  None, 16, 1 << 30, None) == 1
+    # tspm_conv_bwd_quad: the downsample's wgrad tile differs from conv2's
+    c2, ds = L.ConvShape(128, 2, 2, 256, 256, 3, 3, 1, 1, 2, 2), L.ConvShape(128, 4, 4, 128, 256, 1, 1, 2, 0, 2, 2)
+    xs2 = L.hwnc_strides(128, 2, 2, 256)
+    ad, aw, aw_other = L.ConvAlgo(1, 1, 2, 2, 1, 1), L.ConvAlgo(1, 1, 2, 1, 1, 1), L.ConvAlgo(1, 1, 1, 4, 1, 1)
+    assert lib.tspm_conv_bwd_quad_supported(B(c2), B(ad), B(aw), B(xs2), B(ds), B(ad), B(aw), B(xs))
+    assert not lib.tspm_conv_bwd_quad_supported(B(c2), B(ad), B(aw), B(xs2), B(ds), B(ad), B(aw_other), B(xs))
+    assert lib.tspm_conv_bwd_quad(B(c2), B(ad), B(aw), 16, B(xs2), 16, 16, 16, 0, 16, None, 16, 1 << 30, 32, 1 << 30,
+                                  B(ds), B(ad), B(aw_other), 16, B(xs), 16, 16, 16, 16, 48, 1 << 30, 64, 1 << 30, None,
+                                  None) == 1
