@@ -1243,8 +1243,10 @@ def main() -> None:
     loss = step.loss.item()
     result = None
     if rank == 0:
-        rl = {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_fwd_lds, k_bwd_lds = dgrad+wgrad, k_dgrad_lds, "
-                                         "k_wgrad_lds, stem k_conv_*), fp32 MFMA 32x32x2",
+        rl = {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_fwd_lds, k_fwd_pair_lds = a downsampling "
+                                         "block's conv1 + 1x1 downsample, k_bwd_lds = dgrad+wgrad, k_bwd_quad_lds = "
+                                         "conv2 + downsample dgrad+wgrad, k_dgrad_lds, k_wgrad_lds, stem k_stem_* / "
+                                         "k_conv_*), fp32 MFMA 32x32x2",
               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": traffic,
               "traffic_unit": "HBM bytes per step of the conv family (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
               "traffic_per_launch": round(traffic / traffic_launches) if traffic else None,

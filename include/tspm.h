@@ -240,6 +240,19 @@ int tspm_bn_apply_pool(int32_t npos, int32_t n, int32_t c, const float* y, const
                        const float* res_mean, const float* res_inv, const float* res_gamma, const float* res_beta,
                        int32_t relu, int32_t eval, float eps, float* out, float* pooled, tspm_stream_t stream);
 
+/* Round 6 (ABI 21): the training-mode apply (as tspm_bn_apply) with the statistics merge of tspm_bn_finalize folded
+ * into its prologue, for convs whose forward cannot merge its partials in-launch (tspm_conv_fwd_bn_inlaunch == 0;
+ * the caller then passes a tspm_bn_fuse without counters so the conv only writes the partials): every workgroup
+ * merges the `tiles` (<= 256) partial tiles of its 16 channels in double in a fixed order, row block 0 writes
+ * save_mean / save_invstd and updates the running statistics (momentum, unbiased variance), and its rows are
+ * normalised.  One launch instead of tspm_bn_finalize + tspm_bn_apply.  c % 16 == 0. */
+int32_t tspm_conv_fwd_bn_inlaunch(const tspm_conv_shape* shape, const tspm_conv_algo* algo);
+int tspm_bn_apply_merge(int64_t m, int32_t c, int32_t tiles, int64_t rows_per_tile, const float* partial,
+                        float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                        float* save_invstd, const float* y, const float* gamma, const float* beta, int32_t res_mode,
+                        const float* res, const float* res_mean, const float* res_invstd, const float* res_gamma,
+                        const float* res_beta, int32_t relu, float* out, tspm_stream_t stream);
+
 /* ABI 19: the stem's BN apply + ReLU with the following MaxPool2d(3, 2, 1) in the same launch (resnet.py:138-140):
  * pooled [p][q][n][c] and its argmax taps idx exactly as tspm_maxpool_fwd over tspm_bn_apply's output, and that
  * output out [h][w][n][c] (nullable; the BN backward's ReLU mask) — bitwise the two launches.  eval != 0: inv is

@@ -31,6 +31,7 @@ def build(batch, kw, dev):
     pool = kw.pop("_pool", None)    # False: a separate tspm_avgpool_fwd launch after the last block's apply
     bnp = kw.pop("_bnp", None)      # encoders ("a", "i") whose BN backward partial sums come from the dgrad epilogue
     floor = kw.pop("_floor", None)  # the audio encoder's LDS floor (bytes) instead of the default
+    am = kw.pop("_am", None)        # the forward BN merge in the apply (tspm_bn_apply_merge) on / off
     bnpt = kw.pop("_bnpt", None)    # the largest BN (in 32-row tiles) whose backward partial sums come from the dgrad
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
     if stem is not None or stemw is not None:
@@ -45,6 +46,8 @@ def build(batch, kw, dev):
         step.eng_a.fuse_pool = step.eng_i.fuse_pool = bool(pool)
     if bnp is not None:
         step.eng_a.bn_dgrad_part, step.eng_i.bn_dgrad_part = "a" in bnp, "i" in bnp
+    if am is not None:
+        step.eng_a.apply_merge = step.eng_i.apply_merge = bool(am)
     if bnpt is not None:
         step.eng_a.bnp_max_tiles = step.eng_i.bnp_max_tiles = int(bnpt)
     if floor is not None:

@@ -162,6 +162,10 @@ _SIGS = {
     # round 6: a downsampling block's first conv and its 1x1 downsample in one launch
     "tspm_conv_fwd_pair_supported": (c_int32, [_P] * 6),
     "tspm_conv_fwd_pair": (c_int32, [_P] * 7 + [_P, c_size_t] + [_P] * 7 + [_P, c_size_t, _P]),
+    # round 6: the forward statistics merge in the apply's prologue
+    "tspm_conv_fwd_bn_inlaunch": (c_int32, [_P, _P]),
+    "tspm_bn_apply_merge": (c_int32, [c_int64, c_int32, c_int32, c_int64, _P, _P, _P, c_float, c_float] + [_P] * 5 +
+                            [c_int32] + [_P] * 5 + [c_int32, _P, _P]),
     # round 6: a downsampling block's conv2 backward and its downsample's backward in one launch
     "tspm_conv_bwd_quad_supported": (c_int32, [_P] * 8),
     "tspm_conv_bwd_quad": (c_int32, [_P] * 8 + [c_int32, _P, _P, _P, c_size_t, _P, c_size_t] + [_P] * 9 +

@@ -160,6 +160,123 @@ __global__ __launch_bounds__(256) void k_bn_apply(long long n4, int C, const flo
   }
 }
 
+// Round 6: the training-mode apply with the statistics merge folded into its prologue, for the layers whose conv
+// forward cannot merge its per-tile partials in-launch (they used a tspm_bn_finalize launch between the conv and the
+// apply).  Workgroup = 16 channels x a block of rows: the 16 x 16 threads first merge the G <= 256 partial tiles
+// {K, mean - K, M2} of their 16 channels in double (thread (cl, gg) takes tiles gg, gg + 16, ... — at most 16, all
+// loaded at once — then a fixed-order sum over the 16 groups; every workgroup derives the same statistics), row
+// block 0 writes save_mean / save_invstd and the running statistics, then the block's rows are normalised as
+// k_bn_apply does (+ReLU, + residual / + BN(downsample)).  One launch instead of finalize + apply.
+constexpr int kApplyMergeTiles = 256;
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void k_bn_apply_merge(long long M, int C, int G, long long rpt,
+                                                        const float* __restrict__ part, float* __restrict__ rmean,
+                                                        float* __restrict__ rvar, float momentum, float eps,
+                                                        float* __restrict__ smean, float* __restrict__ sinv,
+                                                        const float* __restrict__ y, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, const float* __restrict__ res,
+                                                        const float* __restrict__ mean2, const float* __restrict__ inv2,
+                                                        const float* __restrict__ gamma2,
+                                                        const float* __restrict__ beta2, long long rows_per_block,
+                                                        float* __restrict__ out) {
+  __shared__ double red[256];
+  __shared__ double smu[16];
+  __shared__ float ssc[16], ssf[16];
+  const int t = threadIdx.x, cl = t & 15, gg = t >> 4;
+  const int c = blockIdx.y * 16 + cl;
+  const bool cok = c < C;
+  const int cc = cok ? c : C - 1;
+  const long long plane = (long long)G * C;
+  float k0[16], k1[16], k2[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {  // unconditional (clamped) loads, weight 0 past G
+    const long long o = (long long)min(gg + 16 * u, G - 1) * C + cc;
+    k0[u] = part[o];
+    k1[u] = part[plane + o];
+    k2[u] = part[2 * plane + o];
+  }
+  auto nb_of = [&](int g) -> double { return g < G ? (double)min(rpt, M - (long long)g * rpt) : 0.0; };
+  double s = 0.0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) s += nb_of(gg + 16 * u) * ((double)k0[u] + (double)k1[u]);
+  red[t] = s;
+  __syncthreads();
+  if (gg == 0) {
+    double a = red[cl];
+    for (int k = 1; k < 16; ++k) a += red[k * 16 + cl];
+    smu[cl] = a / (double)M;
+  }
+  __syncthreads();
+  const double mean = smu[cl];
+  double q = 0.0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int g = gg + 16 * u;
+    if (g < G) {
+      const double mb = (double)k0[u] + (double)k1[u];
+      q += (double)k2[u] + nb_of(g) * (mb - mean) * (mb - mean);
+    }
+  }
+  __syncthreads();
+  red[t] = q;
+  __syncthreads();
+  if (gg == 0) {
+    double m2 = red[cl];
+    for (int k = 1; k < 16; ++k) m2 += red[k * 16 + cl];
+    const double n = (double)M;
+    double var = m2 / n;
+    if (var < 0.0) var = 0.0;
+    const float fmean = (float)mean, fvar = (float)var;
+    const float inv = 1.0f / sqrtf(fvar + eps);
+    if (cok) {
+      const float sc = gamma[c] * inv;
+      ssc[cl] = sc;
+      ssf[cl] = beta[c] - fmean * sc;
+      if (blockIdx.x == 0) {
+        smean[c] = fmean;
+        sinv[c] = inv;
+        if (rmean) rmean[c] = momentum * fmean + (1.f - momentum) * rmean[c];
+        if (rvar) {
+          const float unb = M > 1 ? (float)(m2 / (n - 1.0)) : fvar;
+          rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // apply: thread = (row, 4 channels); 64 rows per pass
+  const int q4 = t & 3, rr = t >> 2;
+  const int c4 = blockIdx.y * 4 + q4;
+  if (4 * c4 >= C) return;
+  f32x4 sc, sf, sc2 = {0.f, 0.f, 0.f, 0.f}, sf2 = sc2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { sc[j] = ssc[4 * q4 + j]; sf[j] = ssf[4 * q4 + j]; }
+  if (RES == 2) {
+    sc2 = ld4(gamma2 + 4 * c4) * ld4(inv2 + 4 * c4);
+    sf2 = ld4(beta2 + 4 * c4) - ld4(mean2 + 4 * c4) * sc2;
+  }
+  const long long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (long long row = r0 + rr; row < r1; row += 64) {
+    const long long off = row * C + 4 * c4;
+    const f32x4 v = ld4(y + off);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fmaf(v[j], sc[j], sf[j]);
+    if (RES == 1) {
+      o += ld4(res + off);
+    } else if (RES == 2) {
+      const f32x4 v2 = ld4(res + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += fmaf(v2[j], sc2[j], sf2[j]);
+    }
+    if (RELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = relu_f(o[j]);
+    }
+    st4(out + off, o);
+  }
+}
+
 // The stem's BN apply + ReLU with the MaxPool2d(3, 2, 1) that follows it folded in (resnet.py:138-140; round 5):
 // thread = (pooled output (p, q, n), 4 channels).  It forms relu(bn(y)) for the 3 x 3 window (k_bn_apply's
 // arithmetic), keeps the first maximum in row-major window order with NaN winning (k_maxpool_fwd's rule) and
@@ -858,6 +975,36 @@ extern "C" int tspm_bn_apply(int64_t m, int32_t c, const float* y, const float* 
                              tspm_stream_t stream) {
   return bn_apply_common(m, c, y, mean, invstd, gamma, beta, res_mode, res, res_mean, res_invstd, res_gamma,
                          res_beta, relu, out, out_t, ld_t, false, 0.f, stream);
+}
+
+extern "C" int tspm_bn_apply_merge(int64_t m, int32_t c, int32_t tiles, int64_t rows_per_tile, const float* partial,
+                                   float* running_mean, float* running_var, float momentum, float eps,
+                                   float* save_mean, float* save_invstd, const float* y, const float* gamma,
+                                   const float* beta, int32_t res_mode, const float* res, const float* res_mean,
+                                   const float* res_invstd, const float* res_gamma, const float* res_beta,
+                                   int32_t relu, float* out, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || c % 16 || tiles < 1 || tiles > kApplyMergeTiles || rows_per_tile <= 0 || !partial ||
+      !save_mean || !save_invstd || !y || !gamma || !beta || !out)
+    return TSPM_ERR_INVALID;
+  if ((long long)tiles * rows_per_tile < m || (long long)(tiles - 1) * rows_per_tile >= m) return TSPM_ERR_INVALID;
+  if (res_mode < 0 || res_mode > 2 || (res_mode >= 1 && !res)) return TSPM_ERR_INVALID;
+  if (res_mode == 2 && (!res_mean || !res_invstd || !res_gamma || !res_beta)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int cblk = c / 16;
+  long long rb = cdiv64(m, std::max(1, 128 / cblk));  // ~128 workgroups, >= 64 rows each
+  if (rb < 64) rb = 64;
+  const dim3 grid((unsigned)cdiv64(m, rb), cblk);
+#define BN_AM(RES, RELU)                                                                                             \
+  hipLaunchKernelGGL((k_bn_apply_merge<RES, RELU>), grid, dim3(256), 0, st, (long long)m, c, tiles,                  \
+                     (long long)rows_per_tile, partial, running_mean, running_var, momentum, eps, save_mean,          \
+                     save_invstd, y, gamma, beta, res, res_mean, res_invstd, res_gamma, res_beta, rb, out)
+  const bool r = relu != 0;
+  if (res_mode == 0) { if (r) BN_AM(0, true); else BN_AM(0, false); }
+  else if (res_mode == 1) { if (r) BN_AM(1, true); else BN_AM(1, false); }
+  else { if (r) BN_AM(2, true); else BN_AM(2, false); }
+#undef BN_AM
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
 }
 
 extern "C" int tspm_bn_apply_eval(int64_t m, int32_t c, const float* y, const float* running_mean,

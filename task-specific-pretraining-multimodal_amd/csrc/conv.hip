@@ -669,6 +669,17 @@ extern "C" int32_t tspm_conv_fwd_tiles(const tspm_conv_shape* s, const tspm_conv
   return rows > 0 ? cdiv(s->p * s->q * s->n, rows) : 0;
 }
 
+// 1 when tspm_conv_fwd with a BN fuse that has counters (and no two-level buffers) merges the statistics inside
+// the launch, 0 when it follows the launch with tspm_bn_finalize (round 6: the caller may instead pass no counters
+// and merge in the apply, tspm_bn_apply_merge)
+extern "C" int32_t tspm_conv_fwd_bn_inlaunch(const tspm_conv_shape* s, const tspm_conv_algo* user) {
+  if (!shape_ok(s) || is_stem(user)) return 0;
+  if (is_lds(user)) return lds_of(user).fwd_bn_inlaunch(s, lds_algo(user));
+  const Algo al = fwd_algo(s, user);
+  const int tiles = cdiv(s->p * s->q * s->n, al.tm * 32), groups = 2 * al.wk / al.tn;
+  return (cdiv(tiles, groups) <= kMaxFusedMergeIters && inlaunch_enabled()) ? 1 : 0;
+}
+
 extern "C" int32_t tspm_conv_fwd_tile_rows(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   if (!shape_ok(s)) return 0;
   if (is_stem(user)) return tspm_detail::stem_supported(s) ? tspm_detail::stem_tile_rows(s) : 0;

@@ -314,6 +314,7 @@ struct LdsImpl {
                   const tspm_bn_fuse* bn1, void* ws1, size_t ws1_bytes, const tspm_conv_shape* s2, const LdsAlgo& a2,
                   const float* x2, const float* w2, float* y2, const tspm_bn_fuse* bn2, void* ws2, size_t ws2_bytes,
                   hipStream_t st);
+  int (*fwd_bn_inlaunch)(const tspm_conv_shape* s, const LdsAlgo& a);
   int (*bwd_quad)(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, const float* x, const float* dy,
                   const float* w, float* dx, int beta, float* dw, const tspm_bn_bwd_part* bnp, void* wsd,
                   size_t wsd_bytes, void* wsw, size_t wsw_bytes, const tspm_conv_shape* s2, const LdsAlgo& ad2,

@@ -1031,6 +1031,7 @@ bool lds_wgrad_supported(const tspm_conv_shape* s, const tspm_strides4* xs, cons
 size_t lds_fwd_workspace(const tspm_conv_shape* s, const LdsAlgo& a) {
   return splitk_ws(a.splits, (long long)s->p * s->q * s->n, s->k);
 }
+int lds_fwd_bn_inlaunch(const tspm_conv_shape* s, const LdsAlgo& a) { return bn_levels(s, a).ng == 0 ? 1 : 0; }
 int lds_fwd_bn_counters(const tspm_conv_shape* s, const LdsAlgo& a) {
   const BnLevels lv = bn_levels(s, a);
   return cdiv(s->k, bn_of(a)) * (1 + std::max(lv.ng, 0));
@@ -1361,7 +1362,7 @@ const LdsImpl& TSPM_LDS_IMPL() {
                          &v::lds_fwd_workspace, &v::lds_fwd_bn_counters, &v::lds_fwd_bn_partial_floats,
                          &v::lds_dgrad_workspace, &v::lds_wgrad_workspace, &v::lds_fwd,
                          &v::lds_dgrad, &v::lds_wgrad, &v::lds_bwd_built, &v::lds_bwd, &v::lds_fwd_pair,
-                         &v::lds_bwd_quad};
+                         &v::lds_fwd_bn_inlaunch, &v::lds_bwd_quad};
   return t;
 }
 }  // namespace tspm_detail

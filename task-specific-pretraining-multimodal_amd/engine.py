@@ -57,6 +57,7 @@ class ConvOp:
     algo_dgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
     algo_wgrad: L.ConvAlgo = field(default_factory=L.ConvAlgo)
     bwd_fused: Optional[bool] = None  # tspm_conv_bwd_supported for (algo_dgrad, algo_wgrad); None = not asked
+    bn_inlaunch: Optional[bool] = None  # tspm_conv_fwd_bn_inlaunch for algo_fwd; None = not asked
 
     @property
     def rows_out(self) -> int:
@@ -96,6 +97,8 @@ class BNOp:
     channels: int
     mean: Optional[torch.Tensor] = None      # save_mean  [C]
     invstd: Optional[torch.Tensor] = None    # save_invstd [C]
+    # round 6: (tiles, rows per tile) of partials the conv forward left for the apply to merge (tspm_bn_apply_merge)
+    pending: Optional[Tuple[int, int]] = None
     # round 6: the backward's partial sums written by the dgrad epilogue that produces this BN's incoming gradient
     # (tspm_conv_bwd_ex), [3][rows/32][C]; None when the BN is not eligible (tiles > 128, pooled gradient source)
     part: Optional[torch.Tensor] = None
@@ -167,6 +170,9 @@ class EncoderEngine:
         # a downsampling block's first conv and its 1x1 downsample (same input, independent) in ONE forward launch
         # (tspm_conv_fwd_pair, round 6; the downsample takes the first conv's tile shape); TSPM_FWD_PAIR=0: two launches
         self.fwd_pair = os.environ.get("TSPM_FWD_PAIR", "1") != "0"
+        # the forward BN statistics of convs that cannot merge them in-launch merged in the apply's prologue
+        # (tspm_bn_apply_merge, round 6) instead of a tspm_bn_finalize launch; TSPM_BN_APPLY_MERGE=0 restores it
+        self.apply_merge = os.environ.get("TSPM_BN_APPLY_MERGE", "1") != "0"
         # ... and the backward of its second conv together with the downsample's (tspm_conv_bwd_quad, round 6; the
         # downsample takes conv2's tile shapes); TSPM_BWD_QUAD=0: separate launches
         self.bwd_quad = os.environ.get("TSPM_BWD_QUAD", "1") != "0"
@@ -309,6 +315,7 @@ class EncoderEngine:
                     tuned_bwd = tuned_bwd or kind != "fwd"
             pair = table.get(("bwd",) + base)
             op.bwd_fused = None
+            op.bn_inlaunch = None
             if pair is not None:  # the tuner found the fused launch faster: its (dgrad, wgrad) configs
                 op.algo_dgrad, op.algo_wgrad = L.ConvAlgo(*pair[:6]), L.ConvAlgo(*pair[6:12])
             elif tuned_bwd:       # tuned, and the two separate launches won
@@ -364,23 +371,49 @@ class EncoderEngine:
         lib = L.lib()
         c1, cd = bp.conv1, bp.ds_conv
         a1, ad = self._a(c1.algo_fwd), self._a(bp.ds_pair_algo)
-        if not self.fwd_pair or self.conv_timer or not lib.tspm_conv_fwd_pair_supported(
+        if not self.fwd_pair or not lib.tspm_conv_fwd_pair_supported(
                 ctypes.byref(c1.shape), ctypes.byref(a1), ctypes.byref(strides), ctypes.byref(cd.shape),
                 ctypes.byref(ad), ctypes.byref(strides)):
             return False
         b1 = self._bnf(bp.bn1) if train else None
         b2 = self._bnf(bp.ds_bn, second=True) if train else None
+        if train and self._merge_in_apply(c1, bp.bn1):  # conv1's statistics merged by the bn1 apply (round 6)
+            b1.counters = None
+            bp.bn1.pending = c1.stat_tiles()
+        if self.conv_timer:
+            from .roofline import OpGroup
+            self.conv_timer.begin(OpGroup((c1, cd)), "fwdpair")
         L.check(lib.tspm_conv_fwd_pair(
             ctypes.byref(c1.shape), ctypes.byref(a1), x_ptr, ctypes.byref(strides), self._w(c1).data_ptr(),
             bp.y1.data_ptr(), ctypes.byref(b1) if b1 is not None else None, self.ws_conv.data_ptr(), self.ws_conv_bytes,
             ctypes.byref(cd.shape), ctypes.byref(ad), x_ptr, ctypes.byref(strides), self._w(cd).data_ptr(),
             bp.yd.data_ptr(), ctypes.byref(b2) if b2 is not None else None, self.ws_conv2.data_ptr(),
             self.ws_conv_bytes, sh), "conv_fwd_pair")
+        if self.conv_timer:
+            self.conv_timer.end()
         return True
 
-    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int) -> None:
+    def _merge_in_apply(self, op: ConvOp, bn: BNOp) -> bool:
+        """The conv cannot merge bn's statistics in-launch and the apply can (tspm_bn_apply_merge): the conv then only
+        writes its partial tiles and the apply merges them (bn.pending)."""
+        if not self.apply_merge or self.bn_two_level or bn.channels % 16:
+            return False
+        if op.bn_inlaunch is None:
+            lib = L.lib()
+            op.bn_inlaunch = bool(lib.tspm_conv_fwd_bn_inlaunch(ctypes.byref(op.shape), ctypes.byref(op.algo_fwd)))
+        return not op.bn_inlaunch and op.stat_tiles()[0] <= 256
+
+    def _conv_bn(self, op: ConvOp, bn: BNOp, x_ptr: int, strides: L.Strides4, y: torch.Tensor, sh: int,
+                 merge_ok: bool = False) -> None:
         """conv forward whose epilogue emits the BN partial statistics and, in its last workgroup
-        per channel block, merges them (save_mean/invstd + running statistics): one launch."""
+        per channel block, merges them (save_mean/invstd + running statistics): one launch.  When the merge cannot
+        run in-launch, the partials are left for the apply (round 6)."""
+        if merge_ok and self._merge_in_apply(op, bn):  # (bn1 / bn2 of a block: their apply is tspm_bn_apply)
+            bnf = self._bnf(bn)
+            bnf.counters = None
+            self._conv_fwd(op, x_ptr, strides, y, sh, bnf)
+            bn.pending = op.stat_tiles()
+            return
         self._conv_fwd(op, x_ptr, strides, y, sh, self._bnf(bn))
 
     def _apply(self, bn: BNOp, y, out, res_mode=0, res=None, bn2: Optional[BNOp] = None, relu=True, sh=0, train=True,
@@ -388,6 +421,13 @@ class EncoderEngine:
         lib = L.lib()
         m = bn.module
         if pooled is not None:  # the last block: the adaptive average pool in the same launch
+            if train and bn.pending is not None:  # (its conv left the statistics to merge: the finalize launch)
+                tiles, rpt = bn.pending
+                bn.pending = None
+                L.check(lib.tspm_bn_finalize(bn.rows, bn.channels, tiles, rpt, self.bn_part.data_ptr(),
+                                             L.ptr(m.running_mean), L.ptr(m.running_var),
+                                             BN_MOMENTUM if m.momentum is None else m.momentum, m.eps,
+                                             bn.mean.data_ptr(), bn.invstd.data_ptr(), sh), "bn_finalize")
             h, w = self.final_hw
             m2 = bn2.module if bn2 else None
             if train:
@@ -400,7 +440,19 @@ class EncoderEngine:
                                            L.ptr(m2.bias) if m2 else None, 1 if relu else 0, 0 if train else 1, m.eps,
                                            out.data_ptr(), pooled.data_ptr(), sh), "bn_apply_pool")
             return
-        if train:
+        if train and bn.pending is not None:  # the statistics merge of the conv before, in this launch (round 6)
+            tiles, rpt = bn.pending
+            bn.pending = None
+            L.check(lib.tspm_bn_apply_merge(bn.rows, bn.channels, tiles, rpt, self.bn_part.data_ptr(),
+                                            L.ptr(m.running_mean), L.ptr(m.running_var),
+                                            BN_MOMENTUM if m.momentum is None else m.momentum, m.eps,
+                                            bn.mean.data_ptr(), bn.invstd.data_ptr(), y.data_ptr(), m.weight.data_ptr(),
+                                            m.bias.data_ptr(), res_mode, L.ptr(res),
+                                            L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
+                                            L.ptr(bn2.module.weight) if bn2 else None,
+                                            L.ptr(bn2.module.bias) if bn2 else None, 1 if relu else 0, out.data_ptr(),
+                                            sh), "bn_apply_merge")
+        elif train:
             L.check(lib.tspm_bn_apply(bn.rows, bn.channels, y.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
                                       m.weight.data_ptr(), m.bias.data_ptr(), res_mode, L.ptr(res),
                                       L.ptr(bn2.mean) if bn2 else None, L.ptr(bn2.invstd) if bn2 else None,
@@ -476,14 +528,14 @@ class EncoderEngine:
             if paired:
                 pass
             elif train:
-                self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh)
+                self._conv_bn(bp.conv1, bp.bn1, xin.data_ptr(), xs_in, bp.y1, sh, merge_ok=True)
             else:
                 self._conv_fwd(bp.conv1, xin.data_ptr(), xs_in, bp.y1, sh)
             s2 = bp.conv2.shape
             xs_a1 = L.hwnc_strides(N, s2.h, s2.w, s2.c)
             self._apply(bp.bn1, bp.y1, bp.a1, relu=True, sh=sh, train=train)
             if train:
-                self._conv_bn(bp.conv2, bp.bn2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
+                self._conv_bn(bp.conv2, bp.bn2, bp.a1.data_ptr(), xs_a1, bp.y2, sh, merge_ok=True)
             else:
                 self._conv_fwd(bp.conv2, bp.a1.data_ptr(), xs_a1, bp.y2, sh)
             if bp.ds_conv is not None:
@@ -654,7 +706,7 @@ class EncoderEngine:
         if c2.bwd_fused is None:  # decided once, as _bwd_pair does: the eager and the captured steps agree
             c2.bwd_fused = bool(lib.tspm_conv_bwd_supported(ctypes.byref(s2), ctypes.byref(c2.algo_dgrad),
                                                             ctypes.byref(c2.algo_wgrad), ctypes.byref(xs_a1)))
-        if (not self.bwd_quad or self.conv_timer or not c2.bwd_fused or
+        if (not self.bwd_quad or not c2.bwd_fused or
                 not lib.tspm_conv_bwd_quad_supported(ctypes.byref(s2), ctypes.byref(ad), ctypes.byref(aw),
                                                      ctypes.byref(xs_a1), ctypes.byref(cd.shape), ctypes.byref(qd),
                                                      ctypes.byref(qw), ctypes.byref(xs_in))):
@@ -662,6 +714,9 @@ class EncoderEngine:
         g2, gd = self._grad(c2.module.weight), self._grad(cd.module.weight)
         job = self.adam_carry.take(0.5) if self.adam_carry is not None else None
         b = self.ws_conv_bytes
+        if self.conv_timer:
+            from .roofline import OpGroup
+            self.conv_timer.begin(OpGroup((c2, cd)), "bwdquad")
         L.check(lib.tspm_conv_bwd_quad(
             ctypes.byref(s2), ctypes.byref(ad), ctypes.byref(aw), bp.a1.data_ptr(), ctypes.byref(xs_a1), d2.data_ptr(),
             self._w(c2).data_ptr(), da1.data_ptr(), 0, g2.data_ptr(), ctypes.byref(bnp) if bnp is not None else None,
@@ -669,6 +724,8 @@ class EncoderEngine:
             ctypes.byref(qw), xin.data_ptr(), ctypes.byref(xs_in), dd.data_ptr(), self._w(cd).data_ptr(), Gnv.data_ptr(),
             gd.data_ptr(), self.ws_conv3.data_ptr(), b, self.ws_conv4.data_ptr(), b,
             ctypes.byref(job) if job is not None else None, sh), "conv_bwd_quad")
+        if self.conv_timer:
+            self.conv_timer.end()
         return True
 
     def _dgrad(self, op: ConvOp, dy: torch.Tensor, dx: torch.Tensor, beta: int, sh: int) -> None:

@@ -104,7 +104,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
 # ------------------------------------------------------------------------------------------------
 import re as _re
 
-CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|bwd_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
+CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|fwd_pair_lds|bwd_lds|bwd_quad_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
                           r"conv_wgrad|conv_wgrad_t|stem_fwd|stem_wgrad|reduce_slabs|reduce_slabs_wide)\b")
 CONV_SECONDARY = _re.compile(r"\bk_reduce_slabs(_wide)?\b")  # second kernel of a split-K wgrad launch (variant 0)
 
@@ -151,8 +151,19 @@ class LaunchRecorder:
         pass
 
 
+class OpGroup:
+    """Two convs in one launch (engine: the paired forward ``fwdpair`` = conv1 + downsample, the quad backward
+    ``bwdquad`` = conv2 + downsample dgrad and wgrad): ``shape`` is the first (3x3) conv's, the FLOPs are both."""
+
+    def __init__(self, ops):
+        self.ops = tuple(ops)
+        self.shape = self.ops[0].shape
+
+
 def launch_flops(op, kind) -> int:
-    """Valid-tap FLOPs of one conv launch."""
+    """Valid-tap FLOPs of one conv launch (both convs of a paired / quad launch)."""
+    if kind in ("fwdpair", "bwdquad"):
+        return sum(launch_flops(o, "fwd" if kind == "fwdpair" else "bwd") for o in op.ops)
     s = op.shape
     _, valid = conv_macs(s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad)
     return 2 * valid * (2 if kind == "bwd" else 1)

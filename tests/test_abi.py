@@ -163,6 +163,11 @@ def test_round6_entry_points_validate_before_launch():
     # tspm_bn_bwd_apply_part: more tiles than the merge prologue takes, a missing ReLU output
     assert lib.tspm_bn_bwd_apply_part(512, 256, 1025, *([16] * 10), *([None] * 7), None, None) == 1
     assert lib.tspm_bn_bwd_apply_part(512, 256, 16, 16, 16, None, *([16] * 7), *([None] * 7), None, None) == 1
+    # tspm_bn_apply_merge: more than 256 tiles, channels not a multiple of 16
+    assert lib.tspm_bn_apply_merge(6272, 64, 257, 32, 16, None, None, 0.1, 1e-5, 16, 16, 16, 16, 16, 0, None, None,
+                                   None, None, None, 1, 16, None) == 1
+    assert lib.tspm_bn_apply_merge(6272, 72, 196, 32, 16, None, None, 0.1, 1e-5, 16, 16, 16, 16, 16, 0, None, None,
+                                   None, None, None, 1, 16, None) == 1
     # tspm_conv_fwd_pair: tile shapes differ; both halves split-K on one workspace
     s1, s2 = L.ConvShape(128, 4, 4, 128, 256, 3, 3, 2, 1, 2, 2), L.ConvShape(128, 4, 4, 128, 256, 1, 1, 2, 0, 2, 2)
     xs = L.hwnc_strides(128, 4, 4, 128)
