@@ -513,6 +513,13 @@ typedef struct tspm_bn_bwd_part {
   const float* y2;     /* nullable: a second BN fed by the same gradient (the block's downsample branch) */
   const float* mean2;  /* its save_mean [c] */
   float* part;         /* [2 or 3][(h*w*n)/32][c] */
+  /* Max-pool gather (nullable idx): dx is the gradient of a MaxPool2d(3, 2, 1) output whose argmax taps are idx
+   * ([h][w][n][c] uint8, tspm_bn_apply_maxpool's), and the BN sits before that pool on a pool_h x pool_w map (the
+   * ResNet stem, resnet.py:138-140): out / y are read at each pooled element's argmax position, so the sums are the
+   * BN backward's over the pool's input-gradient (sum over the map of maxpool_bwd(dx) * [out > 0] ...) formed in
+   * the pooled domain — one gathered read per pooled element instead of a pass over the pool's input. */
+  const uint8_t* idx;
+  int32_t pool_h, pool_w;
 } tspm_bn_bwd_part;
 /* tspm_conv_bwd with an optional carried Adam job (as tspm_conv_bwd_adam; nullable) and optional BN-backward
  * partial sums of dx (bnp; nullable). */
@@ -540,6 +547,12 @@ int tspm_conv_bwd_quad(const tspm_conv_shape* s, const tspm_conv_algo* dg, const
  * double in a fixed order, writes dgamma / dbeta (first row block) and dy = gamma*invstd*(g' - mean(g') -
  * xhat*mean(g' xhat)) [dy2 likewise for y2], dres = g' (nullable).  Arguments otherwise as tspm_bn_bwd with g dense
  * (out required). */
+/* tspm_bn_bwd_apply_part with the gradient read through a pooling layer's backward (the stem BN under the max pool:
+ * src->kind TSPM_GSRC_MAXPOOL, as tspm_bn_bwd_src), its partial sums from tspm_conv_bwd_ex's max-pool gather mode
+ * (tspm_bn_bwd_part.idx); single BN, no dres. */
+int tspm_bn_bwd_apply_part_src(int64_t m, int32_t c, int32_t tiles, const float* part, const tspm_bn_gsrc* src,
+                               const float* out, const float* y, const float* mean, const float* invstd,
+                               const float* gamma, float* dgamma, float* dbeta, float* dy, tspm_stream_t stream);
 int tspm_bn_bwd_apply_part(int64_t m, int32_t c, int32_t tiles, const float* part, const float* g, const float* out,
                            const float* y, const float* mean, const float* invstd, const float* gamma, float* dgamma,
                            float* dbeta, float* dy, const float* y2, const float* mean2, const float* invstd2,

@@ -32,6 +32,7 @@ def build(batch, kw, dev):
     bnp = kw.pop("_bnp", None)      # encoders ("a", "i") whose BN backward partial sums come from the dgrad epilogue
     floor = kw.pop("_floor", None)  # the audio encoder's LDS floor (bytes) instead of the default
     am = kw.pop("_am", None)        # the forward BN merge in the apply (tspm_bn_apply_merge) on / off
+    bnps = kw.pop("_bnps", None)    # the stem BN's partial sums gathered by layer1's first data gradient on / off
     bnpt = kw.pop("_bnpt", None)    # the largest BN (in 32-row tiles) whose backward partial sums come from the dgrad
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
     if stem is not None or stemw is not None:
@@ -46,6 +47,8 @@ def build(batch, kw, dev):
         step.eng_a.fuse_pool = step.eng_i.fuse_pool = bool(pool)
     if bnp is not None:
         step.eng_a.bn_dgrad_part, step.eng_i.bn_dgrad_part = "a" in bnp, "i" in bnp
+    if bnps is not None:
+        step.eng_a.bnp_stem = step.eng_i.bnp_stem = bool(bnps)
     if am is not None:
         step.eng_a.apply_merge = step.eng_i.apply_merge = bool(am)
     if bnpt is not None:

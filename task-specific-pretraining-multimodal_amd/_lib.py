@@ -69,7 +69,8 @@ class AdamJob(ctypes.Structure):
 class BnBwdPart(Structure):
     """tspm_bn_bwd_part (ABI 21, round 6): the BN backward's partial sums formed by the dgrad epilogue that writes its
     incoming gradient (tspm_conv_bwd_ex), consumed by tspm_bn_bwd_apply_part."""
-    _fields_ = [(n, c_void_p) for n in ("out", "y", "mean", "y2", "mean2", "part")]
+    _fields_ = [(n, c_void_p) for n in ("out", "y", "mean", "y2", "mean2", "part", "idx")] + \
+        [("pool_h", c_int32), ("pool_w", c_int32)]
 
 
 class BnGSrc(Structure):
@@ -159,6 +160,7 @@ _SIGS = {
     # round 6: the BN backward's partial sums in the producing dgrad's epilogue, and the apply launch alone
     "tspm_conv_bwd_ex": (c_int32, [_P] * 8 + [c_int32, _P, _P, POINTER(BnBwdPart), _P, c_size_t, _P, c_size_t, _P]),
     "tspm_bn_bwd_apply_part": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 18 + [_P]),
+    "tspm_bn_bwd_apply_part_src": (c_int32, [c_int64, c_int32, c_int32] + [_P] * 10 + [_P]),
     # round 6: a downsampling block's first conv and its 1x1 downsample in one launch
     "tspm_conv_fwd_pair_supported": (c_int32, [_P] * 6),
     "tspm_conv_fwd_pair": (c_int32, [_P] * 7 + [_P, c_size_t] + [_P] * 7 + [_P, c_size_t, _P]),

@@ -1164,6 +1164,33 @@ extern "C" int tspm_bn_bwd_apply_part(int64_t m, int32_t c, int32_t tiles, const
   return TSPM_OK;
 }
 
+extern "C" int tspm_bn_bwd_apply_part_src(int64_t m, int32_t c, int32_t tiles, const float* part,
+                                          const tspm_bn_gsrc* src, const float* out, const float* y, const float* mean,
+                                          const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                                          float* dy, tspm_stream_t stream) {
+  if (m <= 0 || !c_ok(c) || tiles < 1 || tiles > 8 * kMergeTiles || !part || !src || !src->gp || !out || !y || !mean ||
+      !invstd || !gamma || !dy)
+    return TSPM_ERR_INVALID;
+  const tspm_bn_gsrc& g = *src;
+  if (g.n <= 0 || g.h <= 0 || g.w <= 0 || (long long)g.h * g.w * g.n != m || m >= (1LL << 24)) return TSPM_ERR_INVALID;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int cblk = cdiv(c, kChanPerBlock);
+  long long rb = cdiv64(m, std::max(1, 512 / cblk));
+  if (rb < 64) rb = 64;
+  const dim3 agrid((unsigned)cdiv64(m, rb), cblk);
+  if (g.kind == TSPM_GSRC_MAXPOOL) {
+    if (!g.idx || g.p != (g.h + 2 - 3) / 2 + 1 || g.q != (g.w + 2 - 3) / 2 + 1) return TSPM_ERR_INVALID;
+    const GMax gs{g.gp, g.idx, g.n, g.w, g.p, g.q, c, 1.0f / (float)g.n, 1.0f / (float)g.w};
+    hipLaunchKernelGGL((k_bn_bwd_apply_m<true, false, false, GMax>), agrid, dim3(256), 0, st, (long long)m, c, tiles,
+                       part, invstd, gamma, nullptr, nullptr, dgamma, dbeta, nullptr, nullptr, gs, out, y, mean, nullptr,
+                       nullptr, rb, dy, nullptr, nullptr);
+  } else {
+    return TSPM_ERR_INVALID;
+  }
+  TSPM_LAUNCH_CHECK();
+  return TSPM_OK;
+}
+
 extern "C" int tspm_bn_bwd_src(int64_t m, int32_t c, const tspm_bn_gsrc* src, const float* out, const float* y,
                                const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                                float* dy, const float* y2, const float* mean2, const float* invstd2,

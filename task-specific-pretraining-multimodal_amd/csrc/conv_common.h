@@ -28,6 +28,8 @@ struct ConvArgs {
   const float* bnb_y2;
   const float* bnb_mean2;
   float* bnb_part;
+  const uint8_t* bnb_idx;    // max-pool gather mode (tspm_bn_bwd_part.idx): bnb_out / bnb_y are [bnb_H][bnb_W][n][c]
+  int bnb_H, bnb_W;
 };
 
 template <int TM, int TN>
@@ -101,9 +103,17 @@ struct Acc {
             const int row = min(row0 + a * 32 + acc_row(h * 8 + j, lane), rows - 1);
             const long long off = (long long)row * ld + c;
             old[j] = accumulate ? out[off] : 0.f;
-            msk[j] = g.bnb_out[off];
-            yy[j] = g.bnb_y[off];
-            yy2[j] = g.bnb_y2 ? g.bnb_y2[off] : 0.f;
+            long long src = off;
+            if (g.bnb_idx) {  // the element the max pool took this output from (dx rows = (p, q, n) of the pool output)
+              const int tap = g.bnb_idx[off];
+              const int pos = row / g.n, nn = row - pos * g.n;
+              const int pp = pos / g.w, qq = pos - pp * g.w;
+              const int hh = 2 * pp - 1 + tap / 3, ww = 2 * qq - 1 + tap % 3;
+              src = (((long long)hh * g.bnb_W + ww) * g.n + nn) * ld + c;
+            }
+            msk[j] = g.bnb_out[src];
+            yy[j] = g.bnb_y[src];
+            yy2[j] = g.bnb_y2 ? g.bnb_y2[src] : 0.f;
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {

@@ -1264,6 +1264,12 @@ int bwd_half(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, con
       return TSPM_ERR_INVALID;
     h.gd.bnb_out = bnp->out; h.gd.bnb_y = bnp->y; h.gd.bnb_mean = bnp->mean;
     h.gd.bnb_y2 = bnp->y2; h.gd.bnb_mean2 = bnp->mean2; h.gd.bnb_part = bnp->part;
+    if (bnp->idx) {  // max-pool gather: dx is the 3x3/2/1 pool's output gradient over a pool_h x pool_w map
+      if (bnp->y2 || bnp->pool_h <= 0 || bnp->pool_w <= 0 || (bnp->pool_h - 1) / 2 + 1 != s->h ||
+          (bnp->pool_w - 1) / 2 + 1 != s->w)
+        return TSPM_ERR_INVALID;
+      h.gd.bnb_idx = bnp->idx; h.gd.bnb_H = bnp->pool_h; h.gd.bnb_W = bnp->pool_w;
+    }
   }
   if (ad.splits > 1) {
     if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;

@@ -166,6 +166,8 @@ class EncoderEngine:
         self.bn_dgrad_part = os.environ.get("TSPM_BN_DGRAD_PART", "1") != "0"
         # ... for BNs of at most this many 32-row tiles (each apply workgroup merges them all in its prologue)
         self.bnp_max_tiles = int(os.environ.get("TSPM_BN_DGRAD_PART_TILES", "1024"))
+        # ... including the stem BN's, gathered through the max pool's argmax taps (TSPM_BN_DGRAD_PART_STEM=0: off)
+        self.bnp_stem = os.environ.get("TSPM_BN_DGRAD_PART_STEM", "1") != "0"
         self._bnp_ready = set()
         # a downsampling block's first conv and its 1x1 downsample (same input, independent) in ONE forward launch
         # (tspm_conv_fwd_pair, round 6; the downsample takes the first conv's tile shape); TSPM_FWD_PAIR=0: two launches
@@ -243,6 +245,11 @@ class EncoderEngine:
             for bn, ok in ((bp.bn1, True), (bp.bn2, i + 1 < len(self.blocks))):
                 if ok and bn.rows % 32 == 0 and bn.rows // 32 <= 1024:
                     bn.part = torch.empty(3 * (bn.rows // 32) * bn.channels, **f32)
+        # the stem BN: its sums over the max pool's input gradient gathered in the pooled domain by layer1's first
+        # conv1 data gradient (tspm_bn_bwd_part.idx); tiles = the pooled map's 32-row tiles
+        mp_rows = p2 * q2 * N
+        if mp_rows % 32 == 0 and mp_rows // 32 <= 1024:
+            self.stem_bn.part = torch.empty(3 * (mp_rows // 32) * C0, **f32)
 
         # backward scratch: grads of block outputs (ping-pong), dy buffers
         max_blk = max(bp.out.numel() for bp in self.blocks)
@@ -603,6 +610,17 @@ class EncoderEngine:
             L.ptr(bn2.module.weight) if bn2 else None, L.ptr(gw2) if bn2 else None, L.ptr(gb2) if bn2 else None,
             L.ptr(dy2), L.ptr(dres), sh), "bn_bwd_apply_part")
 
+    def _bnp_stem_desc(self) -> Optional["L.BnBwdPart"]:
+        """The stem BN's partial-sum descriptor in max-pool gather mode (layer1's first conv1 data gradient writes the
+        pool's output gradient), or None."""
+        bn = self.stem_bn
+        if (not self.bn_dgrad_part or not self.bnp_stem or bn.part is None or self.debug_hook is not None or not self.pool_src
+                or bn.part.numel() // (3 * bn.channels) > self.bnp_max_tiles):
+            return None
+        p1, q1, _, _ = self.mp_shape
+        return L.BnBwdPart(self.a0.data_ptr(), self.y0.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr(),
+                           self.mp_idx.data_ptr(), p1, q1)
+
     def _bnp_desc(self, bp: "BlockPlan", which: int) -> Optional["L.BnBwdPart"]:
         """The partial-sum descriptor for bn1 (which=1) or bn2 (which=2) of block ``bp``, or None when that BN takes
         the partial pass."""
@@ -853,10 +871,10 @@ class EncoderEngine:
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             # conv1's input gradient accumulates last onto the previous block's output gradient (whose bn2 partial sums
             # its epilogue forms, round 6)
-            bnp2 = self._bnp_desc(self.blocks[i - 1], 2) if i > 0 else None
+            bnp2 = self._bnp_desc(self.blocks[i - 1], 2) if i > 0 else self._bnp_stem_desc()
             if self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, carry_share=1.0, bnp=bnp2):
                 if bnp2 is not None:
-                    self._bnp_ready.add(id(self.blocks[i - 1].bn2))
+                    self._bnp_ready.add(id(self.blocks[i - 1].bn2 if i > 0 else self.stem_bn))
             else:
                 self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
                 self._dgrad(bp.conv1, d1, Gnv, 1, sh)
@@ -872,7 +890,16 @@ class EncoderEngine:
         if self.pool_src:  # the stem BN reads the max pool's gradient through its argmax taps (no g_stem tensor)
             src = L.BnGSrc(kind=L.GSRC_MAXPOOL, n=N, h=p1, w=q1, p=p2, q=q2, npos=0, ldg=0, gp=G.data_ptr(),
                            idx=self.mp_idx.data_ptr())
-            self._bn_bwd_src(self.stem_bn, src, self.a0, self.y0, self.dy_stem, sh=sh)
+            if id(self.stem_bn) in self._bnp_ready:  # its partial sums came with layer1's first data gradient
+                self._bnp_ready.discard(id(self.stem_bn))
+                bn, m = self.stem_bn, self.stem_bn.module
+                L.check(lib.tspm_bn_bwd_apply_part_src(
+                    bn.rows, bn.channels, bn.part.numel() // (3 * bn.channels), bn.part.data_ptr(), ctypes.byref(src),
+                    self.a0.data_ptr(), self.y0.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                    m.weight.data_ptr(), self._grad(m.weight).data_ptr(), self._grad(m.bias).data_ptr(),
+                    self.dy_stem.data_ptr(), sh), "bn_bwd_apply_part_src")
+            else:
+                self._bn_bwd_src(self.stem_bn, src, self.a0, self.y0, self.dy_stem, sh=sh)
         else:
             if self.g_stem is None:  # pool_src switched off after construction
                 self.g_stem = torch.empty(self.a0.numel(), device=self.device, dtype=torch.float32)

@@ -124,3 +124,70 @@ def test_dgrad_epilogue_partials_and_apply(gpu, case):
     if ref["dres"] is not None:
         assert torch.equal(got["dres"], ref["dres"])
 
+
+
+@pytest.mark.parametrize("stem_hw,algos", [((14, 14), ((1, 1, 2, 2, 1, 1), (1, 1, 1, 2, 12, 1))),    # ResNet34 image
+                                           ((16, 47), ((2, 1, 2, 1, 1, 1), (1, 1, 2, 1, 24, 1)))])  # ResNet18 audio
+def test_stem_partials_gathered_through_the_max_pool(gpu, stem_hw, algos):
+    """Max-pool gather mode (tspm_bn_bwd_part.idx): layer1's first conv1 data gradient (the pool's output gradient,
+    beta 1 onto the residual) forms the stem BN's partial sums at each pooled element's argmax; the stem BN backward
+    from them (tspm_bn_bwd_apply_part_src) matches the two-launch tspm_bn_bwd_src (partial pass over the gathered
+    gradient) up to the reordered sums, and dx is bitwise the plain launch's."""
+    lib, sh = L.lib(), L.stream_handle()
+    n, C = 128, 64
+    H, W = stem_hw
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    s = _shape(n, P, Q, C, C, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(H * W)
+    y0 = (torch.randn(H * W * n, C, generator=g) * 2 + 0.3).to(gpu)
+    mean = y0.mean(0).contiguous()
+    inv = (1 / (y0.var(0, unbiased=False) + 1e-5).sqrt()).contiguous()
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(gpu), torch.randn(C, generator=g).to(gpu)
+    a0 = torch.empty_like(y0)
+    pooled = torch.empty(P * Q * n, C, device=gpu)
+    idx = torch.empty(P * Q * n, C, dtype=torch.uint8, device=gpu)
+    L.check(lib.tspm_bn_apply_maxpool(n, H, W, C, y0.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+                                      beta.data_ptr(), 0, 1e-5, a0.data_ptr(), pooled.data_ptr(), idx.data_ptr(), P, Q,
+                                      sh), "bn_apply_maxpool")
+    x = torch.randn(P * Q * n * C, generator=g).to(gpu)
+    dy = torch.randn(P * Q * n * C, generator=g).to(gpu)
+    w = (torch.randn(C * 9 * C, generator=g) * 0.05).to(gpu)
+    dx0 = torch.randn(P * Q * n * C, generator=g).to(gpu)
+    ad, aw = L.ConvAlgo(*algos[0]), L.ConvAlgo(*algos[1])
+    xs = L.hwnc_strides(n, P, Q, C)
+    ws = [torch.zeros(1 << 26, dtype=torch.uint8, device=gpu) for _ in range(2)]
+    G = P * Q * n // 32
+    part = torch.full((3 * G * C,), float("nan"), device=gpu)
+    bnp = L.BnBwdPart(a0.data_ptr(), y0.data_ptr(), mean.data_ptr(), None, None, part.data_ptr(), idx.data_ptr(), H, W)
+    dxs = []
+    for B in (None, ctypes.byref(bnp)):
+        dx = dx0.clone()
+        dw = torch.empty(w.numel(), device=gpu)
+        L.check(lib.tspm_conv_bwd_ex(ctypes.byref(s), ctypes.byref(ad), ctypes.byref(aw), x.data_ptr(), ctypes.byref(xs),
+                                     dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 1, dw.data_ptr(), None, B,
+                                     ws[0].data_ptr(), ws[0].numel(), ws[1].data_ptr(), ws[1].numel(), sh), "conv_bwd_ex")
+        dxs.append(dx)
+    torch.cuda.synchronize()
+    assert torch.equal(dxs[0], dxs[1])
+    G_ = dxs[1]
+    src = L.BnGSrc(kind=L.GSRC_MAXPOOL, n=n, h=H, w=W, p=P, q=Q, npos=0, ldg=0, gp=G_.data_ptr(), idx=idx.data_ptr())
+    M = H * W * n
+    res = []
+    for mode in ("ref", "part"):
+        dyo, dg, db = torch.empty(M * C, device=gpu), torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+        if mode == "ref":
+            wsb = lib.tspm_bn_bwd_workspace(M, C)
+            wsn = torch.empty(wsb, dtype=torch.uint8, device=gpu)
+            L.check(lib.tspm_bn_bwd_src(M, C, ctypes.byref(src), a0.data_ptr(), y0.data_ptr(), mean.data_ptr(),
+                                        inv.data_ptr(), gamma.data_ptr(), dg.data_ptr(), db.data_ptr(), dyo.data_ptr(),
+                                        None, None, None, None, None, None, None, None, wsn.data_ptr(), wsb, sh), "bn_bwd_src")
+        else:
+            L.check(lib.tspm_bn_bwd_apply_part_src(M, C, G, part.data_ptr(), ctypes.byref(src), a0.data_ptr(),
+                                                   y0.data_ptr(), mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+                                                   dg.data_ptr(), db.data_ptr(), dyo.data_ptr(), sh), "apply_part_src")
+        res.append((dyo, dg, db))
+    torch.cuda.synchronize()
+    for a, b, k in zip(res[0], res[1], ("dy", "dgamma", "dbeta")):
+        scale = a.abs().max().item() + 1e-30
+        err = (b - a).abs().max().item()
+        assert err <= 2e-5 * scale, f"{k}: max err {err:.3e} (scale {scale:.3e})"
