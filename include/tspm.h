@@ -520,6 +520,17 @@ typedef struct tspm_bn_bwd_part {
    * the pooled domain — one gathered read per pooled element instead of a pass over the pool's input. */
   const uint8_t* idx;
   int32_t pool_h, pool_w;
+  /* Whole BN backward in the same launch (round 6; dy non-null, no idx): the last dgrad tile of each column block
+   * to finish (a ticket on counters[column block]: one uint32 per (c / tile columns), zero before first use, left
+   * zero) merges that block's partial tiles in tspm_bn_bwd_apply_part's order, writes dgamma / dbeta and applies
+   * dy [, dy2] [, dres = g'] over all rows of its channels — tspm_bn_bwd_apply_part's values, no apply launch.
+   * dx and the partials are then published write-through (sc1) for it.  Meant for short maps (the tail is one
+   * workgroup per column block). */
+  const float *invstd, *gamma;
+  float *dgamma, *dbeta, *dy;
+  const float *invstd2, *gamma2;
+  float *dgamma2, *dbeta2, *dy2, *dres;
+  uint32_t* counters;
 } tspm_bn_bwd_part;
 /* tspm_conv_bwd with an optional carried Adam job (as tspm_conv_bwd_adam; nullable) and optional BN-backward
  * partial sums of dx (bnp; nullable). */

@@ -33,6 +33,7 @@ def build(batch, kw, dev):
     floor = kw.pop("_floor", None)  # the audio encoder's LDS floor (bytes) instead of the default
     am = kw.pop("_am", None)        # the forward BN merge in the apply (tspm_bn_apply_merge) on / off
     bnps = kw.pop("_bnps", None)    # the stem BN's partial sums gathered by layer1's first data gradient on / off
+    bnx = kw.pop("_bnx", None)      # rows up to which the whole BN backward runs in the dgrad epilogue (0: off)
     bnpt = kw.pop("_bnpt", None)    # the largest BN (in 32-row tiles) whose backward partial sums come from the dgrad
     step = tspm_amd.FusedTrainStep(model, opt, None, batch, **kw)
     if stem is not None or stemw is not None:
@@ -47,6 +48,8 @@ def build(batch, kw, dev):
         step.eng_a.fuse_pool = step.eng_i.fuse_pool = bool(pool)
     if bnp is not None:
         step.eng_a.bn_dgrad_part, step.eng_i.bn_dgrad_part = "a" in bnp, "i" in bnp
+    if bnx is not None:
+        step.eng_a.bnx_max_rows = step.eng_i.bnx_max_rows = int(bnx)
     if bnps is not None:
         step.eng_a.bnp_stem = step.eng_i.bnp_stem = bool(bnps)
     if am is not None:

@@ -70,7 +70,9 @@ class BnBwdPart(Structure):
     """tspm_bn_bwd_part (ABI 21, round 6): the BN backward's partial sums formed by the dgrad epilogue that writes its
     incoming gradient (tspm_conv_bwd_ex), consumed by tspm_bn_bwd_apply_part."""
     _fields_ = [(n, c_void_p) for n in ("out", "y", "mean", "y2", "mean2", "part", "idx")] + \
-        [("pool_h", c_int32), ("pool_w", c_int32)]
+        [("pool_h", c_int32), ("pool_w", c_int32)] + \
+        [(n, c_void_p) for n in ("invstd", "gamma", "dgamma", "dbeta", "dy", "invstd2", "gamma2", "dgamma2", "dbeta2",
+                                 "dy2", "dres", "counters")]
 
 
 class BnGSrc(Structure):

@@ -899,7 +899,7 @@ extern "C" int tspm_conv_bwd_ex(const tspm_conv_shape* s, const tspm_conv_algo* 
                                   job->blocks < 1))))
     return TSPM_ERR_INVALID;
   if (bnp && (!bnp->out || !bnp->y || !bnp->mean || !bnp->part || (bnp->y2 && !bnp->mean2) ||
-              ((long long)s->h * s->w * s->n) % 32 != 0))
+              ((long long)s->h * s->w * s->n) % 32 != 0 || (bnp->dy && (!bnp->counters || bnp->idx))))
     return TSPM_ERR_INVALID;
   if (!tspm_conv_bwd_supported(s, dg, wg, xs)) return TSPM_ERR_INVALID;
   return lds_of(dg).bwd(s, lds_algo(dg), lds_algo(wg), x, dy, w, dx, beta, dw, (job && job->count > 0) ? job : nullptr,

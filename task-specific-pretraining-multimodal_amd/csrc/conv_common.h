@@ -30,6 +30,10 @@ struct ConvArgs {
   float* bnb_part;
   const uint8_t* bnb_idx;    // max-pool gather mode (tspm_bn_bwd_part.idx): bnb_out / bnb_y are [bnb_H][bnb_W][n][c]
   int bnb_H, bnb_W;
+  // whole-BN-backward mode (tspm_bn_bwd_part.dy): the last tile of each column block applies the BN backward
+  const float *bnx_inv, *bnx_gamma, *bnx_inv2, *bnx_gamma2;
+  float *bnx_dgamma, *bnx_dbeta, *bnx_dy, *bnx_dgamma2, *bnx_dbeta2, *bnx_dy2, *bnx_dres;
+  unsigned* bnx_cnt;
 };
 
 template <int TM, int TN>
@@ -120,7 +124,8 @@ struct Acc {
             const int row = row0 + a * 32 + acc_row(h * 8 + j, lane);
             const float val = accumulate ? (old[j] + v[a][b][h * 8 + j]) : v[a][b][h * 8 + j];
             if (row < rows && colok) {
-              out[(long long)row * ld + col] = val;
+              if (g.bnx_dy) st_sc1(out + (long long)row * ld + col, val);  // read by the column block's last tile
+              else out[(long long)row * ld + col] = val;
               const float gm = msk[j] > 0.f ? val : 0.f;
               sg += gm;
               sx += gm * (yy[j] - mu);
@@ -133,9 +138,15 @@ struct Acc {
         sx2 += __shfl_xor(sx2, 32, 64);
         if (lane < 32 && colok) {
           float* p = g.bnb_part + (long long)((row0 + a * 32) >> 5) * cols + col;
-          p[0] = sg;
-          p[plane] = sx;
-          if (g.bnb_y2) p[2 * plane] = sx2;
+          if (g.bnx_dy) {
+            st_sc1(p, sg);
+            st_sc1(p + plane, sx);
+            if (g.bnb_y2) st_sc1(p + 2 * plane, sx2);
+          } else {
+            p[0] = sg;
+            p[plane] = sx;
+            if (g.bnb_y2) p[2 * plane] = sx2;
+          }
         }
       }
     }

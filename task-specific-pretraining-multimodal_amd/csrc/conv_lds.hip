@@ -632,6 +632,109 @@ __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_fwd_pair_lds(FwdJob 
 // Data gradient: dx[(h,w,n), ci] = sum_{valid (r,s), co} dy[((h+pad-r)/st, (w+pad-s)/st, n), co] w[co,r,s,ci]
 // A image: BM rows (n) x 32 output channels (swizzled); B image: 32 rows (co) x BN input channels.
 // =============================================================================================
+// Round 6: the BatchNorm backward of one dgrad column block [c0, c0 + CB), run by the block's last-finishing tile
+// (ConvArgs.bnx_*): the channels' partial tiles are merged in tspm_bn_bwd_apply_part's order (per channel, 16 row
+// groups each summing tiles rg, rg + 16, ... in double, then the groups in order), the coefficients are formed as
+// k_bn_bwd_apply_m forms them, and dy [, dy2] [, dres] are written over all M rows — tspm_bn_bwd_apply_part's
+// values without its launch.  dx and the partials were published with st_sc1 (write-through); the ticket takes an
+// agent-scope acquire, so they are read with plain (vector) loads.
+__host__ __device__ inline size_t bnx_lds_bytes(int CB) { return 16 + (size_t)16 * CB * 3 * sizeof(double) + (size_t)CB * 8 * sizeof(float); }
+TSPM_DEV void bnx_tail(const ConvArgs& g, const float* __restrict__ dx, int c0, int CB, float* lds) {
+  const int t = threadIdx.x;
+  const int M = g.m, C = g.c, G = M >> 5;
+  const long long plane = (long long)G * C;
+  const bool two = g.bnb_y2 != nullptr;
+  double* acc = reinterpret_cast<double*>(lds + 4);              // [16][CB][3]
+  float* coef = reinterpret_cast<float*>(acc + 16 * CB * 3);      // [8][CB]: ca cb cm ca2 cb2 cm2
+  for (int i = t; i < 16 * CB; i += kThreads) {
+    const int rg = i / CB, cl = i - rg * CB, c = c0 + cl;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    if (c < C)
+      for (int tile = rg; tile < G; tile += 16) {  // (behind the ticket's agent acquire: plain loads)
+        const long long o = (long long)tile * C + c;
+        a0 += (double)g.bnb_part[o];
+        a1 += (double)g.bnb_part[plane + o];
+        if (two) a2 += (double)g.bnb_part[2 * plane + o];
+      }
+    acc[(rg * CB + cl) * 3 + 0] = a0;
+    acc[(rg * CB + cl) * 3 + 1] = a1;
+    acc[(rg * CB + cl) * 3 + 2] = a2;
+  }
+  __syncthreads();
+  for (int cl = t; cl < CB; cl += kThreads) {
+    const int c = c0 + cl;
+    if (c >= C) continue;
+    double sg = acc[cl * 3 + 0], sx = acc[cl * 3 + 1], sx2 = acc[cl * 3 + 2];
+    for (int k = 1; k < 16; ++k) {
+      sg += acc[(k * CB + cl) * 3 + 0];
+      sx += acc[(k * CB + cl) * 3 + 1];
+      sx2 += acc[(k * CB + cl) * 3 + 2];
+    }
+    const double n = (double)M;
+    const double iv = g.bnx_inv[c], ga = g.bnx_gamma[c];
+    const double dg = sx * iv;
+    const double a_ = ga * iv;
+    coef[0 * CB + cl] = (float)a_;
+    coef[1 * CB + cl] = (float)(a_ * iv * dg / n);
+    coef[2 * CB + cl] = (float)(a_ * sg / n);
+    g.bnx_dgamma[c] = (float)dg;
+    g.bnx_dbeta[c] = (float)sg;
+    if (two) {
+      const double iv2 = g.bnx_inv2[c], ga2 = g.bnx_gamma2[c];
+      const double dg2 = sx2 * iv2;
+      const double a2 = ga2 * iv2;
+      coef[3 * CB + cl] = (float)a2;
+      coef[4 * CB + cl] = (float)(a2 * iv2 * dg2 / n);
+      coef[5 * CB + cl] = (float)(a2 * sg / n);
+      g.bnx_dgamma2[c] = (float)dg2;
+      g.bnx_dbeta2[c] = (float)sg;
+    }
+  }
+  __syncthreads();
+  // apply: thread = (row group, 4 channels)
+  const int L4 = CB >> 2, nrg = kThreads / L4;
+  const int q = t % L4, rg = t / L4;
+  const int c = c0 + 4 * q;
+  if (rg >= nrg || c >= C) return;
+  f32x4 ca, cb, cm, ca2 = {0.f, 0.f, 0.f, 0.f}, cb2 = ca2, cm2 = ca2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ca[j] = coef[0 * CB + 4 * q + j];
+    cb[j] = coef[1 * CB + 4 * q + j];
+    cm[j] = coef[2 * CB + 4 * q + j];
+    if (two) {
+      ca2[j] = coef[3 * CB + 4 * q + j];
+      cb2[j] = coef[4 * CB + 4 * q + j];
+      cm2[j] = coef[5 * CB + 4 * q + j];
+    }
+  }
+  const f32x4 mu = ld4(g.bnb_mean + c);
+  const f32x4 mu2 = two ? ld4(g.bnb_mean2 + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;  // rows per batch: their loads in flight together (clamped rows re-read, never stored)
+  for (int rb = rg; rb < M; rb += U * nrg) {
+    f32x4 gv[U], ov[U], yv[U], y2v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long off = (long long)min(rb + u * nrg, M - 1) * C + c;
+      gv[u] = ld4(dx + off);
+      ov[u] = ld4(g.bnb_out + off);
+      yv[u] = ld4(g.bnb_y + off);
+      if (two) y2v[u] = ld4(g.bnb_y2 + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = rb + u * nrg;
+      if (row >= M) continue;
+      const long long off = (long long)row * C + c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[u][j] = ov[u][j] > 0.f ? gv[u][j] : 0.f;
+      st4(g.bnx_dy + off, ca * gv[u] - cm - cb * (yv[u] - mu));
+      if (two) st4(g.bnx_dy2 + off, ca2 * gv[u] - cm2 - cb2 * (y2v[u] - mu2));
+      if (g.bnx_dres) st4(g.bnx_dres + off, gv[u]);
+    }
+  }
+}
+
 template <class C>
 TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const float* __restrict__ w,
                          float* __restrict__ dx, float* __restrict__ slabs, float* lds, const Blk& bk) {
@@ -715,6 +818,10 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
     else acc.store(dx, row0, col0, g.m, Cc, Cc, lane, g.beta != 0);
   }
   TSPM_STAMP(tspm_g_stamps_lds, 5);
+  if (g.bnx_dy) {  // the column block's last tile runs its BN backward (round 6)
+    if (!last_arriver(g.bnx_cnt + bk.y, (unsigned)bk.gx, reinterpret_cast<int*>(lds), true)) return;
+    bnx_tail(g, dx, c0col, C::BN, lds);
+  }
 }
 template <class C>
 __global__ __launch_bounds__(kBlock, min_waves<C>()) void k_dgrad_lds(ConvArgs g, const float* __restrict__ dy,
@@ -1270,6 +1377,15 @@ int bwd_half(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, con
         return TSPM_ERR_INVALID;
       h.gd.bnb_idx = bnp->idx; h.gd.bnb_H = bnp->pool_h; h.gd.bnb_W = bnp->pool_w;
     }
+    if (bnp->dy) {  // the whole BN backward in the epilogue (round 6)
+      if (bnp->idx || !bnp->invstd || !bnp->gamma || !bnp->dgamma || !bnp->dbeta || !bnp->counters ||
+          (bnp->y2 && (!bnp->invstd2 || !bnp->gamma2 || !bnp->dgamma2 || !bnp->dbeta2 || !bnp->dy2)) || s->c % 4)
+        return TSPM_ERR_INVALID;
+      h.gd.bnx_inv = bnp->invstd; h.gd.bnx_gamma = bnp->gamma; h.gd.bnx_dgamma = bnp->dgamma;
+      h.gd.bnx_dbeta = bnp->dbeta; h.gd.bnx_dy = bnp->dy; h.gd.bnx_inv2 = bnp->invstd2; h.gd.bnx_gamma2 = bnp->gamma2;
+      h.gd.bnx_dgamma2 = bnp->dgamma2; h.gd.bnx_dbeta2 = bnp->dbeta2; h.gd.bnx_dy2 = bnp->dy2;
+      h.gd.bnx_dres = bnp->dres; h.gd.bnx_cnt = bnp->counters;
+    }
   }
   if (ad.splits > 1) {
     if (!wsd || wsd_bytes < lds_dgrad_workspace(s, ad)) return TSPM_ERR_WORKSPACE;
@@ -1312,7 +1428,9 @@ int lds_bwd(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw, cons
   }
   LdsAlgo af = ad;  // one launch: the larger of the two halves' floors
   af.floor = std::max(ad.floor, aw.floor);
-  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)), af);
+  size_t need = std::max(lds_bytes(ad, false), lds_bytes(aw, false));
+  if (h.gd.bnx_dy) need = std::max(need, bnx_lds_bytes(bn_of(ad)));
+  L.lds = tspm_detail::lds_with_floor(need, af);
   L.st = st;
   bwd_dispatch(ad, aw, &L);
   TSPM_LAUNCH_CHECK();
@@ -1352,7 +1470,9 @@ int lds_bwd_quad(const tspm_conv_shape* s, const LdsAlgo& ad, const LdsAlgo& aw,
   }
   LdsAlgo af = ad;
   af.floor = std::max(std::max(ad.floor, aw.floor), std::max(ad2.floor, aw2.floor));
-  L.lds = tspm_detail::lds_with_floor(std::max(lds_bytes(ad, false), lds_bytes(aw, false)), af);
+  size_t need = std::max(lds_bytes(ad, false), lds_bytes(aw, false));
+  if (h1.gd.bnx_dy) need = std::max(need, bnx_lds_bytes(bn_of(ad)));
+  L.lds = tspm_detail::lds_with_floor(need, af);
   L.st = st;
   bwd_dispatch(ad, aw, &L);
   TSPM_LAUNCH_CHECK();

@@ -102,6 +102,7 @@ class BNOp:
     # round 6: the backward's partial sums written by the dgrad epilogue that produces this BN's incoming gradient
     # (tspm_conv_bwd_ex), [3][rows/32][C]; None when the BN is not eligible (tiles > 128, pooled gradient source)
     part: Optional[torch.Tensor] = None
+    cnt: Optional[torch.Tensor] = None       # round 6: column-block tickets of the whole-BN-backward epilogue mode
 
 
 @dataclass
@@ -168,7 +169,13 @@ class EncoderEngine:
         self.bnp_max_tiles = int(os.environ.get("TSPM_BN_DGRAD_PART_TILES", "1024"))
         # ... including the stem BN's, gathered through the max pool's argmax taps (TSPM_BN_DGRAD_PART_STEM=0: off)
         self.bnp_stem = os.environ.get("TSPM_BN_DGRAD_PART_STEM", "1") != "0"
+        # ... and for BNs of at most this many rows the WHOLE backward (merge + apply) in that epilogue, by the last
+        # tile of each column block (tspm_bn_bwd_part.dy): no apply launch.  In-step A/B: 128 rows (ResNet34 layer4)
+        # -11 us, 512 rows +16 us (one workgroup per column block applies the whole map), profiles/r6/r6h_ab_*.json;
+        # TSPM_BN_BWD_EPI_ROWS=0: off
+        self.bnx_max_rows = int(os.environ.get("TSPM_BN_BWD_EPI_ROWS", "128"))
         self._bnp_ready = set()
+        self._bnx_done = set()
         # a downsampling block's first conv and its 1x1 downsample (same input, independent) in ONE forward launch
         # (tspm_conv_fwd_pair, round 6; the downsample takes the first conv's tile shape); TSPM_FWD_PAIR=0: two launches
         self.fwd_pair = os.environ.get("TSPM_FWD_PAIR", "1") != "0"
@@ -245,6 +252,7 @@ class EncoderEngine:
             for bn, ok in ((bp.bn1, True), (bp.bn2, i + 1 < len(self.blocks))):
                 if ok and bn.rows % 32 == 0 and bn.rows // 32 <= 1024:
                     bn.part = torch.empty(3 * (bn.rows // 32) * bn.channels, **f32)
+                    bn.cnt = torch.zeros(bn.channels // 32 + 1, device=device, dtype=torch.int32)
         # the stem BN: its sums over the max pool's input gradient gathered in the pooled domain by layer1's first
         # conv1 data gradient (tspm_bn_bwd_part.idx); tiles = the pooled map's 32-row tiles
         mp_rows = p2 * q2 * N
@@ -621,17 +629,34 @@ class EncoderEngine:
         return L.BnBwdPart(self.a0.data_ptr(), self.y0.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr(),
                            self.mp_idx.data_ptr(), p1, q1)
 
-    def _bnp_desc(self, bp: "BlockPlan", which: int) -> Optional["L.BnBwdPart"]:
+    def _bnp_desc(self, bp: "BlockPlan", which: int, dres: Optional[torch.Tensor] = None) -> Optional["L.BnBwdPart"]:
         """The partial-sum descriptor for bn1 (which=1) or bn2 (which=2) of block ``bp``, or None when that BN takes
-        the partial pass."""
+        the partial pass.  For BNs of at most ``bnx_max_rows`` rows the descriptor asks for the whole BN backward in
+        the epilogue (``.dy`` set: bn1 -> g_y1; bn2 -> g_y2 [+ g_yd], ``dres`` = the block-input gradient buffer of
+        an identity block)."""
         bn = bp.bn1 if which == 1 else bp.bn2
         if not self.bn_dgrad_part or bn.part is None or self.debug_hook is not None or bn.rows // 32 > self.bnp_max_tiles:
             return None
         if which == 1:
-            return L.BnBwdPart(bp.a1.data_ptr(), bp.y1.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr())
-        two = bp.ds_conv is not None
-        return L.BnBwdPart(bp.out.data_ptr(), bp.y2.data_ptr(), bn.mean.data_ptr(), bp.yd.data_ptr() if two else None,
-                           bp.ds_bn.mean.data_ptr() if two else None, bn.part.data_ptr())
+            d = L.BnBwdPart(bp.a1.data_ptr(), bp.y1.data_ptr(), bn.mean.data_ptr(), None, None, bn.part.data_ptr())
+        else:
+            two = bp.ds_conv is not None
+            d = L.BnBwdPart(bp.out.data_ptr(), bp.y2.data_ptr(), bn.mean.data_ptr(), bp.yd.data_ptr() if two else None,
+                            bp.ds_bn.mean.data_ptr() if two else None, bn.part.data_ptr())
+        if bn.rows <= self.bnx_max_rows:
+            m = bn.module
+            d.invstd, d.gamma = bn.invstd.data_ptr(), m.weight.data_ptr()
+            d.dgamma, d.dbeta = self._grad(m.weight).data_ptr(), self._grad(m.bias).data_ptr()
+            d.dy = (bp.g_y1 if which == 1 else bp.g_y2).data_ptr()
+            d.counters = bn.cnt.data_ptr()
+            if which == 2 and bp.ds_conv is not None:
+                m2 = bp.ds_bn.module
+                d.invstd2, d.gamma2 = bp.ds_bn.invstd.data_ptr(), m2.weight.data_ptr()
+                d.dgamma2, d.dbeta2 = self._grad(m2.weight).data_ptr(), self._grad(m2.bias).data_ptr()
+                d.dy2 = bp.g_yd.data_ptr()
+            elif which == 2:
+                d.dres = dres.data_ptr()
+        return d
 
     def _bn_bwd_src(self, bn: BNOp, src: "L.BnGSrc", out_mask, y, dy, bn2: Optional[BNOp] = None, y2=None, dy2=None,
                     dres=None, sh=0):
@@ -794,6 +819,7 @@ class EncoderEngine:
         N = self.N
         if phase in (0, 1):
             self._bnp_ready = set()
+            self._bnx_done = set()
             fc = self.enc.fc
             linear_bwd(N, self.final_c, self.hidden, self.pooled.data_ptr(), self.final_c, g_emb.data_ptr(), ld_g,
                        fc.weight.data_ptr(), self._grad(fc.weight).data_ptr(),
@@ -827,15 +853,22 @@ class EncoderEngine:
             Gnv = Gn[:n_in]
             d2 = bp.g_y2
             src = pool_src if (phase in (0, 1) and i == len(self.blocks) - 1) else None
-            # bn2's partial sums came with the gradient when the next block's conv1 backward wrote them (round 6)
+            # bn2's partial sums came with the gradient when the next block's conv1 backward wrote them (round 6) —
+            # or its whole backward did (then no launch here)
             bn2_fn = self._bn_bwd_part if (src is None and id(bp.bn2) in self._bnp_ready) else self._bn_bwd
+            bn2_done = src is None and id(bp.bn2) in self._bnx_done
             self._bnp_ready.discard(id(bp.bn2))
+            self._bnx_done.discard(id(bp.bn2))
             if bp.ds_conv is not None:
                 dd = bp.g_yd
-                if src is not None:
+                if bn2_done:
+                    pass
+                elif src is not None:
                     self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
                 else:
                     bn2_fn(bp.bn2, Gv, bp.out, bp.y2, d2, bn2=bp.ds_bn, y2=bp.yd, dy2=dd, sh=sh)
+            elif bn2_done:
+                pass
             elif src is not None:
                 self._bn_bwd_src(bp.bn2, src, bp.out, bp.y2, d2, dres=Gnv, sh=sh)
             else:
@@ -856,7 +889,9 @@ class EncoderEngine:
                 self._dgrad(bp.conv2, d2, da1, 0, sh)
                 bnp1_done = False
             d1 = bp.g_y1
-            if bnp1_done:
+            if bnp1_done and bnp1.dy:
+                pass  # the whole bn1 backward ran in conv2's dgrad epilogue
+            elif bnp1_done:
                 self._bn_bwd_part(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
             else:
                 self._bn_bwd(bp.bn1, da1, bp.a1, bp.y1, d1, sh=sh)
@@ -871,10 +906,12 @@ class EncoderEngine:
                 self._dgrad(bp.ds_conv, dd, Gnv, 0, sh)
             # conv1's input gradient accumulates last onto the previous block's output gradient (whose bn2 partial sums
             # its epilogue forms, round 6)
-            bnp2 = self._bnp_desc(self.blocks[i - 1], 2) if i > 0 else self._bnp_stem_desc()
+            # (block i-1's identity-residual dres goes to this block's output-gradient buffer G, free once bn2 above ran)
+            bnp2 = self._bnp_desc(self.blocks[i - 1], 2, dres=G[:n_in]) if i > 0 else self._bnp_stem_desc()
             if self._bwd_pair(bp.conv1, xin.data_ptr(), xs_in, d1, Gnv, 1, sh, carry_share=1.0, bnp=bnp2):
                 if bnp2 is not None:
-                    self._bnp_ready.add(id(self.blocks[i - 1].bn2 if i > 0 else self.stem_bn))
+                    tgt = id(self.blocks[i - 1].bn2 if i > 0 else self.stem_bn)
+                    (self._bnx_done if bnp2.dy else self._bnp_ready).add(tgt)
             else:
                 self._wgrad(bp.conv1, xin.data_ptr(), xs_in, d1, sh)
                 self._dgrad(bp.conv1, d1, Gnv, 1, sh)

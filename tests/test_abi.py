@@ -179,6 +179,13 @@ def test_round6_entry_points_validate_before_launch():
                                   None, 32, 1 << 30, None) == 1
     assert lib.tspm_conv_fwd_pair(B(s1), B(a3), 16, B(xs), 16, 16, None, 16, 1 << 30, B(s2), B(a3), 16, B(xs), 16, 16,
                                   None, 16, 1 << 30, None) == 1
+    # tspm_conv_bwd_ex: the whole-BN-backward mode without its tickets
+    assert ctypes.sizeof(L.BnBwdPart) == 160
+    bs, ba, bw = L.ConvShape(128, 2, 2, 256, 256, 3, 3, 1, 1, 2, 2), L.ConvAlgo(1, 1, 2, 2, 4, 1), L.ConvAlgo(1, 1, 1, 2, 1, 1)
+    d = L.BnBwdPart(16, 16, 16, None, None, 16)
+    d.dy = 16
+    assert lib.tspm_conv_bwd_ex(B(bs), B(ba), B(bw), 16, B(L.hwnc_strides(128, 2, 2, 256)), 16, 16, 16, 0, 16, None, B(d),
+                                16, 1 << 30, 32, 1 << 30, None) == 1
     # tspm_conv_bwd_quad: the downsample's wgrad tile differs from conv2's
     c2, ds = L.ConvShape(128, 2, 2, 256, 256, 3, 3, 1, 1, 2, 2), L.ConvShape(128, 4, 4, 128, 256, 1, 1, 2, 0, 2, 2)
     xs2 = L.hwnc_strides(128, 2, 2, 256)

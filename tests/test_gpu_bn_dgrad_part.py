@@ -191,3 +191,83 @@ def test_stem_partials_gathered_through_the_max_pool(gpu, stem_hw, algos):
         scale = a.abs().max().item() + 1e-30
         err = (b - a).abs().max().item()
         assert err <= 2e-5 * scale, f"{k}: max err {err:.3e} (scale {scale:.3e})"
+
+
+# (block conv shape, dgrad algo, wgrad algo, beta, two, dres): layers of at most 512 rows (the whole-BN-backward mode)
+WHOLE = [
+    ((128, 2, 2, 256, 256, 3, 3, 1, 1), (1, 1, 2, 2, 4, 1), (1, 1, 1, 2, 1, 1), 0, False, False),  # R34 l3 conv2 -> bn1
+    ((128, 2, 2, 256, 256, 3, 3, 1, 1), (1, 1, 2, 2, 4, 1), (1, 1, 1, 2, 1, 1), 1, False, True),   # l3 conv1 -> bn2 + dres
+    ((128, 1, 1, 512, 512, 3, 3, 1, 1), (1, 1, 1, 4, 1, 1), (1, 1, 2, 1, 1, 1), 1, False, True),   # l4
+    ((128, 2, 2, 256, 512, 3, 3, 2, 1), (1, 1, 1, 4, 1, 1), (1, 1, 2, 1, 1, 1), 1, True, False),   # l4 conv1 -> l3 bn2 + ds
+    ((128, 1, 3, 512, 512, 3, 3, 1, 1), (1, 1, 2, 2, 4, 1), (1, 1, 2, 2, 1, 1), 0, False, False),  # R18 l4 (384 rows)
+]
+
+
+@pytest.mark.parametrize("case", WHOLE, ids=lambda c: f"{c[0]}-b{c[3]}-two{int(c[4])}-res{int(c[5])}")
+def test_whole_bn_backward_in_the_dgrad_epilogue(gpu, case):
+    """tspm_bn_bwd_part.dy (round 6): the last tile of each dgrad column block merges the partial tiles and applies
+    the BN backward itself — dy / dy2 / dres / dgamma / dbeta equal tspm_bn_bwd_apply_part over the same partial sums
+    (same merge order and expressions: bitwise), dx bitwise the plain launch's, the tickets left zero, over three
+    back-to-back launches on the same buffers."""
+    shp, dga, wga, beta, two, with_dres = case
+    lib, sh = L.lib(), L.stream_handle()
+    s = _shape(*shp)
+    M, C = s.n * s.h * s.w, s.c
+    G = M // 32
+    g = torch.Generator().manual_seed(sum(shp) * 3 + beta)
+    x = torch.randn(M * C, generator=g).to(gpu)
+    dyin = torch.randn(s.n * s.p * s.q * s.k, generator=g).to(gpu)
+    w = (torch.randn(s.k * s.r * s.s * C, generator=g) * 0.05).to(gpu)
+    dx0 = torch.randn(M * C, generator=g).to(gpu)
+    out = torch.relu(torch.randn(M, C, generator=g)).to(gpu)
+    y = (torch.randn(M, C, generator=g) * 2 + 0.5).to(gpu)
+    y2 = (torch.randn(M, C, generator=g) * 3 - 1).to(gpu) if two else None
+    mean, mean2 = y.mean(0), (y2.mean(0) if two else None)
+    inv = (1 / (y.var(0, unbiased=False) + 1e-5).sqrt()).contiguous()
+    inv2 = (1 / (y2.var(0, unbiased=False) + 1e-5).sqrt()).contiguous() if two else None
+    gamma = (torch.rand(C, generator=g) + 0.5).to(gpu)
+    gamma2 = (torch.rand(C, generator=g) + 0.5).to(gpu) if two else None
+    ad, aw = L.ConvAlgo(*dga), L.ConvAlgo(*wga)
+    xs = L.hwnc_strides(s.n, s.h, s.w, s.c)
+    ws = [torch.zeros(1 << 26, dtype=torch.uint8, device=gpu) for _ in range(2)]
+    cnt = torch.zeros(C // 32 + 1, dtype=torch.int32, device=gpu)
+
+    def outs():
+        return dict(dy=torch.full((M * C,), float("nan"), device=gpu), dg=torch.empty(C, device=gpu),
+                    db=torch.empty(C, device=gpu), dy2=torch.full((M * C,), float("nan"), device=gpu) if two else None,
+                    dg2=torch.empty(C, device=gpu) if two else None, db2=torch.empty(C, device=gpu) if two else None,
+                    dres=torch.full((M * C,), float("nan"), device=gpu) if with_dres else None)
+
+    res = []
+    for whole in (False, True):
+        for rep in range(3):
+            o = outs()
+            part = torch.full((3 * G * C,), float("nan"), device=gpu)
+            bnp = L.BnBwdPart(out.data_ptr(), y.data_ptr(), mean.data_ptr(), L.ptr(y2), L.ptr(mean2), part.data_ptr())
+            if whole:
+                bnp.invstd, bnp.gamma, bnp.dgamma, bnp.dbeta = inv.data_ptr(), gamma.data_ptr(), o["dg"].data_ptr(), \
+                    o["db"].data_ptr()
+                bnp.dy, bnp.counters = o["dy"].data_ptr(), cnt.data_ptr()
+                if two:
+                    bnp.invstd2, bnp.gamma2, bnp.dgamma2, bnp.dbeta2, bnp.dy2 = (
+                        inv2.data_ptr(), gamma2.data_ptr(), o["dg2"].data_ptr(), o["db2"].data_ptr(), o["dy2"].data_ptr())
+                if with_dres:
+                    bnp.dres = o["dres"].data_ptr()
+            dx = dx0.clone()
+            dw = torch.empty(w.numel(), device=gpu)
+            L.check(lib.tspm_conv_bwd_ex(ctypes.byref(s), ctypes.byref(ad), ctypes.byref(aw), x.data_ptr(),
+                                         ctypes.byref(xs), dyin.data_ptr(), w.data_ptr(), dx.data_ptr(), beta,
+                                         dw.data_ptr(), None, ctypes.byref(bnp), ws[0].data_ptr(), ws[0].numel(),
+                                         ws[1].data_ptr(), ws[1].numel(), sh), "conv_bwd_ex")
+            if not whole:
+                L.check(lib.tspm_bn_bwd_apply_part(
+                    M, C, G, part.data_ptr(), dx.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                    inv.data_ptr(), gamma.data_ptr(), o["dg"].data_ptr(), o["db"].data_ptr(), o["dy"].data_ptr(),
+                    L.ptr(y2), L.ptr(mean2), L.ptr(inv2), L.ptr(gamma2), L.ptr(o["dg2"]), L.ptr(o["db2"]),
+                    L.ptr(o["dy2"]), L.ptr(o["dres"]), sh), "bn_bwd_apply_part")
+            torch.cuda.synchronize()
+            res.append([dx.cpu(), dw.cpu()] + [v.cpu() for v in o.values() if v is not None])
+    assert int(cnt.abs().sum()) == 0
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert torch.equal(a, b)
