@@ -330,7 +330,7 @@ def _save(side, seed, res, desc):
 
 
 # ------------------------------------------------------------------------------------------------ compare
-def compare(out_path, pt=False):
+def compare(out_path, pt=False, seed_range=None):
     from scipy import stats
     rs, os_ = ("pt_reference", "pt_ours") if pt else ("reference", "ours")
 
@@ -339,6 +339,8 @@ def compare(out_path, pt=False):
                 for p in sorted(glob.glob(os.path.join(AP.OUT, f"accproto_{side}_s*.json")))}
     ref, our = runs(rs), runs(os_)
     seeds = sorted(set(ref) & set(our))
+    if seed_range is not None:  # a pre-registered seed block, analysed alone (round 6: 200-295)
+        seeds = [s for s in seeds if seed_range[0] <= s <= seed_range[1]]
 
     def tost(o, r):
         d = 100 * (np.asarray(o) - np.asarray(r))
@@ -379,9 +381,10 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--out", default=None)
     ap.add_argument("--pt", action="store_true")
+    ap.add_argument("--seed-range", default=None, help="compare: only seeds lo-hi (inclusive)")
     a = ap.parse_args()
     if a.cmd == "compare":
-        compare(a.out, a.pt)
+        compare(a.out, a.pt, tuple(int(x) for x in a.seed_range.split("-")) if a.seed_range else None)
         return
     for s in (int(x) for x in a.seeds.split(",")):
         if a.cmd == "reference":
