@@ -159,7 +159,7 @@ def bwd_pairs(ops, timings, args, dev, topk=4):
         def top(k):
             res = []
             for _, a in sorted(timings[k]):
-                if len(a) == 6 and a[5] == 1 and a not in res:
+                if len(a) == 6 and a[5] in (1, 4) and a not in res:
                     res.append(a)
                 if len(res) == topk:
                     break
@@ -168,6 +168,8 @@ def bwd_pairs(ops, timings, args, dev, topk=4):
         b = Bufs(s, stem, dev)
         best = None
         for ad, aw in itertools.product(top(key), top(wkey)):
+            if ad[5] != aw[5]:  # one launch, one kernel build
+                continue
             A, W = L.ConvAlgo(*ad), L.ConvAlgo(*aw)
             if not lib.tspm_conv_bwd_supported(ctypes.byref(s), ctypes.byref(A), ctypes.byref(W), ctypes.byref(xs)):
                 continue
@@ -232,9 +234,18 @@ LDS_SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32]
 MAX_WGS = int(os.environ.get("TUNE_MAX_WGS", "0"))  # > 0: only grids up to this many workgroups
 
 
-def lds_candidates(kind, s):
-    """Supported variant-1 (LDS-staged) configurations of one launch, with split-K only while the
-    grid stays under ~2048 workgroups (TUNE_MAX_WGS: a tighter cap, for concurrency experiments)."""
+def lds_candidates(kind, s, variants=(1,)):
+    """Supported LDS-staged configurations of one launch (variant 1; with --variants also 2 and / or 4 — variant 4
+    takes wk <= 2 only), with split-K only while the grid stays under ~2048 workgroups (TUNE_MAX_WGS: a tighter cap,
+    for concurrency experiments)."""
+    for v in variants:
+        for a in _lds_candidates_v1(kind, s):
+            if v == 4 and a[3] > 2:
+                continue
+            yield a[:5] + (v,)
+
+
+def _lds_candidates_v1(kind, s):
     for (tm, tn), (wn, wk) in itertools.product(LDS_TILES, LDS_WAVES):
         wm = 4 // (wn * wk)
         bm, bn = wm * tm * 32, wn * tn * 32
@@ -267,7 +278,9 @@ def main():
     ap.add_argument("--only-kind", default=None)
     ap.add_argument("--encoders", default="audio,image", help="audio (ResNet18), image (ResNet34) or both")
     ap.add_argument("--no-bwd", action="store_true", help="skip the fused dgrad + wgrad pair pass")
+    ap.add_argument("--variants", default="1", help="LDS variants to search: 1 (default), 2, 4 (comma-separated)")
     args = ap.parse_args()
+    variants = tuple(int(v) for v in args.variants.split(","))
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -289,7 +302,7 @@ def main():
         best = (tuple(base), t_base)
         timings[key] = [(t_base, tuple(base))] if t_base is not None else []
         n_ok = 0
-        cands = [] if stem else list(lds_candidates(kind, s))
+        cands = [] if stem else list(lds_candidates(kind, s, variants))
         for algo in cands:
             f, out = launcher(kind, s, xs, b, algo)
             out.fill_(float("nan"))

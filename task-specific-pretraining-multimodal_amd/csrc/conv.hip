@@ -635,16 +635,20 @@ Algo wgrad_algo(const tspm_conv_shape* s, const tspm_conv_algo* user) {
   return pick(user, s->k, cols, iters, true);
 }
 
-// variants 1 and 2 (LDS-staged, conv_lds.hip: register-staged loader waves / single-role LDS-DMA ring):
+// variants 1, 2 and 4 (LDS-staged, conv_lds.hip: register-staged loader waves / single-role LDS-DMA ring / the
+// register-staged kernels with exact three-piece bf16 products):
 // wm = 4 / (wn * wk)
 // the per-call launch options of ABI 21 (tspm_conv_algo.lds_floor / flags) are in range
 bool opts_ok(const tspm_conv_algo* u) {
   return !u || (u->lds_floor >= 0 && u->lds_floor <= 160 * 1024 && (u->flags & ~TSPM_ALGO_HANDOFF_ACQUIRE) == 0);
 }
-bool is_lds(const tspm_conv_algo* user) { return user && (user->variant == 1 || user->variant == 2); }
+bool is_lds(const tspm_conv_algo* user) {
+  return user && (user->variant == 1 || user->variant == 2 || user->variant == 4);
+}
 bool is_stem(const tspm_conv_algo* user) { return user && user->variant == 3; }
 const tspm_detail::LdsImpl& lds_of(const tspm_conv_algo* user) {
-  return user->variant == 2 ? tspm_detail::lds_impl_dma() : tspm_detail::lds_impl_reg();
+  return user->variant == 2 ? tspm_detail::lds_impl_dma()
+                            : (user->variant == 4 ? tspm_detail::lds_impl_x9() : tspm_detail::lds_impl_reg());
 }
 tspm_detail::LdsAlgo lds_algo(const tspm_conv_algo* u) {
   tspm_detail::LdsAlgo a{u->tm, u->tn, 0, u->wn, u->wk, u->splits > 0 ? u->splits : 1,

@@ -345,6 +345,7 @@ struct LdsImpl {
 };
 const LdsImpl& lds_impl_reg();
 const LdsImpl& lds_impl_dma();
+const LdsImpl& lds_impl_x9();  // variant 4: variant 1 with the fp32 products on bf16 MFMA (exact 3-piece split)
 // Minimum dynamic LDS of an LDS-staged launch (tspm_conv_algo.lds_floor, ABI 21): a caller-chosen floor caps how
 // many of the launch's workgroups share a CU, leaving room for a concurrent stream's kernels.  Passed per call.
 inline size_t lds_with_floor(size_t lds, const LdsAlgo& a) { return std::max(lds, std::min(a.floor, (size_t)160 * 1024)); }

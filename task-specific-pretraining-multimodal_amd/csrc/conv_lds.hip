@@ -79,6 +79,20 @@ constexpr int kThreads = 256;  // compute (MFMA) threads: 4 waves, one per SIMD
 static_assert(TSPM_LOADER_WAVES == 0 || TSPM_LOADER_WAVES == 2, "variant 1 (2) or variant 2 (0)");
 constexpr int kLoaderThreads = TSPM_LOADER_WAVES == 2 ? 256 : 0;
 constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
+// TSPM_LDS_SPLIT (variant 4, the third build of this file): the variant-1 kernels with every fp32 product formed
+// on the bf16 matrix cores.  The loader waves split each fp32 operand exactly into three bf16 pieces
+// (x = h + m + l: h = x truncated to bf16, m = the remainder truncated, l = what is left — at most 8 significant
+// bits each, so the sum is exact) and stage the three planes in LDS; each 16-deep reduction step of a 32x32 tile
+// is the 9 v_mfma_f32_32x32x16_bf16 of all piece pairs.  Every piece product is exact in the fp32 accumulator
+// (8 x 8 significant bits), so each x*w is formed exactly as the sum of its 9 parts; only the grouping of the
+// fp32 additions differs from the f32 MFMA's fmaf chain.  9 x 32 cycles per 16-deep step against 8 x 64 for
+// v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md: bf16 MFMA 1/16 the cycles per FLOP of f32).
+#ifdef TSPM_LDS_SPLIT
+constexpr bool kSplit = true;
+static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the register loader waves");
+#else
+constexpr bool kSplit = false;
+#endif
 // minimum waves per SIMD the register allocation must allow (__launch_bounds__ second argument): with
 // loader waves, 4 (two 512-thread workgroups per CU, so the two encoder streams' conv launches can share
 // CUs) for the one-block-per-wave tiles, 2 for the larger wave tiles (128 VGPRs would spill them)
@@ -175,7 +189,8 @@ struct Cfg {
   static constexpr int TM = TM_, TN = TN_, WM = WM_, WN = WN_, WK = WK_;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   static constexpr int KGW = 4 / WK;                     // 8-k groups per wave per stage
-  static constexpr int STAGE = (BM + BN) * 32;           // floats per stage image (A then B)
+  // floats per stage image (A then B): 32 fp32 per row, or (split build) three planes of 32 bf16 per row
+  static constexpr int STAGE = (BM + BN) * (kSplit ? 48 : 32);
   static constexpr int D = ring_depth<STAGE>();          // LDS ring slots
   static constexpr int NI = (BM + BN) / 32;              // LDS-DMA instructions per thread per stage
   static_assert(WM * WN * WK == 4, "4 waves per workgroup");
@@ -252,6 +267,85 @@ TSPM_DEV void mma_plain(Acc<C::TM, C::TN>& acc, const f32x4 (&A)[C::KGW][C::TM],
         for (int b = 0; b < C::TN; ++b) acc.v[a][b] = mfma32(A[kk][a][j], B[kk][b][j], acc.v[a][b]);
 }
 
+// ---- split build (variant 4): the three-plane bf16 stage image ------------------------------------------------
+// Plane p of an operand with R rows (A: R = BM, B: R = BN) holds 32 bf16 per GEMM row or column, R * 64 bytes; the
+// A planes come first, then the B planes.  Two layouts, by how the operand sits in memory:
+//  * row operands (the reduction index runs along a memory row: fwd x and w, dgrad dy): [row][32 k], 64-B rows of
+//    four 16-B chunks, chunk c of row r at c ^ ((r >> 2) & 3) — the ds_read_b128 fragment reads (32 rows of one
+//    chunk per lane half) then cover all 64 banks in each 16-lane group;
+//  * column operands (the reduction index runs down memory rows: dgrad w, wgrad dy and x): [32 k][R], read with
+//    ds_read_b64_tr_b16 (4 k-rows x 16 columns per 16-lane group, delivered per column); rows of 128 B swap their
+//    64-B halves on k-rows with bit 1 set and rows of >= 256 B rotate their 64-B quarters by k & 3, so the four
+//    k-rows of a transposed read land on distinct banks.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
+// Exact split of 4 fp32 values into three bf16 pieces, packed 2 per dword (element 2i in the low half).
+// h = x truncated to bf16; r = x - h is exact (same sign and binade); m = r truncated; l = r - m (<= 8 significant
+// bits: exact in bf16).  Non-finite inputs stay non-finite (a NaN keeps a NaN piece; an infinity gives inf - inf).
+TSPM_DEV void split3(const f32x4& v, uint2& H, uint2& M, uint2& L) {
+  unsigned hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned xb = __float_as_uint(v[j]);
+    const float r = v[j] - __uint_as_float(xb & 0xffff0000u);
+    const unsigned rb = __float_as_uint(r);
+    hb[j] = xb;
+    mb[j] = rb;
+    lb[j] = __float_as_uint(r - __uint_as_float(rb & 0xffff0000u));
+  }
+  // v_perm_b32: the high halves of (lo, hi) -> one dword
+  H = make_uint2(__builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u), __builtin_amdgcn_perm(hb[3], hb[2], 0x07060302u));
+  M = make_uint2(__builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u), __builtin_amdgcn_perm(mb[3], mb[2], 0x07060302u));
+  L = make_uint2(__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u), __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u));
+}
+// byte offset of (k-row k, column col) in a column plane of CC columns
+template <int CC>
+TSPM_DEV int col_off(int k, int col) {
+  constexpr int RB = CC * 2;
+  const int t = RB <= 64 ? 0 : (RB == 128 ? ((k >> 1) & 1) : (k & 3));
+  return k * RB + ((col * 2) ^ (t << 6));
+}
+// byte offset of 4 consecutive k (fp32 chunk q of the stage, k = 4q..4q+3) of row `row` in a row plane
+TSPM_DEV int row_off(int row, int q) { return row * 64 + ((((q >> 1) ^ ((row >> 2) & 3))) << 4) + ((q & 1) << 3); }
+// the 32x32x16 operand fragment (lane: GEMM row/column lane & 31, k = 16 s + 8 (lane >> 5) + j) of a row plane
+TSPM_DEV bf16x8 frag_row16(const char* plane, int row0, int s, int lane) {
+  const int row = row0 + (lane & 31), c = 2 * s + (lane >> 5);
+  return *reinterpret_cast<const bf16x8*>(plane + row * 64 + ((c ^ ((row >> 2) & 3)) << 4));
+}
+// ... of a column plane: two transposed reads, k-rows 16 s + 8 h + [0, 4) and [4, 8); lane 4q+p of each 16-lane group
+// addresses k-row q, columns 4p..4p+3 of the group's 16 columns
+template <int CC>
+TSPM_DEV bf16x8 frag_col16(const char* plane, int col0, int s, int lane) {
+  const int g = (lane >> 4) & 3, i = lane & 15;
+  const int col = col0 + 16 * (g & 1) + 4 * (i & 3);
+  const int k = 16 * s + 8 * (g >> 1) + (i >> 2);
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(plane + col_off<CC>(k, col)));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(plane + col_off<CC>(k + 4, col)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// a stage piece's byte offset (plane 0 of its operand, relative to the operand's first plane): the loader's lane
+// mapping of the row operands (row (i*4+wv)*8 + lane/8, fp32 chunk (lane & 7) ^ swz(row) — the bodies pre-swizzle
+// the global address) and of the column operands (element e = (i*4+wv)*64 + lane: k-row e / (CC/4), 4 columns)
+template <int CC, bool COL>
+TSPM_DEV int split_piece_off(int i, int wv, int lane) {
+  if constexpr (COL) {
+    const int e = (i * 4 + wv) * 64 + lane;
+    return col_off<CC>(e / (CC / 4), (e % (CC / 4)) * 4);
+  } else {
+    const int row = (i * 4 + wv) * 8 + (lane >> 3);
+    return row_off(row, (lane & 7) ^ swz(row));
+  }
+}
+template <int CC, bool COL>
+TSPM_DEV bf16x8 split_frag(const char* plane, int blk0, int s, int lane) {
+  if constexpr (COL) return frag_col16<CC>(plane, blk0, s, lane);
+  else return frag_row16(plane, blk0, s, lane);
+}
+
 // LDS-DMA ring over stages [st0, st1): C::D stage slots of C::STAGE floats.  prep(st) returns the
 // operand offsets of stage st, issue_i(off, slot, i) issues this thread's i-th of C::NI
 // global_load_lds (16 B per lane, lane-linear destination) of that stage into the slot,
@@ -303,13 +397,100 @@ struct LoopClock {
 #define TSPM_LOOP_FLUSH() do {} while (0)
 #endif
 
-template <class C, class Prep, class Src, class Dst, class Frags>
+// ACOL / BCOL (split build only): the A / B operand is a column operand (see the split image above); the split
+// build ignores dst_i and frags and places / reads the three planes itself.
+template <class C, bool ACOL = false, bool BCOL = false, class Prep, class Src, class Dst, class Frags>
 TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Prep&& prep, Src&& src_i, Dst&& dst_i,
                         Frags&& frags) {
   constexpr int D = C::D, NI = C::NI, SF = C::STAGE;
+  constexpr int NA = C::BM / 32;                          // loader pieces of the A operand
+  constexpr int PA = C::BM * 64, PB = C::BN * 64;         // split build: bytes per bf16 plane of A / B
   const int n = st1 - st0;
   const bool loader = is_loader_wave();
   if (n <= 0) return loader;
+  if constexpr (kSplit) {
+    const int lane = threadIdx.x & 63;
+    if (loader) {
+      const int wv = (threadIdx.x >> 6) & 3;
+      constexpr int RS = reg_stages<NI>();
+      f32x4 R[RS][NI];
+      int doff[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        doff[i] = i < NA ? split_piece_off<C::BM, ACOL>(i, wv, lane)
+                         : 3 * PA + split_piece_off<C::BN, BCOL>(i - NA, wv, lane);
+      auto load = [&](int st, f32x4 (&Rb)[NI]) {
+        const Off off = prep(st);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
+      };
+      auto store = [&](int it, f32x4 (&Rb)[NI]) {
+        char* slot = reinterpret_cast<char*>(lds + (it & 1) * SF);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          uint2 h, m, l;
+          split3(Rb[i], h, m, l);
+          const int ps = i < NA ? PA : PB;
+          *reinterpret_cast<uint2*>(slot + doff[i]) = h;
+          *reinterpret_cast<uint2*>(slot + doff[i] + ps) = m;
+          *reinterpret_cast<uint2*>(slot + doff[i] + 2 * ps) = l;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      };
+      // the variant-1 loader loop (unconditional loads, full trips one basic block): see below
+      const int last = st1 - 1;
+#pragma unroll
+      for (int j = 0; j < RS; ++j) load(min(st0 + j, last), R[j]);
+      int it = 0;
+      for (; it + RS <= n; it += RS) {
+#pragma unroll
+        for (int j = 0; j < RS; ++j) {
+          store(it + j, R[j]);
+          load(min(st0 + it + j + RS, last), R[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RS - 1; ++j)
+        if (it + j < n) store(it + j, R[j]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      return true;
+    }
+    static_assert(C::WK <= 2, "split build: each wave takes whole 16-deep steps");
+    const WaveId<C> id;
+    constexpr int NS = 2 / C::WK;  // 16-deep steps per wave per stage
+    for (int it = 0; it < n; ++it) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* img = reinterpret_cast<const char*>(lds + (it % D) * SF);
+#pragma unroll
+      for (int ss = 0; ss < NS; ++ss) {
+        const int s = id.wk * NS + ss;
+        bf16x8 A[3][C::TM], B[3][C::TN];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+          for (int a = 0; a < C::TM; ++a)
+            A[p][a] = split_frag<C::BM, ACOL>(img + p * PA, (id.wm * C::TM + a) * 32, s, lane);
+#pragma unroll
+          for (int b = 0; b < C::TN; ++b)
+            B[p][b] = split_frag<C::BN, BCOL>(img + 3 * PA + p * PB, (id.wn * C::TN + b) * 32, s, lane);
+        }
+        // the 9 piece products, smallest first
+        constexpr int PQ[9][2] = {{2, 2}, {1, 2}, {2, 1}, {0, 2}, {1, 1}, {2, 0}, {0, 1}, {1, 0}, {0, 0}};
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+            for (int b = 0; b < C::TN; ++b)
+              acc.v[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[PQ[t][0]][a], B[PQ[t][1]][b], acc.v[a][b], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    return false;
+  }
   if constexpr (kLoaderThreads > 0) {
     if (loader) {
       const int lane4 = (threadIdx.x & 63) * 4;
@@ -778,7 +959,7 @@ TSPM_DEV void dgrad_body(const ConvArgs& g, const float* __restrict__ dy, const 
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  if (ring_loop<C>(
+  if (ring_loop<C, false, true>(
       acc, lds, st0, st1,
       [&](int st) -> Off {
         const int t = st / kb, k0 = (st - t * kb) << 5;
@@ -870,7 +1051,7 @@ TSPM_DEV void wgrad_body(const ConvArgs& g, const float* __restrict__ x, const f
   }
   Acc<C::TM, C::TN> acc;
   acc.zero();
-  if (ring_loop<C>(
+  if (ring_loop<C, true, true>(
       acc, lds, st0, st1,
       [&](int st) -> Off {
         const int pc = st / n32, nc = st - pc * n32;
@@ -1032,13 +1213,14 @@ bool algo_ok(const LdsAlgo& a) {
   // in round 5 with the round-3 fragment-prefetch experiment that raced on them)
   if (!((a.tm == 1 && (a.tn == 1 || a.tn == 2)) || (a.tm == 2 && a.tn == 1))) return false;
   if (!(a.wm >= 1 && a.wn >= 1 && a.wk >= 1 && a.wm * a.wn * a.wk == 4)) return false;
+  if (kSplit && a.wk > 2) return false;
   return a.splits >= 1 && a.splits <= 256;
 }
 int bm_of(const LdsAlgo& a) { return a.wm * a.tm * 32; }
 int bn_of(const LdsAlgo& a) { return a.wn * a.tn * 32; }
 
 size_t lds_bytes(const LdsAlgo& a, bool bn_tail) {
-  const size_t st1 = (size_t)(bm_of(a) + bn_of(a)) * 32 * sizeof(float);
+  const size_t st1 = (size_t)(bm_of(a) + bn_of(a)) * (kSplit ? 48 : 32) * sizeof(float);  // = Cfg::STAGE
   int depth = kRegStage ? 2 : TSPM_RING_MAX;  // = ring_depth<>
   while (depth > 2 && st1 * depth > TSPM_RING_BYTES) --depth;
   const size_t stage = depth * st1;
@@ -1091,7 +1273,13 @@ bool slab_fits(int splits, long long rows, long long cols) { return splits <= 1 
   TSPM_LDS_CASE(TM_, TN_, 1, 4, 1, FN)    \
   TSPM_LDS_CASE(TM_, TN_, 2, 1, 2, FN)    \
   TSPM_LDS_CASE(TM_, TN_, 1, 2, 2, FN)    \
-  TSPM_LDS_CASE(TM_, TN_, 1, 1, 4, FN)
+  TSPM_LDS_CASE_WK4(TM_, TN_, FN)
+// wk == 4 (8-deep slices of a stage per wave): not in the split build, whose waves take whole 16-deep steps
+#ifdef TSPM_LDS_SPLIT
+#define TSPM_LDS_CASE_WK4(TM_, TN_, FN)
+#else
+#define TSPM_LDS_CASE_WK4(TM_, TN_, FN) TSPM_LDS_CASE(TM_, TN_, 1, 1, 4, FN)
+#endif
 #define TSPM_LDS_DISPATCH(FN)   \
   TSPM_LDS_WAVES(1, 1, FN)      \
   TSPM_LDS_WAVES(1, 2, FN)      \
@@ -1333,7 +1521,9 @@ bool bwd_w(const LdsAlgo& aw, const BwdLaunch* L) {  // L == nullptr: query only
     return true;                                                \
   }
   TSPM_BW(1, 2, 2, 1)
+#ifndef TSPM_LDS_SPLIT
   TSPM_BW(1, 1, 1, 4)
+#endif
   TSPM_BW(1, 1, 2, 2)
   TSPM_BW(1, 2, 1, 2)
   TSPM_BW(2, 2, 2, 1)
@@ -1345,7 +1535,9 @@ bool bwd_dispatch(const LdsAlgo& ad, const LdsAlgo& aw, const BwdLaunch* L) {
   if (is_cfg(ad, TM_, WM_, WN_, WK_)) return bwd_w<Cfg<TM_, 1, WM_, WN_, WK_>>(aw, L);
   TSPM_BD(1, 1, 2, 2)
   TSPM_BD(1, 1, 4, 1)
+#ifndef TSPM_LDS_SPLIT
   TSPM_BD(1, 1, 1, 4)
+#endif
   TSPM_BD(2, 2, 2, 1)
   TSPM_BD(2, 1, 4, 1)
 #undef TSPM_BD

@@ -149,12 +149,14 @@ def conv_wgrad(x_nchw: torch.Tensor, dy_nchw: torch.Tensor, rs, stride: int, pad
 
 
 def lds_supported(kind: str, case, algo) -> bool:
-    """Mirror of the variant-1 (LDS-staged) support rules in include/tspm.h."""
+    """Mirror of the variant-1/2/4 (LDS-staged) support rules in include/tspm.h."""
     n, c, h, w, k, r, s, st, pad = case
     tm, tn, wn, wk, sp = algo[:5]
-    if len(algo) < 6 or algo[5] not in (1, 2):
+    if len(algo) < 6 or algo[5] not in (1, 2, 4):
         return True
     if wn * wk == 0 or 4 % (wn * wk):
+        return False
+    if algo[5] == 4 and wk > 2:  # variant 4 (bf16-piece products): waves take whole 16-deep steps
         return False
     wm = 4 // (wn * wk)
     bm, bn = wm * tm * 32, wn * tn * 32

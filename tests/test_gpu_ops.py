@@ -43,7 +43,11 @@ ALGOS = [(0, 0, 0, 0, 0), (1, 1, 1, 1, 1), (2, 2, 2, 2, 1), (1, 2, 1, 8, 1), (1,
 LDS_ALGOS = [(1, 1, 1, 1, 1, 1), (1, 1, 2, 1, 1, 1), (1, 1, 4, 1, 1, 1), (1, 1, 1, 4, 1, 1),
              (1, 2, 1, 2, 3, 1), (2, 1, 1, 4, 2, 1), (1, 1, 2, 2, 5, 1), (2, 1, 2, 1, 2, 1),
              # variant 2: the same kernels with single-role waves and an LDS-DMA ring (the batch-256 / 1024 tables)
-             (1, 1, 2, 1, 1, 2), (2, 1, 1, 4, 2, 2), (1, 1, 2, 2, 5, 2), (1, 2, 1, 1, 2, 2)]
+             (1, 1, 2, 1, 1, 2), (2, 1, 1, 4, 2, 2), (1, 1, 2, 2, 5, 2), (1, 2, 1, 1, 2, 2),
+             # variant 4: variant 1 with each fp32 product formed from exact bf16 pieces on the bf16 MFMA (round 6);
+             # every plane layout (64-, 128-, 256- and 512-byte column rows) and both 16-deep step splits
+             (1, 1, 1, 1, 1, 4), (1, 1, 2, 1, 1, 4), (1, 1, 4, 1, 1, 4), (1, 2, 1, 2, 3, 4), (1, 1, 2, 2, 5, 4),
+             (2, 1, 2, 1, 2, 4), (2, 1, 1, 2, 2, 4), (2, 1, 1, 1, 1, 4)]
 
 
 def _check(out, ref, bound, what):

@@ -1,0 +1,131 @@
+"""Variant 4 (round 6): the LDS-staged conv kernels with every fp32 product formed from an exact three-piece bf16
+split on the bf16 MFMA (csrc/conv_lds.hip, TSPM_LDS_SPLIT).
+
+* Exactness of the split and of the 9 piece products: data chosen so that every output element is ONE product of a
+  full 24-bit-mantissa value and a power of two (one-hot reduction), which the fp32 result holds exactly — the
+  kernel must return it bit for bit whatever its summation order, so a dropped, misplaced or mis-rounded piece of
+  either operand shows.  Forward, data gradient and weight gradient; row and column operand layouts.
+* Accuracy against fp64 at the exact ResNet18 / ResNet34 layer shapes of the bench batch: the §8(c) bound
+  (64 eps sum|w||x|) and, per shape, a maximum normalised error no larger than twice variant 1's (the fp32 MFMA's
+  fmaf chain) plus 2 eps — the bf16-piece path is not a reduced-precision path.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from abi_helpers import conv_bound, conv_dgrad, conv_fwd, conv_wgrad
+
+pytestmark = pytest.mark.gpu
+EPS32 = 2.0 ** -23
+
+# (tm, tn, wn, wk, splits, variant 4): row / column plane widths 64..512 B, 16-deep steps per wave 2 and 1
+SPLIT_ALGOS = [(1, 1, 1, 1, 1, 4), (1, 1, 2, 2, 3, 4), (2, 1, 1, 1, 1, 4), (1, 2, 1, 2, 2, 4), (2, 1, 2, 1, 2, 4)]
+
+
+def _full_mantissa(shape, g):
+    """fp32 values with all 24 significant bits random (so all three bf16 pieces are non-zero), both signs."""
+    m = torch.randint(2 ** 23, 2 ** 24, shape, generator=g, dtype=torch.int64).double()
+    e = torch.randint(-6, 6, shape, generator=g).double()
+    sgn = torch.randint(0, 2, shape, generator=g).double() * 2 - 1
+    return (sgn * m * torch.pow(2.0, e - 23)).float()
+
+
+def _pow2(shape, g):
+    e = torch.randint(-3, 4, shape, generator=g).double()
+    sgn = torch.randint(0, 2, shape, generator=g).double() * 2 - 1
+    return (sgn * torch.pow(2.0, e)).float()
+
+
+@pytest.mark.parametrize("algo", SPLIT_ALGOS)
+@pytest.mark.parametrize("full_side", ["x", "w"])
+def test_split_fwd_single_product_is_exact(gpu, algo, full_side):
+    """1x1 conv, C = K = 64, 256 rows: x[n, c] non-zero only at c = n % C, so y[n, k] = x[n, c_n] * w[k, c_n]."""
+    n, c, k = 256, 64, 64
+    g = torch.Generator().manual_seed(5)
+    onehot = torch.zeros(n, c)
+    onehot[torch.arange(n), torch.arange(n) % c] = 1
+    if full_side == "x":
+        x, wt = _full_mantissa((n, c), g) * onehot, _pow2((k, c), g)
+    else:
+        x, wt = _pow2((n, c), g) * onehot, _full_mantissa((k, c), g)
+    x4, w4 = x.reshape(n, c, 1, 1), wt.reshape(k, c, 1, 1)
+    ref = F.conv2d(x4.double(), w4.double())
+    assert torch.equal(ref.float().double(), ref)  # each output is one product: exact in fp32
+    out = conv_fwd(x4.to(gpu), w4.to(gpu), 1, 0, algo).cpu()
+    assert torch.equal(out.double(), ref), f"{algo}: {(out.double() != ref).sum().item()} elements differ"
+
+
+@pytest.mark.parametrize("algo", SPLIT_ALGOS)
+@pytest.mark.parametrize("full_side", ["dy", "w"])
+def test_split_dgrad_single_product_is_exact(gpu, algo, full_side):
+    """dx[n, c] = sum_k dy[n, k] w[k, c] with dy one-hot in k (column operand w read by transposed LDS reads)."""
+    n, c, k = 256, 64, 64
+    g = torch.Generator().manual_seed(6)
+    onehot = torch.zeros(n, k)
+    onehot[torch.arange(n), (3 * torch.arange(n)) % k] = 1
+    if full_side == "dy":
+        dy, wt = _full_mantissa((n, k), g) * onehot, _pow2((k, c), g)
+    else:
+        dy, wt = _pow2((n, k), g) * onehot, _full_mantissa((k, c), g)
+    dy4, w4 = dy.reshape(n, k, 1, 1), wt.reshape(k, c, 1, 1)
+    ref = torch.nn.grad.conv2d_input((n, c, 1, 1), w4.double(), dy4.double())
+    out = conv_dgrad(dy4.to(gpu), w4.to(gpu), (1, 1), 1, 0, algo).cpu()
+    assert torch.equal(out.double(), ref), f"{algo}: {(out.double() != ref).sum().item()} elements differ"
+
+
+@pytest.mark.parametrize("algo", SPLIT_ALGOS)
+@pytest.mark.parametrize("full_side", ["x", "dy"])
+def test_split_wgrad_single_product_is_exact(gpu, algo, full_side):
+    """dw[k, c] = sum_n dy[n, k] x[n, c] with dy[n, k] non-zero only at n = k (both operands column operands)."""
+    n, c, k = 256, 64, 64
+    g = torch.Generator().manual_seed(7)
+    onehot = torch.zeros(n, k)
+    onehot[torch.arange(k), torch.arange(k)] = 1
+    if full_side == "x":
+        x, dy = _full_mantissa((n, c), g), _pow2((n, k), g) * onehot
+    else:
+        x, dy = _pow2((n, c), g), _full_mantissa((n, k), g) * onehot
+    x4, dy4 = x.reshape(n, c, 1, 1), dy.reshape(n, k, 1, 1)
+    ref = torch.nn.grad.conv2d_weight(x4.double(), (k, c, 1, 1), dy4.double())
+    out = conv_wgrad(x4.to(gpu), dy4.to(gpu), (1, 1), 1, 0, algo).cpu()
+    assert torch.equal(out.double(), ref), f"{algo}: {(out.double() != ref).sum().item()} elements differ"
+
+
+# exact layer shapes of the bench step (batch 128): R34 layer1-4, R18-audio layer3/4 incl. the 1x1 downsample
+SHAPES = [
+    (128, 64, 7, 7, 64, 3, 3, 1, 1),
+    (128, 64, 7, 7, 128, 3, 3, 2, 1),
+    (128, 128, 4, 4, 128, 3, 3, 1, 1),
+    (128, 256, 2, 2, 256, 3, 3, 1, 1),
+    (128, 512, 1, 1, 512, 3, 3, 1, 1),
+    (128, 256, 2, 6, 512, 3, 3, 2, 1),
+    (128, 256, 2, 6, 512, 1, 1, 2, 0),
+]
+
+
+def _ratio(out, ref, bound):
+    return ((out.double().cpu() - ref).abs() / (bound + 1e-30)).max().item()
+
+
+@pytest.mark.parametrize("case", SHAPES)
+def test_split_accuracy_matches_fp32_mfma(gpu, case):
+    n, c, h, w, k, r, s, st, pad = case
+    g = torch.Generator().manual_seed(hash(case) % (2 ** 31))
+    x = torch.randn(n, c, h, w, generator=g)
+    wt = torch.randn(k, c, r, s, generator=g) * 0.05
+    p, q = (h + 2 * pad - r) // st + 1, (w + 2 * pad - s) // st + 1
+    dy = torch.randn(n, k, p, q, generator=g)
+    v1, v4 = (1, 1, 2, 1, 1, 1), (1, 1, 2, 1, 1, 4)
+    ref = F.conv2d(x.double(), wt.double(), None, st, pad)
+    bound = conv_bound(x, wt, st, pad)
+    rd = torch.nn.grad.conv2d_input((n, c, h, w), wt.double(), dy.double(), st, pad)
+    bd = torch.nn.grad.conv2d_input((n, c, h, w), wt.double().abs(), dy.double().abs(), st, pad)
+    rw = torch.nn.grad.conv2d_weight(x.double(), (k, c, r, s), dy.double(), st, pad)
+    bw = torch.nn.grad.conv2d_weight(x.double().abs(), (k, c, r, s), dy.double().abs(), st, pad)
+    xg, wg, dyg = x.to(gpu), wt.to(gpu), dy.to(gpu)
+    for what, run, rf, bd_ in (("fwd", lambda a: conv_fwd(xg, wg, st, pad, a), ref, bound),
+                               ("dgrad", lambda a: conv_dgrad(dyg, wg, (h, w), st, pad, a), rd, bd),
+                               ("wgrad", lambda a: conv_wgrad(xg, dyg, (r, s), st, pad, a), rw, bw)):
+        e1, e4 = _ratio(run(v1), rf, bd_), _ratio(run(v4), rf, bd_)
+        assert e4 <= 64 * EPS32, f"{what} {case}: variant 4 error {e4 / EPS32:.2f} eps beyond the 64-eps bound"
+        assert e4 <= 2 * e1 + 2 * EPS32, f"{what} {case}: variant 4 {e4 / EPS32:.2f} eps vs variant 1 {e1 / EPS32:.2f}"
