@@ -37,6 +37,7 @@ from conv_bench import step_ops  # noqa: E402
 from tune_convs import Bufs, bwd_launcher, graph_time, launcher, lds_candidates  # noqa: E402
 
 B = int(os.environ.get("TUNE_BATCH", "128"))  # per-rank batch of the tuned step
+VARIANTS = tuple(int(v) for v in os.environ.get("TUNE_VARIANTS", "1").split(","))  # LDS variants searched
 
 
 def build(table, dev):
@@ -90,9 +91,11 @@ def candidates(kind, s, xs, base, top, dev):
     timed, seen = [], {tuple(base)}
     neigh = []
     for sp in (base[4] // 2, base[4] * 2):
-        if sp >= 1 and base[5] == 1:
-            neigh.append(tuple(base[:4]) + (sp, 1))
-    allc = list(lds_candidates(kind, s))
+        if sp >= 1 and base[5] in (1, 4):
+            neigh.append(tuple(base[:4]) + (sp, base[5]))
+    if base[5] in (1, 2) and base[3] <= 2:  # round 6: the variant-4 twin (bf16-piece products) of the current config
+        neigh.append(tuple(base[:5]) + (4,))
+    allc = list(lds_candidates(kind, s, VARIANTS))
     for algo in neigh + allc:
         algo = tuple(algo)
         if algo in seen:
@@ -131,6 +134,16 @@ def bwd_candidates(s, xs, base, dev):
     rdx, rdw = b.dx.clone(), b.dw.clone()
     sx, sw = float(rdx.abs().max()) + 1e-30, float(rdw.abs().max()) + 1e-30
     out = []
+    if ad[5] == aw[5] and ad[5] in (1, 2) and ad[3] <= 2 and aw[3] <= 2:  # round 6: the pair's variant-4 twin
+        d, w = ad[:5] + (4,), aw[:5] + (4,)
+        A, W = L.ConvAlgo(*d), L.ConvAlgo(*w)
+        if lib.tspm_conv_bwd_supported(ctypes.byref(s), ctypes.byref(A), ctypes.byref(W), ctypes.byref(xs)):
+            b.dx.fill_(float("nan"))
+            b.dw.fill_(float("nan"))
+            if bwd_launcher(s, xs, b, d, w)() == 0:
+                torch.cuda.synchronize()
+                if float((b.dx - rdx).abs().max()) <= 1e-5 * sx and float((b.dw - rdw).abs().max()) <= 1e-5 * sw:
+                    out.append(d + w)
     for side in (0, 1):
         for f in (0.5, 2.0):
             d, w = list(ad), list(aw)
