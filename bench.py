@@ -159,7 +159,10 @@ def conv_roofline(seq, run_serial, replays: int, run_concurrent=None):
            "achieved": flops / (conv_us * 1e-6) / 1e12 if conv_us else None,
            "kernel_ms_per_step": sum(k["dur"] for k in ks) / replays / 1e3, "kernels_per_step": len(ks) / replays,
            "conv_launches_per_step": len(seq), "families": {}, "profiled_steps": replays,
-           "incomplete_steps_dropped": dropped}
+           "incomplete_steps_dropped": dropped,
+           # round 6: the share of the conv family's device time in the variant-4 kernels (k_*_x9: fp32 products
+           # from exact bf16 pieces on the bf16 MFMA), whose own product-rate ceiling is 2.5 PF / 9 bf16 products
+           "x9_conv_ms_per_step": sum(k["dur"] for k in conv if "_x9" in k["name"]) / replays / 1e3}
     for k in ks:
         fam = ("conv" if CONV_KERNEL.search(k["name"]) else "bn" if "k_bn_" in k["name"] else
                "adam" if "k_adam" in k["name"] else "pool" if "pool" in k["name"] else "other")
@@ -1246,7 +1249,9 @@ def main() -> None:
         rl = {"bound": "mfma", "kernel": "conv implicit-GEMM family (k_fwd_lds, k_fwd_pair_lds = a downsampling "
                                          "block's conv1 + 1x1 downsample, k_bwd_lds = dgrad+wgrad, k_bwd_quad_lds = "
                                          "conv2 + downsample dgrad+wgrad, k_dgrad_lds, k_wgrad_lds, stem k_stem_* / "
-                                         "k_conv_*), fp32 MFMA 32x32x2",
+                                         "k_conv_*; the variant-4 builds k_*_x9 form each fp32 product from an exact "
+                                         "3-piece bf16 split, 9 bf16 MFMA 32x32x16 per 16-deep step), fp32 MFMA "
+                                         "32x32x2; peak = the fp32 MFMA peak for the whole family",
               "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": traffic,
               "traffic_unit": "HBM bytes per step of the conv family (PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
               "traffic_per_launch": round(traffic / traffic_launches) if traffic else None,
@@ -1262,6 +1267,7 @@ def main() -> None:
             ach = roof["achieved"]
             rl.update({"achieved": round(ach, 3), "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                        "conv_ms_per_step": round(roof["conv_kernel_ms_per_step"], 4),
+                       "x9_conv_ms_per_step": round(roof["x9_conv_ms_per_step"], 4),
                        "valid_tap_flop_per_step": roof["valid_tap_flop_per_step"],
                        "launches_per_step": roof["conv_launches_per_step"],
                        "kernels_per_step": roof["kernels_per_step"],

@@ -20,7 +20,7 @@ import re
 import sys
 from collections import defaultdict
 
-CONV = re.compile(r"k_(fwd|dgrad|wgrad|bwd)_lds|k_conv_|k_stem_|k_reduce_slabs")
+CONV = re.compile(r"k_(fwd|dgrad|wgrad|bwd)_(lds|x9)|k_(fwd_pair|bwd_quad)_(lds|x9)|k_conv_|k_stem_|k_reduce_slabs")
 CLOCK_MAX_HZ = 2.4e9
 SIMDS = 256 * 4
 

@@ -16,7 +16,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-FAMILIES = [("conv", ("k_fwd_lds", "k_fwd_pair_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k_bwd_quad_lds", "k_conv_", "k_stem_", "k_reduce_slabs")),
+FAMILIES = [("conv", ("k_fwd_lds", "k_fwd_pair_lds", "k_dgrad_lds", "k_wgrad_lds", "k_bwd_lds", "k_bwd_quad_lds", "k_fwd_x9", "k_fwd_pair_x9", "k_dgrad_x9", "k_wgrad_x9", "k_bwd_x9", "k_bwd_quad_x9", "k_conv_", "k_stem_", "k_reduce_slabs")),
             ("bn", ("k_bn_", "k_bn1d")), ("pool", ("k_maxpool", "k_avgpool")), ("adam", ("k_adam",)),
             ("gather", ("k_avmnist_gather",)), ("head", ("k_head_", "k_gemm_small", "k_gemm_pair", "k_splitk_reduce",
                                                          "k_cross_entropy", "k_act_bwd", "k_dropout")),

@@ -15,7 +15,7 @@ import statistics
 import sys
 from collections import Counter, defaultdict
 
-CONV = re.compile(r"\bk_(fwd_lds|fwd_pair_lds|bwd_lds|bwd_quad_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|conv_wgrad|"
+CONV = re.compile(r"\bk_(fwd_lds|fwd_pair_lds|bwd_lds|bwd_quad_lds|dgrad_lds|wgrad_lds|fwd_x9|fwd_pair_x9|bwd_x9|bwd_quad_x9|dgrad_x9|wgrad_x9|conv_fwd_vec|conv_fwd_gather|conv_dgrad|conv_wgrad|"
                   r"conv_wgrad_t|reduce_slabs|reduce_slabs_wide)\b")
 PEAK = 157.3
 FLOPS = 82030559232  # valid-tap FLOPs of the conv launches of one batch-128 step (bench.py line)

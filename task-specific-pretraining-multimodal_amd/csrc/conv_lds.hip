@@ -90,6 +90,13 @@ constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
 #ifdef TSPM_LDS_SPLIT
 constexpr bool kSplit = true;
 static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the register loader waves");
+// the split build's kernels carry their own names (k_fwd_x9, ...) so that traces tell the two builds apart
+#define k_fwd_lds k_fwd_x9
+#define k_fwd_pair_lds k_fwd_pair_x9
+#define k_dgrad_lds k_dgrad_x9
+#define k_wgrad_lds k_wgrad_x9
+#define k_bwd_lds k_bwd_x9
+#define k_bwd_quad_lds k_bwd_quad_x9
 #else
 constexpr bool kSplit = false;
 #endif

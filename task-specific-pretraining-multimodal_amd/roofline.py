@@ -104,7 +104,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
 # ------------------------------------------------------------------------------------------------
 import re as _re
 
-CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|fwd_pair_lds|bwd_lds|bwd_quad_lds|dgrad_lds|wgrad_lds|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
+CONV_KERNEL = _re.compile(r"\bk_(fwd_lds|fwd_pair_lds|bwd_lds|bwd_quad_lds|dgrad_lds|wgrad_lds|fwd_x9|fwd_pair_x9|bwd_x9|bwd_quad_x9|dgrad_x9|wgrad_x9|conv_fwd_vec|conv_fwd_gather|conv_dgrad|"
                           r"conv_wgrad|conv_wgrad_t|stem_fwd|stem_wgrad|reduce_slabs|reduce_slabs_wide)\b")
 CONV_SECONDARY = _re.compile(r"\bk_reduce_slabs(_wide)?\b")  # second kernel of a split-K wgrad launch (variant 0)
 
