@@ -433,10 +433,14 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
       };
       auto store = [&](int it, f32x4 (&Rb)[NI]) {
         char* slot = reinterpret_cast<char*>(lds + (it & 1) * SF);
+        const unsigned neg = (it & 1) ? 0x80008000u : 0u;  // odd stages stage -A (see the compute loop)
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           uint2 h, m, l;
           split3(Rb[i], h, m, l);
+          if (i < NA) {
+            h.x ^= neg; h.y ^= neg; m.x ^= neg; m.y ^= neg; l.x ^= neg; l.y ^= neg;
+          }
           const int ps = i < NA ? PA : PB;
           *reinterpret_cast<uint2*>(slot + doff[i]) = h;
           *reinterpret_cast<uint2*>(slot + doff[i] + ps) = m;
@@ -467,7 +471,24 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
     static_assert(C::WK <= 2, "split build: each wave takes whole 16-deep steps");
     const WaveId<C> id;
     constexpr int NS = 2 / C::WK;  // 16-deep steps per wave per stage
+    // Sign alternation.  The bf16 MFMA's accumulation is not an unbiased rounding: measured against fp64
+    // (scripts/split_bias.py) its error has a mean of about -3e-8 of the mean |result| whatever the signs of the
+    // data (a two's-complement truncation toward -inf), which a long reduction turns into a drift (-2.9e-6 over the
+    // 49k rows of an audio layer1 weight gradient, against +1.5e-8 for the f32 MFMA).  Odd stages therefore stage
+    // -A (the loader flips the pieces' sign bits) and run on the negated accumulator: before stage `it` the
+    // accumulator holds sigma * S (sigma = +1 on even, -1 on odd stages), the stage adds sigma * P, and the
+    // accumulator is negated between stages — so the truncation pushes the true sum down on even stages and up on
+    // odd ones.  Negations are exact; the products are unchanged.
+    auto negate = [&]() {
+#pragma unroll
+      for (int a = 0; a < C::TM; ++a)
+#pragma unroll
+        for (int b = 0; b < C::TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc.v[a][b][r] = -acc.v[a][b][r];
+    };
     for (int it = 0; it < n; ++it) {
+      if (it > 0) negate();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const char* img = reinterpret_cast<const char*>(lds + (it % D) * SF);
@@ -495,6 +516,7 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
               acc.v[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[PQ[t][0]][a], B[PQ[t][1]][b], acc.v[a][b], 0, 0, 0);
       }
     }
+    if (!(n & 1)) negate();  // the last stage (n - 1) was odd
     __builtin_amdgcn_s_barrier();
     return false;
   }
