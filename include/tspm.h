@@ -45,8 +45,9 @@ enum {
  * 20 = tspm_conv_bwd_adam, the fused backward launch carrying an Adam update over earlier-finished parameters,
  * and tspm_head_desc.adam_step; 21 = round 6: no mutable global state and no environment reads inside the library —
  * tspm_set_conv_lds_floor removed, the floor and the hand-off mode are per-call tspm_conv_algo fields, and the
- * head's row block is tspm_head_desc.rows_per_block). */
-#define TSPM_ABI_VERSION 21
+ * head's row block is tspm_head_desc.rows_per_block); 22 = round 6: tspm_conv_algo.variant 4, the LDS-staged kernels with
+ * every fp32 product formed from an exact three-piece bf16 split on the bf16 MFMA (same structs and entry points). */
+#define TSPM_ABI_VERSION 22
 int tspm_abi_version(void);  /* returns TSPM_ABI_VERSION */
 /* Static string for a status code. */
 const char* tspm_status_string(int status);
@@ -81,6 +82,13 @@ typedef struct tspm_conv_shape {
  *   of loads in flight) into two LDS slots.
  * variant 2 — the same tiles and rules with single-role waves: the 4 waves issue the operand loads
  *   themselves as LDS-DMA into a 2-4-slot ring (faster for the batch-256 / 1024 grids; ABI 15).
+ * variant 4 — variant 1's kernels (same tiles, splits, epilogues, fused launches) with every fp32 product formed on
+ *   the bf16 matrix cores: the loader waves split each fp32 operand exactly into three bf16 pieces (x = h + m + l,
+ *   h = x truncated to bf16, m the remainder truncated, l what is left: at most 8 significant bits each, so exact) and
+ *   each 16-deep step of a 32x32 tile is the 9 v_mfma_f32_32x32x16_bf16 of the piece pairs — each product x*w is formed
+ *   exactly as the sum of its 9 exact parts in the fp32 accumulator; the sign of the staged A operand and of the
+ *   accumulator alternates per stage so the bf16 MFMA's truncating accumulation does not bias long reductions.
+ *   wk <= 2 (the waves take whole 16-deep steps).  Round 6, ABI 22.
  * variant 3 — the ResNet stems only (c == 1, 7x7, stride 2, pad 3, k == 64; forward and weight
  *   gradient; the other fields are ignored): a workgroup owns one image and a band of output rows,
  *   stages the band's input rows (and, for the weight gradient, its dy rows) in LDS and runs the band
