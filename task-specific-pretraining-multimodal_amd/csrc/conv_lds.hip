@@ -89,6 +89,11 @@ constexpr bool kRegStage = TSPM_LOADER_WAVES == 2;
 // v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md: bf16 MFMA 1/16 the cycles per FLOP of f32).
 #ifdef TSPM_LDS_SPLIT
 constexpr bool kSplit = true;
+// wk == 1 tiles: stages per sign block of the bias-cancelling sign alternation (ring_loop)
+#ifndef TSPM_SPLIT_SIGN_EVERY
+#define TSPM_SPLIT_SIGN_EVERY 1
+#endif
+constexpr int kSignEvery = TSPM_SPLIT_SIGN_EVERY;
 static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the register loader waves");
 // the split build's kernels carry their own names (k_fwd_x9, ...) so that traces tell the two builds apart
 #define k_fwd_lds k_fwd_x9
@@ -99,6 +104,7 @@ static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the regist
 #define k_bwd_quad_lds k_bwd_quad_x9
 #else
 constexpr bool kSplit = false;
+constexpr int kSignEvery = 1;
 #endif
 // minimum waves per SIMD the register allocation must allow (__launch_bounds__ second argument): with
 // loader waves, 4 (two 512-thread workgroups per CU, so the two encoder streams' conv launches can share
@@ -347,6 +353,16 @@ TSPM_DEV int split_piece_off(int i, int wv, int lane) {
     return row_off(row, (lane & 7) ^ swz(row));
   }
 }
+// the 16-deep step (0 or 1) of the stage a loader piece belongs to (same lane mapping as split_piece_off)
+template <int CC, bool COL>
+TSPM_DEV int split_piece_step(int i, int wv, int lane) {
+  if constexpr (COL) {
+    return ((i * 4 + wv) * 64 + lane) / (CC / 4) >> 4;
+  } else {
+    const int row = (i * 4 + wv) * 8 + (lane >> 3);
+    return ((lane & 7) ^ swz(row)) >> 2;
+  }
+}
 template <int CC, bool COL>
 TSPM_DEV bf16x8 split_frag(const char* plane, int blk0, int s, int lane) {
   if constexpr (COL) return frag_col16<CC>(plane, blk0, s, lane);
@@ -422,10 +438,13 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
       constexpr int RS = reg_stages<NI>();
       f32x4 R[RS][NI];
       int doff[NI];
+      unsigned nstep[NI];  // wk == 2: the sign flip of the A pieces of step 1 (the second wave's half of each stage)
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i) {
         doff[i] = i < NA ? split_piece_off<C::BM, ACOL>(i, wv, lane)
                          : 3 * PA + split_piece_off<C::BN, BCOL>(i - NA, wv, lane);
+        nstep[i] = (C::WK == 2 && i < NA && split_piece_step<C::BM, ACOL>(i, wv, lane) == 1) ? 0x80008000u : 0u;
+      }
       auto load = [&](int st, f32x4 (&Rb)[NI]) {
         const Off off = prep(st);
 #pragma unroll
@@ -433,13 +452,15 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
       };
       auto store = [&](int it, f32x4 (&Rb)[NI]) {
         char* slot = reinterpret_cast<char*>(lds + (it & 1) * SF);
-        const unsigned neg = (it & 1) ? 0x80008000u : 0u;  // odd stages stage -A (see the compute loop)
+        // wk == 1: the A pieces of every other block of kSignEvery stages are staged negated (see the compute loop)
+        const unsigned neg = (C::WK == 1 && ((it / kSignEvery) & 1)) ? 0x80008000u : 0u;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           uint2 h, m, l;
           split3(Rb[i], h, m, l);
           if (i < NA) {
-            h.x ^= neg; h.y ^= neg; m.x ^= neg; m.y ^= neg; l.x ^= neg; l.y ^= neg;
+            const unsigned ng = neg ^ nstep[i];
+            h.x ^= ng; h.y ^= ng; m.x ^= ng; m.y ^= ng; l.x ^= ng; l.y ^= ng;
           }
           const int ps = i < NA ? PA : PB;
           *reinterpret_cast<uint2*>(slot + doff[i]) = h;
@@ -474,11 +495,14 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
     // Sign alternation.  The bf16 MFMA's accumulation is not an unbiased rounding: measured against fp64
     // (scripts/split_bias.py) its error has a mean of about -3e-8 of the mean |result| whatever the signs of the
     // data (a two's-complement truncation toward -inf), which a long reduction turns into a drift (-2.9e-6 over the
-    // 49k rows of an audio layer1 weight gradient, against +1.5e-8 for the f32 MFMA).  Odd stages therefore stage
-    // -A (the loader flips the pieces' sign bits) and run on the negated accumulator: before stage `it` the
-    // accumulator holds sigma * S (sigma = +1 on even, -1 on odd stages), the stage adds sigma * P, and the
-    // accumulator is negated between stages — so the truncation pushes the true sum down on even stages and up on
-    // odd ones.  Negations are exact; the products are unchanged.
+    // 49k rows of an audio layer1 weight gradient, against +1.5e-8 for the f32 MFMA).  So half of every reduction
+    // runs negated, and the truncation pushes the true sum down in one half and up in the other:
+    //  * wk == 2: the second wave's steps (k 16..31 of each stage) are staged as -A (the loader flips the pieces'
+    //    sign bits); that wave accumulates -S1 and negates its accumulator once before the k-slice combine — no
+    //    per-stage cost;
+    //  * wk == 1: blocks of kSignEvery stages alternate: the loader stages -A on odd blocks and the accumulator,
+    //    which holds sigma * S (sigma = the block's sign), is negated between blocks (a wait for the MFMA chain).
+    // Negations are exact; the products are unchanged.
     auto negate = [&]() {
 #pragma unroll
       for (int a = 0; a < C::TM; ++a)
@@ -488,7 +512,7 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
           for (int r = 0; r < 16; ++r) acc.v[a][b][r] = -acc.v[a][b][r];
     };
     for (int it = 0; it < n; ++it) {
-      if (it > 0) negate();
+      if (C::WK == 1 && it > 0 && it % kSignEvery == 0) negate();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const char* img = reinterpret_cast<const char*>(lds + (it % D) * SF);
@@ -516,7 +540,7 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
               acc.v[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[PQ[t][0]][a], B[PQ[t][1]][b], acc.v[a][b], 0, 0, 0);
       }
     }
-    if (!(n & 1)) negate();  // the last stage (n - 1) was odd
+    if (C::WK == 1 ? (((n - 1) / kSignEvery) & 1) : id.wk == 1) negate();  // back to +S
     __builtin_amdgcn_s_barrier();
     return false;
   }
