@@ -435,7 +435,11 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
     const int lane = threadIdx.x & 63;
     if (loader) {
       const int wv = (threadIdx.x >> 6) & 3;
+#ifdef TSPM_SPLIT_REG_STAGES  // A/B builds: the split loader's register stages alone
+      constexpr int RS = TSPM_SPLIT_REG_STAGES;
+#else
       constexpr int RS = reg_stages<NI>();
+#endif
       f32x4 R[RS][NI];
       int doff[NI];
       unsigned nstep[NI];  // wk == 2: the sign flip of the A pieces of step 1 (the second wave's half of each stage)
