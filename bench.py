@@ -209,6 +209,8 @@ def exchange_block(step, one, args, world: int, ms_per_step: float) -> dict:
     w0 = [p["host_wait_ms"][0] for p in probe]
     w1 = [p["host_wait_ms"][1] for p in probe]
     tail = [p["events"][0].elapsed_time(p["events"][1]) for p in probe]
+    win0 = [p["window_ms"][0] for p in probe]
+    win1 = [p["window_ms"][1] for p in probe]
     phase_bytes = [sum(v.numel() * 4 for v in ph) for ph in ar.phases]
     step.allreduce, step.graph, step.graph_opt = None, None, None
     for i in range(3):  # capture + settle the local step
@@ -222,7 +224,8 @@ def exchange_block(step, one, args, world: int, ms_per_step: float) -> dict:
         one(i)
     torch.cuda.synchronize()
     local_ms = (time.perf_counter() - t0) / P * 1e3
-    vals = [local_ms, sum(tail) / len(tail), max(tail), sum(w0) / len(w0), sum(w1) / len(w1)]
+    vals = [local_ms, sum(tail) / len(tail), max(tail), sum(w0) / len(w0), sum(w1) / len(w1),
+            sum(win0) / len(win0), sum(win1) / len(win1)]
     if world > 1:
         t = torch.tensor(vals, dtype=torch.float64, device=step.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -230,13 +233,20 @@ def exchange_block(step, one, args, world: int, ms_per_step: float) -> dict:
     out = exchange_summary(vals, phase_bytes, [len(ph) for ph in ar.phases], world, ms_per_step, P)
     out["rank0_tail_ms"] = _stats(tail)
     out["rank0_host_wait_ms"] = {"phase0": _stats(w0), "phase1": _stats(w1)}
+    out["rank0_window_ms"] = {"phase0": _stats(win0), "phase1": _stats(win1)}
     return out
 
 
 def exchange_summary(vals, phase_bytes, buckets, world: int, ms_per_step: float, steps: int) -> dict:
-    """The line's ``exchange`` block from [local_ms, tail_mean, tail_max, wait0_mean, wait1_mean] (maxima over
-    ranks; shared by the GPU bench and the gloo dry run)."""
-    return {"rccl_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+    """The line's ``exchange`` block from [local_ms, tail_mean, tail_max, wait0_mean, wait1_mean[, window0_mean,
+    window1_mean]] (maxima over ranks; shared by the GPU bench and the gloo dry run).  window = the rest of the
+    backward after the host saw a late phase's flag: the span that phase's exchange (+ its Adam ranges) must fit in
+    to stay hidden — at N > 1 compare it with the phase's bytes over the measured RCCL rate (round 6, VERDICT r5
+    item 7)."""
+    win = {}
+    if len(vals) >= 7:
+        win = {"late_phase_window_ms_per_step": {"phase0_mean": round(vals[5], 4), "phase1_mean": round(vals[6], 4)}}
+    return {**win, "rccl_world_size": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": str(dist.get_backend()) if dist.is_initialized() else None,
             "forced_1rank_exchange": world == 1,
             "phases": len(phase_bytes), "bytes_per_phase": phase_bytes, "buckets_per_phase": buckets,
@@ -1044,7 +1054,7 @@ def dry_run(args) -> None:
             for k in range(3):
                 ar.wait(ar.launch(k))
             tails.append((time.perf_counter() - t1) * 1e3)
-        vals = torch.tensor([0.0, sum(tails) / len(tails), max(tails), 0.0, 0.0], dtype=torch.float64)
+        vals = torch.tensor([0.0, sum(tails) / len(tails), max(tails), 0.0, 0.0, 0.0, 0.0], dtype=torch.float64)
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
         exchange = exchange_summary(vals.tolist(), [v.numel() * 4 for ph in ar.phases for v in ph[:1]],
                                     [len(ph) for ph in ar.phases], world, ms_per_step, args.exchange_steps)

@@ -500,7 +500,13 @@ class FusedTrainStep:
         if probe is not None:
             ev_end = torch.cuda.Event(enable_timing=True)
             ev_end.record(main)
-            probe.append({"host_wait_ms": ((t1 - t0) * 1e3, (t3 - t2) * 1e3), "events": (ev_graph, ev_end)})
+            # the window each late phase's exchange has to hide in: from the host seeing that phase's flag to the
+            # end of the fwd+bwd graph (the rest of the backward), host clock, the graph's end polled (probe only)
+            while not ev_graph.query():
+                pass
+            t4 = time.perf_counter()
+            probe.append({"host_wait_ms": ((t1 - t0) * 1e3, (t3 - t2) * 1e3), "events": (ev_graph, ev_end),
+                          "window_ms": ((t4 - t1) * 1e3, (t4 - t3) * 1e3)})
 
     def close(self) -> None:
         """Release the step's device-side resources in a safe order, before the process group goes away

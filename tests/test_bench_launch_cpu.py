@@ -94,4 +94,4 @@ def test_gpus2_line_carries_roofline_cpu_baseline_and_exchange():
     ex = res["exchange"]
     assert ex["rccl_world_size"] == 2 and ex["phases"] == 3 and ex["steps_probed"] == 3
     assert {"exposed_tail_ms_per_step", "host_wait_ms_per_step", "local_step_ms",
-            "exchange_exposed_ms_per_step"} <= set(ex)
+            "exchange_exposed_ms_per_step", "late_phase_window_ms_per_step"} <= set(ex)
