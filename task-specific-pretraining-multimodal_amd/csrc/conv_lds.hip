@@ -94,6 +94,15 @@ constexpr bool kSplit = true;
 #define TSPM_SPLIT_SIGN_EVERY 1
 #endif
 constexpr int kSignEvery = TSPM_SPLIT_SIGN_EVERY;
+// Stage pairs (A/B switch): a 4-slot LDS ring with one loader -> compute barrier per two stages, for tiles whose four
+// stage images fit TSPM_PAIR_MAX_BYTES (so two workgroups still share a CU); other tiles keep 2 slots, 1 barrier per stage
+#ifndef TSPM_SPLIT_PAIR
+#define TSPM_SPLIT_PAIR 0
+#endif
+#ifndef TSPM_PAIR_MAX_BYTES
+#define TSPM_PAIR_MAX_BYTES (80 * 1024)
+#endif
+constexpr bool kPairBuild = TSPM_SPLIT_PAIR != 0;
 static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the register loader waves");
 // the split build's kernels carry their own names (k_fwd_x9, ...) so that traces tell the two builds apart
 #define k_fwd_lds k_fwd_x9
@@ -105,6 +114,8 @@ static_assert(TSPM_LOADER_WAVES == 2, "the split build stages through the regist
 #else
 constexpr bool kSplit = false;
 constexpr int kSignEvery = 1;
+constexpr bool kPairBuild = false;
+#define TSPM_PAIR_MAX_BYTES (80 * 1024)
 #endif
 // minimum waves per SIMD the register allocation must allow (__launch_bounds__ second argument): with
 // loader waves, 4 (two 512-thread workgroups per CU, so the two encoder streams' conv launches can share
@@ -191,7 +202,8 @@ constexpr int reg_stages() {
 }
 template <int STAGE>
 constexpr int ring_depth() {
-  if (kRegStage) return 2;  // register staging: the loads in flight sit in registers
+  // register staging: the loads in flight sit in registers (split build with stage pairs: 4 slots when they fit)
+  if (kRegStage) return (kPairBuild && STAGE * 4 * 4 <= TSPM_PAIR_MAX_BYTES) ? 4 : 2;
   int d = TSPM_RING_MAX;
   while (d > 2 && STAGE * 4 * d > TSPM_RING_BYTES) --d;
   return d;
@@ -455,7 +467,7 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
         for (int i = 0; i < NI; ++i) Rb[i] = *reinterpret_cast<const f32x4*>(src_i(off, i));
       };
       auto store = [&](int it, f32x4 (&Rb)[NI]) {
-        char* slot = reinterpret_cast<char*>(lds + (it & 1) * SF);
+        char* slot = reinterpret_cast<char*>(lds + (it % D) * SF);
         // wk == 1: the A pieces of every other block of kSignEvery stages are staged negated (see the compute loop)
         const unsigned neg = (C::WK == 1 && ((it / kSignEvery) & 1)) ? 0x80008000u : 0u;
 #pragma unroll
@@ -471,8 +483,10 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
           *reinterpret_cast<uint2*>(slot + doff[i] + ps) = m;
           *reinterpret_cast<uint2*>(slot + doff[i] + 2 * ps) = l;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if (D == 2 || (it & 1) || it == n - 1) {  // stage pairs: one barrier per two stages (and after the last)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
       };
       // the variant-1 loader loop (unconditional loads, full trips one basic block): see below
       const int last = st1 - 1;
@@ -517,8 +531,10 @@ TSPM_DEV bool ring_loop(Acc<C::TM, C::TN>& acc, float* lds, int st0, int st1, Pr
     };
     for (int it = 0; it < n; ++it) {
       if (C::WK == 1 && it > 0 && it % kSignEvery == 0) negate();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      if (D == 2 || !(it & 1)) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
       const char* img = reinterpret_cast<const char*>(lds + (it % D) * SF);
 #pragma unroll
       for (int ss = 0; ss < NS; ++ss) {
@@ -1278,8 +1294,8 @@ int bn_of(const LdsAlgo& a) { return a.wn * a.tn * 32; }
 
 size_t lds_bytes(const LdsAlgo& a, bool bn_tail) {
   const size_t st1 = (size_t)(bm_of(a) + bn_of(a)) * (kSplit ? 48 : 32) * sizeof(float);  // = Cfg::STAGE
-  int depth = kRegStage ? 2 : TSPM_RING_MAX;  // = ring_depth<>
-  while (depth > 2 && st1 * depth > TSPM_RING_BYTES) --depth;
+  int depth = kRegStage ? ((kPairBuild && st1 * 4 <= TSPM_PAIR_MAX_BYTES) ? 4 : 2) : TSPM_RING_MAX;  // = ring_depth<>
+  while (!kRegStage && depth > 2 && st1 * depth > TSPM_RING_BYTES) --depth;
   const size_t stage = depth * st1;
   const size_t comb = (size_t)(a.wk - 1) * a.wm * a.wn * a.tm * a.tn * 16 * 64 * sizeof(float);
   const size_t tail = bn_tail ? 16 + 8 * (size_t)(kThreads + bn_of(a)) : 16;
