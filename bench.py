@@ -1278,6 +1278,9 @@ def main() -> None:
             rl.update({"achieved": round(ach, 3), "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                        "conv_ms_per_step": round(roof["conv_kernel_ms_per_step"], 4),
                        "x9_conv_ms_per_step": round(roof["x9_conv_ms_per_step"], 4),
+                       # the variant-4 kernels' own ceiling in fp32 products: dense bf16 MFMA 2.5 PF / 9 piece
+                       # products per fp32 product (frac above keeps the f32 MFMA peak for the whole family)
+                       "x9_fp32_product_peak_tflops": round(2500.0 / 9, 1),
                        "valid_tap_flop_per_step": roof["valid_tap_flop_per_step"],
                        "launches_per_step": roof["conv_launches_per_step"],
                        "kernels_per_step": roof["kernels_per_step"],
