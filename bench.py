@@ -1333,6 +1333,9 @@ def main() -> None:
             "metric": METRIC, "value": round(value, 2), "unit": "samples/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32",
+            "dtype_note": "fp32 storage, fp32 products, fp32 accumulation; the variant-4 conv kernels (k_*_x9) form each "
+                          "fp32 product exactly from a three-piece bf16 split on the bf16 MFMA (DESIGN 3.1; "
+                          "tests/test_gpu_split.py: single products bit-exact, error vs fp64 at the f32 MFMA's level)",
             "data": f"synthetic AVMNIST-shaped corpus of {args.corpus} samples resident in HBM (audio f32 [32,94] "
                     "log-normal-ish, image uint8 [28,28]); each step gathers a shuffled batch on device "
                     "(colormap LUT, 1/255, masks) into the step's inputs; random-init weights (seed 0)",
