@@ -1268,6 +1268,10 @@ def main() -> None:
               "traffic_source": traffic_src,
               "step_valid_tflops_per_gpu": round(step_tflops, 3),
               "step_frac_of_peak": round(step_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+              "which_is_which": "frac / achieved / r34_3x3: conv kernels' device time in a ONE-stream re-capture of "
+                                "the step (carried Adam and the audio LDS floor off, each kernel alone on the chip; "
+                                "reads ~2 % above a rocprofv3 recompute of the same schedule, r*_roofline_from_trace"
+                                ".txt); step_frac_of_peak: valid FLOPs of the TIMED two-stream step / ms_per_step",
               "timing": f"device kernel durations (torch.profiler: the rocprofiler timestamps) of {R} replays of the "
                         "step captured on ONE stream after the timed region (each kernel alone on the chip, as "
                         "under rocprofv3 kernel tracing); conv_ms_per_step = summed conv-kernel durations per step; "
