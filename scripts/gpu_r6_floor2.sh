@@ -5,5 +5,4 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 T=${1:-r6fl}
 P=task-specific-pretraining-multimodal_amd
-timeout -k 10 500 python -u scripts/ab_lib.py --rounds 4 --a $P/libtspm.so --b $P/libtspm.so --env-b TSPM_SLACK_LDS_FLOOR=0 -- --steps 200 --no-cpu-baseline --pcie-steps 0 --profile-steps 0 > gpurun_out/${T}_0.json 2> gpurun_out/${T}_0.err
-timeout -k 10 500 python -u scripts/ab_lib.py --rounds 4 --a $P/libtspm.so --b $P/libtspm.so --env-b TSPM_SLACK_LDS_FLOOR=54000 -- --steps 200 --no-cpu-baseline --pcie-steps 0 --profile-steps 0 > gpurun_out/${T}_54k.json 2> gpurun_out/${T}_54k.err
+timeout -k 10 500 python -u scripts/ab_lib.py --rounds 4 --a $P/libtspm.so --b $P/libtspm.so --env-b TSPM_SLACK_PARTS=f -- --steps 200 --no-cpu-baseline --pcie-steps 0 --profile-steps 0 > gpurun_out/${T}_f.json 2> gpurun_out/${T}_f.err
