@@ -21,7 +21,15 @@ from tspm_amd import _lib as L  # noqa: E402
 from tune_convs import LDS_SPLITS, LDS_TILES, LDS_WAVES, graph_time  # noqa: E402
 
 
-def candidates(s):
+def candidates(s, variants=(1,)):
+    for v in variants:
+        for a in _candidates_v1(s):
+            if v == 4 and a[3] > 2:  # variant 4 (bf16-piece products): wk <= 2
+                continue
+            yield a[:5] + (v,)
+
+
+def _candidates_v1(s):
     for tm, tn in LDS_TILES:
         for wn, wk in LDS_WAVES:
             wm = 4 // (wn * wk)
@@ -45,7 +53,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variants", default="1", help="LDS variants searched: 1 (default) and / or 4 (round 6)")
     args = ap.parse_args()
+    variants = tuple(int(v) for v in args.variants.split(","))
     dev = torch.device("cuda", 0)
     lib = L.lib()
     B, T, F, C = args.batch, args.steps, args.feat, args.channels
@@ -77,7 +87,7 @@ def main():
         scale = float(ref.abs().max())
         t_base = graph_time(lambda: make(base), args.reps, args.iters)
         best = (t_base, base)
-        for algo in candidates(s):
+        for algo in candidates(s, variants):
             y.fill_(float("nan"))
             if make(algo)() != 0:
                 continue
