@@ -100,6 +100,7 @@ SHAPES = [
     (128, 512, 1, 1, 512, 3, 3, 1, 1),
     (128, 256, 2, 6, 512, 3, 3, 2, 1),
     (128, 256, 2, 6, 512, 1, 1, 2, 0),
+    (256, 768, 50, 1, 128, 5, 1, 1, 0),  # the MOSEI TextCNN's h = 5 conv (variant 4 in its batch-256 table)
 ]
 
 
