@@ -50,7 +50,8 @@ def distinct_ops(batch, dev):
             s = op.shape
             key = (s.n, s.h, s.w, s.c, s.k, s.r, s.s, s.stride, s.pad)
             if op is eng.stem:
-                xs = L.Strides4(h * w, w, 1, 0) if three_d else L.Strides4(h * w, h * w, w, 1)
+                # (sn, sh, sw, sc) of the reference NCHW input, as EncoderEngine.input_strides: [N,H,W] audio, [N,1,H,W] image
+                xs = L.Strides4(h * w, w, 1, 0) if three_d else L.Strides4(h * w, w, 1, h * w)
                 kinds = ("fwd", "wgrad")
             else:
                 xs = L.hwnc_strides(s.n, s.h, s.w, s.c)
