@@ -151,10 +151,14 @@ def test_bn_apply_maxpool_equals_apply_then_maxpool(gpu, n, h, w, c, ev):
 def test_pool_fusions_leave_the_step_bitwise_unchanged(gpu, monkeypatch):
     """Four graph-replayed AVMNIST steps with the pooling fusions (TSPM_BN_POOL_SRC / TSPM_STEM_FUSE, the
     defaults) give bitwise the parameters, BN buffers and Adam moments of the step with the separate pooling
-    launches."""
+    launches.  The stem BN's partial sums formed in layer1's first dgrad epilogue (round 6, TSPM_BN_DGRAD_PART_STEM:
+    a different summation order, held to fp64 per tile in tests/test_gpu_bn_dgrad_part.py) exist only with the pooling
+    fold, so they are switched off in both runs: the comparison is of the pooling fusions alone.  (At batch 32 they
+    became reachable once the batch-32 table put LDS-staged kernels on that dgrad, round 6.)"""
     import tspm_amd
     from oracle import avmnist_ref as orc
     results = []
+    monkeypatch.setenv("TSPM_BN_DGRAD_PART_STEM", "0")
     for on in ("1", "0"):
         monkeypatch.setenv("TSPM_BN_POOL_SRC", on)
         monkeypatch.setenv("TSPM_STEM_FUSE", on)
